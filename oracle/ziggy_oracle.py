@@ -1,0 +1,208 @@
+"""CPU ORACLE for the HIP-GP structured-kernel PCG hot path — TEST INFRASTRUCTURE ONLY.
+
+This module restates, in NumPy/SciPy, the reference algorithm of `suyashk12/hipgp`
+(package `ziggy`, snapshot mounted at /root/reference).  It is the checker that the HIP
+path is compared against; it is imported only by `tests/`, `__graft_entry__.smoke()` and
+`bench.py`'s `cpu_baseline` leg.  The product path (`hipgp_amd`, `ziggy`) never imports it.
+
+Parity pinning: every function below is checked against golden vectors produced by running
+the reference itself (tests/golden/make_golden.py -> tests/golden/*.npz) in
+tests/test_oracle.py.  FFT boundary: the reference calls torch-1.4 `torch.fft/ifft`
+(unnormalised forward / 1/N inverse C2C); here `scipy.fft.fftn/ifftn` with the same
+definition, computed in the input precision (complex64 for fp32, complex128 for fp64).
+"""
+import numpy as np
+import scipy.fft as sfft
+
+_WORKERS = -1   # all host cores for scipy.fft (bench cpu_baseline states the core count)
+
+
+def set_workers(n):
+    global _WORKERS
+    _WORKERS = n
+
+
+# --------------------------------------------------------------------------------------
+# kernels (ziggy/kernels.py)
+# --------------------------------------------------------------------------------------
+def kernel_eval(kind, x, y, params, nu=None):
+    """Stationary kernel k(x, y) for x:(N,D), y:(M,D) -> (N,M).
+    SqExp: `kernels.py:73-79`; Matern nu in {.5,1.5,2.5}: `kernels.py:145-158`."""
+    sig2, ell = params
+    x = np.asarray(x)
+    y = np.asarray(y)
+    if kind == "sqexp":
+        sq = np.sum(((x[:, None, :] - y[None, :, :]) / ell) ** 2, axis=-1)
+        return sig2 * np.exp(-sq / 2)
+    if kind == "matern":
+        sq = np.sum((x[:, None, :] - y[None, :, :]) ** 2, axis=-1)
+        if nu == .5:
+            k = np.exp(-np.sqrt(sq) / ell)
+        elif nu == 1.5:
+            dp = np.sqrt(3) * np.sqrt(sq) / ell
+            k = (1 + dp) * np.exp(-dp)
+        elif nu == 2.5:
+            dp = np.sqrt(5) * np.sqrt(sq) / ell
+            k = (1 + dp + (5. / 3.) * sq / (ell ** 2)) * np.exp(-dp)
+        else:
+            raise ValueError(nu)
+        return (sig2 * k).astype(x.dtype)
+    raise ValueError(kind)
+
+
+def grid_points(grids):
+    """C-order meshgrid(indexing='ij') points, last axis fastest (`hipgp.py:63-64`)."""
+    mesh = np.meshgrid(*grids, indexing="ij")
+    return np.stack([g.reshape(-1) for g in mesh], axis=-1)
+
+
+# --------------------------------------------------------------------------------------
+# ToeplitzTensor (ziggy/misc/toeplitz_tensor.py)
+# --------------------------------------------------------------------------------------
+def toeplitz_column(grids, kfun, jitter):
+    """`toeplitz_tensor.py:127-133`: first row k(x0, x_j), nugget on c0 (absent in
+    `toeplitz_expanded.py:242-250`, i.e. jitter=0)."""
+    xs = grid_points(grids)
+    row = np.array(kfun(xs[0][None, :], xs))[0].copy()
+    row[0] += jitter
+    return row
+
+
+def expanded_dims(dims):
+    """n_i = 2 m_i - 2 (m_i > 1) else m_i  (`hipgp.py:72`)."""
+    return tuple(2 * m - 2 if m > 1 else m for m in dims)
+
+
+def circulant_embed(K):
+    """`toeplitz_tensor.py:135-143`: per dim cat([K, flip(K)[1:-1]])."""
+    for d in range(K.ndim):
+        rev = np.flip(K, axis=d)
+        idx = [slice(None)] * d + [slice(1, -1)]
+        K = np.concatenate([K, rev[tuple(idx)]], axis=d)
+    return K
+
+
+def _cdtype(dt):
+    return np.complex64 if np.dtype(dt) == np.float32 else np.complex128
+
+
+class ToeplitzOracle:
+    """Restatement of `ToeplitzTensor.__init__` (`toeplitz_tensor.py:9-45`) and its ops."""
+
+    def __init__(self, column, dims, clamp_min=1e-6):
+        self.dims = tuple(int(m) for m in dims)
+        self.ndim = len(self.dims)
+        self.M = int(np.prod(self.dims))
+        self.dtype = np.asarray(column).dtype
+        self.column = np.asarray(column)
+        self.C = circulant_embed(self.column.reshape(self.dims))
+        self.ndims = self.C.shape
+        self.Mp = int(np.prod(self.ndims))
+        F = sfft.fftn(self.C.astype(_cdtype(self.dtype)), workers=_WORKERS)
+        # D = clamp(Re FFT(C), 1e-6); imag discarded (`toeplitz_tensor.py:25-31`)
+        self.D = np.maximum(F.real, self.dtype.type(clamp_min)).astype(self.dtype)
+        self.D_sqrt = np.sqrt(self.D)
+        self.Di = (1. / self.D).astype(self.dtype)
+
+    def _apply(self, spec, x_full):
+        ax = tuple(range(1, self.ndim + 1))
+        Fv = sfft.fftn(x_full, axes=ax, workers=_WORKERS)
+        return sfft.ifftn(Fv * spec[None], axes=ax, workers=_WORKERS)
+
+    def _pad(self, v):
+        B = v.shape[0]
+        c = np.zeros((B,) + self.ndims, dtype=_cdtype(self.dtype))
+        c[(slice(None),) + tuple(slice(0, m) for m in self.dims)] = v.reshape((B,) + self.dims)
+        return c
+
+    def _crop(self, c):
+        B = c.shape[0]
+        return np.ascontiguousarray(
+            c[(slice(None),) + tuple(slice(0, m) for m in self.dims)].real).reshape(B, -1)
+
+    def matmul_K(self, v):           # `toeplitz_tensor.py:70-83`
+        return self._crop(self._apply(self.D, self._pad(v))).astype(self.dtype)
+
+    def matmul_Cinv(self, v):        # `toeplitz_tensor.py:114-125`
+        return self._crop(self._apply(self.Di, self._pad(v))).astype(self.dtype)
+
+    def matmul_RT(self, v):          # `toeplitz_tensor.py:85-97` (full expanded grid, no crop)
+        B = v.shape[0]
+        return self._apply(self.D_sqrt, self._pad(v)).real.reshape(B, -1).astype(self.dtype)
+
+    def matmul_R(self, w):           # `toeplitz_tensor.py:99-112`
+        B = w.shape[0]
+        c = w.reshape((B,) + self.ndims).astype(_cdtype(self.dtype))
+        return self._crop(self._apply(self.D_sqrt, c)).astype(self.dtype)
+
+    def solve(self, b, do_precond=True, maxiter=100, tol=1e-8, callback=None):
+        """`ToeplitzTensor._solve` (`toeplitz_tensor.py:54-68`)."""
+        P = self.matmul_Cinv if do_precond else None
+        return conj_grad2(self.matmul_K, b, precond=P, maxiter=maxiter, tol=tol,
+                          callback=callback)
+
+
+# --------------------------------------------------------------------------------------
+# CG (ziggy/misc/cg.py)
+# --------------------------------------------------------------------------------------
+def conj_grad2(A_mul, b, precond=None, maxiter=20, tol=1e-10, callback=None, info=None):
+    """Row layout (bsz, M), per-RHS alpha/beta (`cg.py:44-80`): x0=0, r=b-A0, break when
+    ALL sqrt(r.r) < tol (after the x/r update), callback after the p update."""
+    if precond is None:
+        precond = lambda x: x
+    x = np.zeros_like(b)
+    r = b - A_mul(x)
+    z = precond(r)
+    p = z
+    n_done = 0
+    with np.errstate(invalid="ignore", divide="ignore"):
+        for n in range(maxiter):
+            rs = np.sum(r * z, axis=1)
+            Ap = A_mul(p)
+            alpha = rs / np.sum(p * Ap, axis=1)
+            x = x + alpha[:, None] * p
+            r = r - alpha[:, None] * Ap
+            rnew = np.sum(r * r, axis=1)
+            n_done = n + 1
+            if np.all(np.sqrt(rnew) < tol):
+                break
+            z = precond(r)
+            beta = np.sum(z * r, axis=1) / rs
+            p = z + beta[:, None] * p
+            if callback is not None:
+                callback(n, x)
+    if info is not None:
+        info["iters"] = n_done
+    return x
+
+
+def conj_grad(A_mul, b, precond=None, maxiter=20, tol=1e-10, callback=None, info=None):
+    """Column layout (M, L), dim=0 dots (`cg.py:5-41`)."""
+    At = lambda y: A_mul(y.T).T
+    Pt = None if precond is None else (lambda y: precond(y.T).T)
+    cb = None if callback is None else (lambda n, x: callback(n, x.T))
+    return conj_grad2(At, b.T, precond=Pt, maxiter=maxiter, tol=tol, callback=cb,
+                      info=info).T
+
+
+# --------------------------------------------------------------------------------------
+# gram_solve (ziggy/misc/toeplitz_expanded.py) and compute_kn (ziggy/hipgp.py)
+# --------------------------------------------------------------------------------------
+def gram_solve(grids, kfun, vec, maxiter=20, do_precond=True, tol=1e-10, callback=None,
+               mult_RT=True, info=None):
+    """`toeplitz_expanded.py:17-58`: ToeplitzMatmul has NO jitter (`:248`)."""
+    dims = tuple(len(g) for g in grids)
+    T = ToeplitzOracle(toeplitz_column(grids, kfun, 0.0).astype(vec.dtype), dims)
+    Kmul = lambda x: T.matmul_K(x.T).T
+    P = (lambda x: T.matmul_Cinv(x.T).T) if do_precond else None
+    d = conj_grad(Kmul, vec.T, precond=P, maxiter=maxiter, tol=tol, callback=callback,
+                  info=info)
+    if mult_RT:
+        return T.matmul_RT(d.T)
+    return d.T
+
+
+def compute_kn(T, Knm, maxiter_cg=10, tol=1e-8):
+    """`hipgp.py:117-146` (ziggy whitening): kn = R^T K^{-1} Knm^T."""
+    d0 = T.solve(Knm, do_precond=True, maxiter=maxiter_cg, tol=tol)
+    return T.matmul_RT(d0)
