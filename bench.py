@@ -1,0 +1,237 @@
+"""Benchmark: Toeplitz-FFT Kuu matvecs/sec + PCG wall-clock at M = 1M inducing points.
+
+Workload (BASELINE.json configs[1]): 2-D 1024x1024 grid on [-1,1]^2,
+SqExp(sig2=1, ell=0.01), jitter 1e-3, fp32, B = 32 right-hand sides per GPU = rows of Knm for
+32 synthetic observations x ~ U(-1,1)^2 (seeded per rank).
+
+  step          = one batched Kuu matvec over the rank's 32 RHS (hgp_toeplitz_apply, op K)
+  value         = RHS-matvecs/s over all ranks (weak scaling: each rank owns 32 RHS)
+  pcg_*         = compute_kn wall-clock (hipgp.py:117-146): spectrum setup + PCG(maxiter 20,
+                  tol 1e-8, C^-1 preconditioner) + R^T, for the same 32 RHS
+  roofline      = HBM roofline of the batched K matvec (3 pass kernels back to back) with
+                  SURVEY §8(d)'s algorithmic bytes B_K = 8M + 32*m1*h2 per RHS
+  cpu_baseline  = the NumPy/SciPy oracle (scipy.fft, all worker threads given) on a bounded
+                  sample of the same workload, rank 0 at N=1 only
+
+Multi-GPU: one process per GPU (torchrun); RHS are sharded (each rank its own 32), no
+collective inside the timed region apart from the barriers; max-over-ranks timing.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--m", type=int, default=1024, help="grid points per axis (2-D)")
+    ap.add_argument("--rhs", type=int, default=32)
+    ap.add_argument("--pcg-reps", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    return ap.parse_args()
+
+
+def make_problem(m, B, device, seed):
+    import ziggy.kernels as zk
+    k = zk.SqExp(dtype=torch.float32)
+    params = (1.0, 0.01)
+    kf = lambda x, y: k.forward(x, y, params=params)
+    grids = [torch.linspace(-1, 1, m, device=device, dtype=torch.float32) for _ in range(2)]
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    xobs = (torch.rand(B, 2, generator=g, dtype=torch.float32) * 2 - 1).to(device)
+    xx = torch.meshgrid(*grids, indexing="ij")
+    xs = torch.stack([x.reshape(-1) for x in xx], dim=-1)
+    Knm = torch.cat([kf(xobs[i:i + 1], xs) for i in range(B)], dim=0).contiguous()   # (B, M)
+    return grids, kf, Knm
+
+
+def time_events(fn, reps, stream):
+    s = torch.cuda.Event(enable_timing=True)
+    e = torch.cuda.Event(enable_timing=True)
+    s.record(stream)
+    for _ in range(reps):
+        fn()
+    e.record(stream)
+    e.synchronize()
+    return s.elapsed_time(e) / reps
+
+
+def cpu_baseline(m, B, threads, grids_np, seed):
+    """Oracle (scipy.fft) K matvecs on a bounded sample + one RHS of the PCG solve."""
+    from oracle import ziggy_oracle as zo
+    zo.set_workers(threads)
+    kf = lambda x, y: zo.kernel_eval("sqexp", x, y, (1.0, 0.01))
+    col = zo.toeplitz_column(grids_np, kf, 1e-3).astype(np.float32)
+    T = zo.ToeplitzOracle(col, (m, m))
+    rs = np.random.RandomState(seed)
+    nb = 4
+    v = rs.randn(nb, m * m).astype(np.float32)
+    T.matmul_K(v[:1])                       # warm the FFT plans
+    t0 = time.perf_counter()
+    reps = 0
+    while True:
+        T.matmul_K(v)
+        reps += 1
+        if time.perf_counter() - t0 > 8.0 or reps >= 20:
+            break
+    dt = (time.perf_counter() - t0) / reps
+    mv_s = nb / dt
+    t0 = time.perf_counter()
+    xs = T.solve(v[:1], do_precond=True, maxiter=20, tol=1e-8)
+    T.matmul_RT(xs)
+    pcg1 = time.perf_counter() - t0
+    return {"value": mv_s, "unit": "RHS-matvecs/s", "cores": threads, "kind": "port",
+            "sample": f"oracle K matvec on {nb} RHS x {reps} reps (scipy.fft, {threads} workers); "
+                      f"PCG(20)+R^T on 1 RHS = {pcg1:.2f} s -> extrapolated {pcg1 * B:.1f} s for B={B}",
+            "pcg_1rhs_s": pcg1, "pcg_extrapolated_s": pcg1 * B}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        import torch.distributed as tdist
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local if dist else 0)
+    torch.cuda.set_device(device)
+
+    from hipgp_amd import _lib
+    from hipgp_amd.plan import ToeplitzPlan
+    from ziggy.misc.toeplitz_tensor import ToeplitzTensor
+
+    m, B = args.m, args.rhs
+    M = m * m
+    grids, kf, Knm = make_problem(m, B, device, seed=1234 + rank)
+    stream = torch.cuda.current_stream(device)
+
+    # ---- plan + spectrum, then the timed K matvec steps --------------------------------------
+    T = ToeplitzTensor(grids, kf, batch_shape=(B,), jitter_val=1e-3)
+    plan = T._plan
+    y = torch.empty_like(Knm)
+    step = lambda: plan.apply(_lib.OP_K, Knm, out=y)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        tdist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        tdist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if dist:
+        tt = torch.tensor([dt], device=device, dtype=torch.float64)
+        tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
+        dt = float(tt.item())
+    ms_per_step = dt / args.steps * 1e3
+    value = world * B * args.steps / dt
+
+    # ---- per-kernel event timing of the K matvec (same stream as the launches) ---------------
+    op_ms = time_events(step, 10, stream)
+    npass = _lib.lib().hgp_op_pass_count(plan._h)
+    pass_ms = []
+    for pidx in range(npass):
+        fn = lambda: _lib.check(_lib.lib().hgp_toeplitz_apply_pass(
+            plan._h, _lib.OP_K, Knm.data_ptr(), y.data_ptr(), B, pidx))
+        fn()
+        pass_ms.append(time_events(fn, 10, stream))
+    h2 = m                                                   # n2/2 + 1 = m2
+    bytes_K_rhs = 8 * M + 32 * m * h2                        # SURVEY §8(d) B_K (d=2), fp32
+    achieved = B * bytes_K_rhs / (op_ms * 1e-3) / 1e9
+    L = plan.L_K
+    pair_int = m * L[1] * 8                                  # complex intermediate per RHS pair
+    Q = (B + 1) // 2
+    pass_bytes = [Q * (2 * M * 4 + pair_int), Q * 2 * pair_int + L[0] * L[1] * 4, Q * (pair_int + 2 * M * 4)]
+    kernels = [{"pass": i, "ms": round(pass_ms[i], 4),
+                "gbs": round(pass_bytes[i] / (pass_ms[i] * 1e-3) / 1e9, 1)} for i in range(npass)]
+
+    # ---- PCG wall-clock: compute_kn = setup + PCG(20) + R^T -----------------------------------
+    def compute_kn():
+        Tk = ToeplitzTensor(grids, kf, batch_shape=None, jitter_val=1e-3)
+        d0 = Tk.inv_matmul(Knm, do_precond=True, maxiter=20, tol=1e-8)
+        return Tk._matmul_by_RT(d0)
+
+    compute_kn()
+    torch.cuda.synchronize()
+    pcg_times = []
+    for _ in range(args.pcg_reps):
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        kn = compute_kn()
+        torch.cuda.synchronize()
+        pcg_times.append(time.perf_counter() - t1)
+    del kn
+    # split: setup alone, and the PCG+R^T alone with a prebuilt plan
+    t1 = time.perf_counter()
+    Tk = ToeplitzTensor(grids, kf, batch_shape=None, jitter_val=1e-3)
+    torch.cuda.synchronize()
+    setup_s = time.perf_counter() - t1
+    t1 = time.perf_counter()
+    d0 = Tk.inv_matmul(Knm, do_precond=True, maxiter=20, tol=1e-8)
+    Tk._matmul_by_RT(d0)
+    torch.cuda.synchronize()
+    solve_s = time.perf_counter() - t1
+    pcg_ms = float(np.median(pcg_times) * 1e3)
+    if dist:
+        tt = torch.tensor([pcg_ms], device=device, dtype=torch.float64)
+        tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
+        pcg_ms = float(tt.item())
+
+    out = {
+        "metric": "Toeplitz-FFT Kuu matvecs/sec + PCG wall-clock at M=1M inducing",
+        "value": value,
+        "unit": "RHS-matvecs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (Knm rows of seeded uniform observations; random-free kernel grid)",
+        "config": {"workload": f"C2: 2-D {m}x{m} SqExp(1,0.01) jitter 1e-3, batched K matvec, "
+                               f"{B} RHS per GPU", "M": M, "rhs_per_gpu": B, "global_rhs": B * world,
+                   "parallelism": f"rhs-shard x{world}"},
+        "pcg_wall_clock_ms": pcg_ms,
+        "pcg": {"what": "compute_kn: setup + PCG(maxiter=20, tol=1e-8, precond) + R^T, B RHS",
+                "median_ms": pcg_ms, "setup_ms": setup_s * 1e3, "pcg_plus_rt_ms": solve_s * 1e3},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "batched K matvec = 3 pass kernels (FWD rows, CONV cols, INV rows)",
+                     "op_ms": op_ms, "bytes_per_launch": B * bytes_K_rhs, "passes": kernels},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        grids_np = [np.linspace(-1, 1, m, dtype=np.float32) for _ in range(2)]
+        out["cpu_baseline"] = cpu_baseline(m, B, args.cpu_threads, grids_np, seed=7)
+        out["cpu_baseline"]["speedup_matvec"] = value / out["cpu_baseline"]["value"]
+        out["cpu_baseline"]["speedup_pcg"] = out["cpu_baseline"]["pcg_extrapolated_s"] * 1e3 / pcg_ms
+    if rank == 0:
+        print(json.dumps(out))
+    if dist:
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

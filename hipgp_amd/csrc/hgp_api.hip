@@ -1,0 +1,696 @@
+// hgp_api.hip — plan object and the extern "C" ABI of libhipgp.so (see include/hipgp.h).
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/hipgp.h"
+#include "hgp_internal.hpp"
+
+using namespace hgp;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                              \
+  do {                                                                                             \
+    hipError_t _e = (expr);                                                                        \
+    if (_e != hipSuccess)                                                                          \
+      return fail(HGP_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));                   \
+  } while (0)
+
+#define HGP_TRY(expr)                                                                              \
+  do {                                                                                             \
+    int _rc = (expr);                                                                              \
+    if (_rc != 0) return _rc;                                                                      \
+  } while (0)
+
+int64_t next_pow2(int64_t v) {
+  int64_t p = 1;
+  while (p < v) p <<= 1;
+  return p;
+}
+
+struct DevBuf {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+  int ensure(size_t need) {
+    if (need <= bytes) return 0;
+    if (ptr) (void)hipFree(ptr);
+    ptr = nullptr;
+    bytes = 0;
+    hipError_t e = hipMalloc(&ptr, need);
+    if (e != hipSuccess) return fail(HGP_E_OOM, std::string("hipMalloc(") + std::to_string(need) + "): " + hipGetErrorString(e));
+    bytes = need;
+    return 0;
+  }
+  void release() {
+    if (ptr) (void)hipFree(ptr);
+    ptr = nullptr;
+    bytes = 0;
+  }
+};
+
+}  // namespace
+
+struct hgp_plan {
+  int device = 0;
+  int dtype = HGP_F32;
+  hipStream_t stream = nullptr;
+  int d = 0;                              // effective dims (axes with m > 1)
+  int ndim_user = 0;
+  int64_t m[3] = {1, 1, 1}, n[3] = {1, 1, 1}, LK[3] = {1, 1, 1}, LR[3] = {1, 1, 1};
+  int64_t M = 1, Mp = 1, prodLK = 1, prodLR = 1;
+  size_t esz = 4;
+  // tables
+  DevBuf twK[3], twR[3], tw64K[3], tw64R[3], Wdct[3];
+  // spectra
+  DevBuf specK, specI, specR, Dm3;
+  bool have_spec = false;
+  DevBuf nclamp;
+  // scratch
+  DevBuf ws1, ws2, set1, set2, setM1, setM2;
+  // CG state
+  DevBuf r, z, p, Ap, part_op, part_u, scal, flags, bT, xT;
+  int64_t cg_nrhs = 0;
+  int cg_precond = 0, cg_layout = 0;
+  void* cg_x_user = nullptr;
+  void* cg_x = nullptr;
+  bool cg_active = false;
+  int64_t ws_budget = (int64_t)1 << 30;
+
+  ~hgp_plan() {
+    for (int a = 0; a < 3; ++a) { twK[a].release(); twR[a].release(); tw64K[a].release(); tw64R[a].release(); Wdct[a].release(); }
+    DevBuf* bufs[] = {&specK, &specI, &specR, &Dm3, &nclamp, &ws1, &ws2, &set1, &set2, &setM1, &setM2,
+                      &r, &z, &p, &Ap, &part_op, &part_u, &scal, &flags, &bT, &xT};
+    for (DevBuf* b : bufs) b->release();
+  }
+};
+
+namespace {
+
+// op geometry: per-axis input/output lengths and transform length
+struct OpGeom {
+  int64_t in[3], out[3], L[3];
+  int64_t in_M, out_M;
+  const DevBuf* tw;        // per-axis twiddle tables (plan dtype)
+  const void* spec;
+  int spec_kind;
+};
+
+OpGeom op_geom(const hgp_plan* P, int op) {
+  OpGeom g;
+  for (int a = 0; a < 3; ++a) { g.in[a] = 1; g.out[a] = 1; g.L[a] = 1; }
+  g.in_M = g.out_M = 1;
+  for (int a = 0; a < P->d; ++a) {
+    const bool rtype = (op == HGP_OP_RT || op == HGP_OP_R);
+    g.L[a] = rtype ? P->LR[a] : P->LK[a];
+    g.in[a] = (op == HGP_OP_R) ? P->n[a] : P->m[a];
+    g.out[a] = (op == HGP_OP_RT) ? P->n[a] : P->m[a];
+    g.in_M *= g.in[a];
+    g.out_M *= g.out[a];
+  }
+  g.tw = (op == HGP_OP_RT || op == HGP_OP_R) ? P->twR : P->twK;
+  if (op == HGP_OP_K) { g.spec = P->specK.ptr; g.spec_kind = SPEC_REAL; }
+  else if (op == HGP_OP_CINV) { g.spec = P->specI.ptr; g.spec_kind = SPEC_REAL; }
+  else if (op == HGP_OP_RT) { g.spec = P->specR.ptr; g.spec_kind = SPEC_CPLX; }
+  else { g.spec = P->specR.ptr; g.spec_kind = SPEC_CPLX_CONJ; }
+  return g;
+}
+
+template <typename T>
+int launch(int H, int mode, int lay, const PassDesc& d, int64_t lines_contig, hipStream_t s) {
+  const PassGeom g = pass_geom<T>(H, lay);
+  if (g.C == 0) return fail(HGP_E_UNSUPPORTED, "transform half-length " + std::to_string(H) + " not supported");
+  int64_t nb;
+  if (lay == LAY_STRIDED) nb = (int64_t)d.Q * d.Rn * ((d.In + g.C - 1) / g.C);
+  else nb = (lines_contig + g.C - 1) / g.C;
+  if (nb <= 0) return 0;
+  if (nb > 0x7fffffff) return fail(HGP_E_UNSUPPORTED, "grid too large");
+  hipError_t e = launch_pass<T>(H, mode, lay, d, nb, s);
+  if (e != hipSuccess) return fail(HGP_E_HIP, std::string("k_pass launch: ") + hipGetErrorString(e));
+  return 0;
+}
+
+PassDesc base_desc() {
+  PassDesc d;
+  std::memset(&d, 0, sizeof(d));
+  return d;
+}
+
+// y = op(x) on RHS [0, nrhs); optional fused dot with `dotv` into partial[b][Rn_last].
+template <typename T>
+int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void* dotv, void* partial,
+           const int* done, int only_pass = -1) {
+  const OpGeom g = op_geom(P, op);
+  const int d = P->d;
+  const int64_t Q = (nrhs + 1) / 2;
+  const size_t cs = sizeof(C2<T>);
+  // per-pair workspace (complex elements)
+  int64_t B1 = 0, B2 = 0;
+  if (d == 2) B1 = std::max(g.in[0], g.out[0]) * g.L[1];
+  if (d == 3) {
+    B1 = std::max(g.in[0] * g.in[1], g.out[0] * g.out[1]) * g.L[2];
+    B2 = std::max(g.in[0], g.out[0]) * g.L[1] * g.L[2];
+  }
+  int64_t Qc = Q;
+  if (B1 + B2 > 0) {
+    const int64_t per = (B1 + B2) * (int64_t)cs;
+    Qc = std::max<int64_t>(1, std::min<int64_t>(Q, P->ws_budget / per));
+    HGP_TRY(P->ws1.ensure((size_t)(B1 * Qc) * cs));
+    if (B2) HGP_TRY(P->ws2.ensure((size_t)(B2 * Qc) * cs));
+  }
+  const T* xin = reinterpret_cast<const T*>(x);
+  T* yout = reinterpret_cast<T*>(y);
+  const T* dv = reinterpret_cast<const T*>(dotv);
+  T* part = reinterpret_cast<T*>(partial);
+  int64_t rn_last = (d == 1) ? 1 : (d == 2 ? g.out[0] : g.out[0] * g.out[1]);
+
+  for (int64_t q0 = 0; q0 < Q; q0 += Qc) {
+    int pass_no = 0;
+    const int64_t qn = std::min(Qc, Q - q0);
+    const int nr = (int)std::min<int64_t>(nrhs - 2 * q0, 2 * qn);
+    const T* xi = xin + 2 * q0 * g.in_M;
+    T* yo = yout + 2 * q0 * g.out_M;
+    const T* dvc = dv ? dv + 2 * q0 * g.out_M : nullptr;
+    T* pc = part ? part + 2 * q0 * rn_last : nullptr;
+
+    if (d == 1) {
+      PassDesc D = base_desc();
+      D.in = View{(void*)xi, g.in_M, 0, 1, (int)g.in[0]};
+      D.out = View{yo, g.out_M, 0, 1, (int)g.out[0]};
+      D.dot = dvc; D.partial = pc;
+      D.spec = g.spec; D.spec_kind = g.spec_kind; D.spec_i = 0; D.spec_r = 0; D.spec_p = 1;
+      D.tw = g.tw[0].ptr; D.nrhs = nr; D.Q = (int)qn; D.Rn = 1; D.In = 1; D.done = done;
+      if (only_pass < 0 || only_pass == pass_no) HGP_TRY(launch<T>((int)(g.L[0] / 2), PASS_CONV, LAY_RP, D, qn, P->stream));
+      ++pass_no;
+    } else if (d == 2) {
+      C2<T>* w1 = reinterpret_cast<C2<T>*>(P->ws1.ptr);
+      // A: FWD along axis 1 (rows of the real pair) -> w1 [q][i0][k1]
+      PassDesc A = base_desc();
+      A.in = View{(void*)xi, g.in_M, g.in[1], 1, (int)g.in[1]};
+      A.out = View{w1, B1, g.L[1], 1, (int)g.L[1]};
+      A.tw = g.tw[1].ptr; A.nrhs = nr; A.Q = (int)qn; A.Rn = (int)g.in[0]; A.In = 1; A.done = done;
+      if (only_pass < 0 || only_pass == pass_no) HGP_TRY(launch<T>((int)(g.L[1] / 2), PASS_FWD, LAY_RP, A, qn * g.in[0], P->stream));
+      ++pass_no;
+      // B: CONV along axis 0 (strided columns), in place
+      PassDesc Bd = base_desc();
+      Bd.in = View{w1, B1, 0, g.L[1], (int)g.in[0]};
+      Bd.out = View{w1, B1, 0, g.L[1], (int)g.out[0]};
+      Bd.spec = g.spec; Bd.spec_kind = g.spec_kind; Bd.spec_i = 1; Bd.spec_p = g.L[1]; Bd.spec_r = 0;
+      Bd.tw = g.tw[0].ptr; Bd.nrhs = nr; Bd.Q = (int)qn; Bd.Rn = 1; Bd.In = (int)g.L[1]; Bd.done = done;
+      if (only_pass < 0 || only_pass == pass_no) HGP_TRY(launch<T>((int)(g.L[0] / 2), PASS_CONV, LAY_STRIDED, Bd, 0, P->stream));
+      ++pass_no;
+      // C: INV along axis 1 -> real pair rows, crop, fused dot
+      PassDesc Cd = base_desc();
+      Cd.in = View{w1, B1, g.L[1], 1, (int)g.L[1]};
+      Cd.out = View{yo, g.out_M, g.out[1], 1, (int)g.out[1]};
+      Cd.dot = dvc; Cd.partial = pc;
+      Cd.tw = g.tw[1].ptr; Cd.nrhs = nr; Cd.Q = (int)qn; Cd.Rn = (int)g.out[0]; Cd.In = 1; Cd.done = done;
+      if (only_pass < 0 || only_pass == pass_no) HGP_TRY(launch<T>((int)(g.L[1] / 2), PASS_INV, LAY_RP, Cd, qn * g.out[0], P->stream));
+      ++pass_no;
+    } else {
+      C2<T>* w1 = reinterpret_cast<C2<T>*>(P->ws1.ptr);
+      C2<T>* w2 = reinterpret_cast<C2<T>*>(P->ws2.ptr);
+      const int64_t L1 = g.L[1], L2 = g.L[2];
+      // P1: FWD axis 2: real pair rows (i0,i1) -> w1 [q][i0][i1][k2]
+      PassDesc P1 = base_desc();
+      P1.in = View{(void*)xi, g.in_M, g.in[2], 1, (int)g.in[2]};
+      P1.out = View{w1, B1, L2, 1, (int)L2};
+      P1.tw = g.tw[2].ptr; P1.nrhs = nr; P1.Q = (int)qn; P1.Rn = (int)(g.in[0] * g.in[1]); P1.In = 1; P1.done = done;
+      if (only_pass < 0 || only_pass == pass_no) HGP_TRY(launch<T>((int)(L2 / 2), PASS_FWD, LAY_RP, P1, qn * g.in[0] * g.in[1], P->stream));
+      ++pass_no;
+      // P2: FWD axis 1 (strided): lines (i0, k2) -> w2 [q][i0][k1][k2]
+      PassDesc P2 = base_desc();
+      P2.in = View{w1, B1, g.in[1] * L2, L2, (int)g.in[1]};
+      P2.out = View{w2, B2, L1 * L2, L2, (int)L1};
+      P2.tw = g.tw[1].ptr; P2.nrhs = nr; P2.Q = (int)qn; P2.Rn = (int)g.in[0]; P2.In = (int)L2; P2.done = done;
+      if (only_pass < 0 || only_pass == pass_no) HGP_TRY(launch<T>((int)(L1 / 2), PASS_FWD, LAY_STRIDED, P2, 0, P->stream));
+      ++pass_no;
+      // P3: CONV axis 0 (strided, in place): lines (k1,k2)
+      PassDesc P3 = base_desc();
+      P3.in = View{w2, B2, 0, L1 * L2, (int)g.in[0]};
+      P3.out = View{w2, B2, 0, L1 * L2, (int)g.out[0]};
+      P3.spec = g.spec; P3.spec_kind = g.spec_kind; P3.spec_i = 1; P3.spec_p = L1 * L2; P3.spec_r = 0;
+      P3.tw = g.tw[0].ptr; P3.nrhs = nr; P3.Q = (int)qn; P3.Rn = 1; P3.In = (int)(L1 * L2); P3.done = done;
+      if (only_pass < 0 || only_pass == pass_no) HGP_TRY(launch<T>((int)(g.L[0] / 2), PASS_CONV, LAY_STRIDED, P3, 0, P->stream));
+      ++pass_no;
+      // P4: INV axis 1 (strided): lines (o0, k2) -> w1 [q][o0][o1][k2]
+      PassDesc P4 = base_desc();
+      P4.in = View{w2, B2, L1 * L2, L2, (int)L1};
+      P4.out = View{w1, B1, g.out[1] * L2, L2, (int)g.out[1]};
+      P4.tw = g.tw[1].ptr; P4.nrhs = nr; P4.Q = (int)qn; P4.Rn = (int)g.out[0]; P4.In = (int)L2; P4.done = done;
+      if (only_pass < 0 || only_pass == pass_no) HGP_TRY(launch<T>((int)(L1 / 2), PASS_INV, LAY_STRIDED, P4, 0, P->stream));
+      ++pass_no;
+      // P5: INV axis 2: rows (o0,o1) -> real pair, crop, fused dot
+      PassDesc P5 = base_desc();
+      P5.in = View{w1, B1, L2, 1, (int)L2};
+      P5.out = View{yo, g.out_M, g.out[2], 1, (int)g.out[2]};
+      P5.dot = dvc; P5.partial = pc;
+      P5.tw = g.tw[2].ptr; P5.nrhs = nr; P5.Q = (int)qn; P5.Rn = (int)(g.out[0] * g.out[1]); P5.In = 1; P5.done = done;
+      if (only_pass < 0 || only_pass == pass_no) HGP_TRY(launch<T>((int)(L2 / 2), PASS_INV, LAY_RP, P5, qn * g.out[0] * g.out[1], P->stream));
+      ++pass_no;
+    }
+  }
+  return 0;
+}
+
+// Forward FFT of a full (unpruned) fp64 complex L-grid: a -> result pointer (a or b).
+int fwd_grid_f64(hgp_plan* P, const int64_t* L, const DevBuf* tw64, double2* a, double2* b, double2** result) {
+  const int d = P->d;
+  hipStream_t s = P->stream;
+  if (d == 1) {
+    PassDesc D = base_desc();
+    D.in = View{a, L[0], 0, 1, (int)L[0]};
+    D.out = View{b, L[0], 0, 1, (int)L[0]};
+    D.tw = tw64[0].ptr; D.Q = 1; D.Rn = 1; D.In = 1; D.nrhs = 2;
+    HGP_TRY(launch<double>((int)(L[0] / 2), PASS_FWD, LAY_CONTIG, D, 1, s));
+    *result = b;
+  } else if (d == 2) {
+    PassDesc A = base_desc();
+    A.in = View{a, 0, L[1], 1, (int)L[1]};
+    A.out = View{b, 0, L[1], 1, (int)L[1]};
+    A.tw = tw64[1].ptr; A.Q = 1; A.Rn = (int)L[0]; A.In = 1; A.nrhs = 2;
+    HGP_TRY(launch<double>((int)(L[1] / 2), PASS_FWD, LAY_CONTIG, A, L[0], s));
+    PassDesc Bd = base_desc();
+    Bd.in = View{b, 0, 0, L[1], (int)L[0]};
+    Bd.out = View{a, 0, 0, L[1], (int)L[0]};
+    Bd.tw = tw64[0].ptr; Bd.Q = 1; Bd.Rn = 1; Bd.In = (int)L[1]; Bd.nrhs = 2;
+    HGP_TRY(launch<double>((int)(L[0] / 2), PASS_FWD, LAY_STRIDED, Bd, 0, s));
+    *result = a;
+  } else {
+    PassDesc A = base_desc();
+    A.in = View{a, 0, L[2], 1, (int)L[2]};
+    A.out = View{b, 0, L[2], 1, (int)L[2]};
+    A.tw = tw64[2].ptr; A.Q = 1; A.Rn = (int)(L[0] * L[1]); A.In = 1; A.nrhs = 2;
+    HGP_TRY(launch<double>((int)(L[2] / 2), PASS_FWD, LAY_CONTIG, A, L[0] * L[1], s));
+    PassDesc Bd = base_desc();
+    Bd.in = View{b, 0, L[1] * L[2], L[2], (int)L[1]};
+    Bd.out = View{a, 0, L[1] * L[2], L[2], (int)L[1]};
+    Bd.tw = tw64[1].ptr; Bd.Q = 1; Bd.Rn = (int)L[0]; Bd.In = (int)L[2]; Bd.nrhs = 2;
+    HGP_TRY(launch<double>((int)(L[1] / 2), PASS_FWD, LAY_STRIDED, Bd, 0, s));
+    PassDesc Cd = base_desc();
+    Cd.in = View{a, 0, 0, L[1] * L[2], (int)L[0]};
+    Cd.out = View{b, 0, 0, L[1] * L[2], (int)L[0]};
+    Cd.tw = tw64[0].ptr; Cd.Q = 1; Cd.Rn = 1; Cd.In = (int)(L[1] * L[2]); Cd.nrhs = 2;
+    HGP_TRY(launch<double>((int)(L[0] / 2), PASS_FWD, LAY_STRIDED, Cd, 0, s));
+    *result = b;
+  }
+  return 0;
+}
+
+template <typename T>
+int upload_twiddles(DevBuf& buf, int64_t L) {
+  std::vector<T> h((size_t)(2 * L));
+  for (int64_t q = 0; q < L; ++q) {
+    const double ang = -2.0 * M_PI * (double)q / (double)L;
+    h[2 * q] = (T)std::cos(ang);
+    h[2 * q + 1] = (T)std::sin(ang);
+  }
+  HGP_TRY(buf.ensure(h.size() * sizeof(T)));
+  HIP_TRY(hipMemcpy(buf.ptr, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+  return 0;
+}
+
+// W[k][t] = w_t cos(2 pi t k / n), w_0 = w_{m-1} = 1, else 2  (length-n DFT of the even
+// extension restricted to the m unique points = DCT-I)
+int upload_dct(DevBuf& buf, int64_t m, int64_t n) {
+  std::vector<double> h((size_t)(m * m));
+  for (int64_t k = 0; k < m; ++k)
+    for (int64_t t = 0; t < m; ++t) {
+      const double w = (t == 0 || t == m - 1) ? 1.0 : 2.0;
+      const int64_t e = (t * k) % n;
+      h[(size_t)(k * m + t)] = w * std::cos(2.0 * M_PI * (double)e / (double)n);
+    }
+  HGP_TRY(buf.ensure(h.size() * sizeof(double)));
+  HIP_TRY(hipMemcpy(buf.ptr, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
+  return 0;
+}
+
+template <typename T>
+int set_column_t(hgp_plan* P, const void* column, double jitter, double clamp_min, int64_t* n_clamped) {
+  hipStream_t s = P->stream;
+  const int d = P->d;
+  const int64_t M = P->M;
+  HGP_TRY(P->setM1.ensure(3 * M * sizeof(double)));
+  HGP_TRY(P->setM2.ensure(3 * M * sizeof(double)));
+  HGP_TRY(P->Dm3.ensure(3 * M * sizeof(double)));
+  HGP_TRY(P->nclamp.ensure(sizeof(unsigned long long)));
+  double* a = reinterpret_cast<double*>(P->setM1.ptr);
+  double* b = reinterpret_cast<double*>(P->setM2.ptr);
+  to_f64<T>(column, a, M, jitter, s);
+  // D_raw = DCT-I over every axis (length-n FFT of the circulant embedding, real part)
+  for (int ax = 0; ax < d; ++ax) {
+    int64_t I = 1;
+    for (int c = ax + 1; c < d; ++c) I *= P->m[c];
+    dct_axis(reinterpret_cast<double*>(P->Wdct[ax].ptr), a, b, (int)P->m[ax], I, M / P->m[ax], 1.0, s);
+    std::swap(a, b);
+  }
+  HIP_TRY(hipMemsetAsync(P->nclamp.ptr, 0, sizeof(unsigned long long), s));
+  double* D3 = reinterpret_cast<double*>(P->Dm3.ptr);
+  clamp_spectrum(a, D3, M, clamp_min, reinterpret_cast<unsigned long long*>(P->nclamp.ptr), s);
+  // generators: c_K = IFFT_n(D), c_inv = IFFT_n(1/D), s = IFFT_n(sqrt D) on the m-grid
+  double* src = D3;
+  double* dst = a;
+  for (int ax = 0; ax < d; ++ax) {
+    int64_t I = 1;
+    for (int c = ax + 1; c < d; ++c) I *= P->m[c];
+    dct_axis(reinterpret_cast<double*>(P->Wdct[ax].ptr), src, dst, (int)P->m[ax], I, 3 * M / P->m[ax],
+             1.0 / (double)P->n[ax], s);
+    src = dst;
+    dst = (dst == a) ? b : a;
+  }
+  const double* cK = src;
+  const double* cI = src + M;
+  const double* sv = src + 2 * M;
+  // operator spectra on the power-of-two grids
+  const int64_t big = std::max(P->prodLK, P->prodLR);
+  HGP_TRY(P->set1.ensure((size_t)big * sizeof(double2)));
+  HGP_TRY(P->set2.ensure((size_t)big * sizeof(double2)));
+  double2* g1 = reinterpret_cast<double2*>(P->set1.ptr);
+  double2* g2 = reinterpret_cast<double2*>(P->set2.ptr);
+  GridDims gd;
+  gd.d = d;
+  for (int ax = 0; ax < 3; ++ax) { gd.m[ax] = P->m[ax]; gd.n[ax] = P->n[ax]; gd.L[ax] = P->LK[ax]; }
+  embed_K(cK, cI, g1, gd, s);
+  double2* F = nullptr;
+  HGP_TRY(fwd_grid_f64(P, P->LK, P->tw64K, g1, g2, &F));
+  HGP_TRY(P->specK.ensure((size_t)P->prodLK * sizeof(T)));
+  HGP_TRY(P->specI.ensure((size_t)P->prodLK * sizeof(T)));
+  extract_pair<T>(F, P->specK.ptr, P->specI.ptr, P->prodLK, 1.0 / (double)P->prodLK, s);
+  for (int ax = 0; ax < 3; ++ax) gd.L[ax] = P->LR[ax];
+  embed_R(sv, g1, gd, s);
+  HGP_TRY(fwd_grid_f64(P, P->LR, P->tw64R, g1, g2, &F));
+  HGP_TRY(P->specR.ensure((size_t)P->prodLR * sizeof(C2<T>)));
+  extract_cplx<T>(F, P->specR.ptr, P->prodLR, 1.0 / (double)P->prodLR, s);
+  HIP_TRY(hipGetLastError());
+  P->have_spec = true;
+  if (n_clamped) {
+    unsigned long long h = 0;
+    HIP_TRY(hipMemcpyAsync(&h, P->nclamp.ptr, sizeof(h), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    *n_clamped = (int64_t)h;
+  }
+  return 0;
+}
+
+// ---- PCG -------------------------------------------------------------------------------------
+int rn_last(const hgp_plan* P) {
+  if (P->d == 1) return 1;
+  if (P->d == 2) return (int)P->m[0];
+  return (int)(P->m[0] * P->m[1]);
+}
+
+template <typename T>
+int pcg_begin_t(hgp_plan* P, const void* b, void* x, int64_t nrhs, int use_precond, int layout) {
+  hipStream_t s = P->stream;
+  const int64_t M = P->M;
+  const size_t vb = (size_t)(nrhs * M) * sizeof(T);
+  HGP_TRY(P->r.ensure(vb));
+  HGP_TRY(P->z.ensure(vb));
+  HGP_TRY(P->p.ensure(vb));
+  HGP_TRY(P->Ap.ensure(vb));
+  const int npo = rn_last(P), npu = update_np(M);
+  HGP_TRY(P->part_op.ensure((size_t)(nrhs * npo) * sizeof(T)));
+  HGP_TRY(P->part_u.ensure((size_t)(nrhs * npu) * sizeof(T)));
+  HGP_TRY(P->scal.ensure((size_t)(4 * nrhs) * sizeof(T)));
+  HGP_TRY(P->flags.ensure(16));
+  const void* brow = b;
+  void* xrow = x;
+  if (layout == HGP_LAYOUT_COLS) {
+    HGP_TRY(P->bT.ensure(vb));
+    HGP_TRY(P->xT.ensure(vb));
+    transpose<T>(b, P->bT.ptr, M, nrhs, s);   // (M, nrhs) -> (nrhs, M)
+    brow = P->bT.ptr;
+    xrow = P->xT.ptr;
+  }
+  int* flags = reinterpret_cast<int*>(P->flags.ptr);
+  HIP_TRY(hipMemsetAsync(flags, 0, 16, s));
+  T* sc = reinterpret_cast<T*>(P->scal.ptr);
+  T* rs = sc;
+  cg_init<T>(brow, xrow, P->r.ptr, nrhs * M, s);
+  if (use_precond) {
+    HGP_TRY(run_op<T>(P, HGP_OP_CINV, P->r.ptr, P->z.ptr, nrhs, P->r.ptr, P->part_op.ptr, nullptr));
+    reduce_rows<T>(P->part_op.ptr, npo, (int)nrhs, rs, s);
+    vcopy<T>(P->z.ptr, P->p.ptr, nrhs * M, nullptr, s);
+  } else {
+    rowdot_part<T>(P->r.ptr, P->r.ptr, P->part_u.ptr, nrhs, M, npu, s);
+    reduce_rows<T>(P->part_u.ptr, npu, (int)nrhs, rs, s);
+    vcopy<T>(P->r.ptr, P->p.ptr, nrhs * M, nullptr, s);
+  }
+  HIP_TRY(hipGetLastError());
+  P->cg_nrhs = nrhs;
+  P->cg_precond = use_precond;
+  P->cg_layout = layout;
+  P->cg_x_user = x;
+  P->cg_x = xrow;
+  P->cg_active = true;
+  return 0;
+}
+
+template <typename T>
+int pcg_step_t(hgp_plan* P, double tol) {
+  hipStream_t s = P->stream;
+  const int64_t nrhs = P->cg_nrhs, M = P->M;
+  const int npo = rn_last(P), npu = update_np(M);
+  int* flags = reinterpret_cast<int*>(P->flags.ptr);
+  int* done = flags;
+  int* iters = flags + 1;
+  T* sc = reinterpret_cast<T*>(P->scal.ptr);
+  T* rs = sc;
+  T* alpha = sc + nrhs;
+  T* beta = sc + 2 * nrhs;
+  T* rnew = sc + 3 * nrhs;
+  // Ap = K p ; fused p.Ap
+  HGP_TRY(run_op<T>(P, HGP_OP_K, P->p.ptr, P->Ap.ptr, nrhs, P->p.ptr, P->part_op.ptr, done));
+  cg_alpha<T>(P->part_op.ptr, npo, (int)nrhs, rs, alpha, done, s);
+  cg_update_xr<T>(P->cg_x, P->r.ptr, P->p.ptr, P->Ap.ptr, alpha, P->part_u.ptr, nrhs, M, done, s);
+  cg_check<T>(P->part_u.ptr, npu, (int)nrhs, tol, rnew, done, iters, s);
+  if (P->cg_precond) {
+    HGP_TRY(run_op<T>(P, HGP_OP_CINV, P->r.ptr, P->z.ptr, nrhs, P->r.ptr, P->part_op.ptr, done));
+    cg_beta<T>(P->part_op.ptr, npo, (int)nrhs, rs, beta, done, s);
+    cg_update_p<T>(P->p.ptr, P->z.ptr, beta, nrhs, M, done, s);
+  } else {
+    cg_beta<T>(P->part_u.ptr, npu, (int)nrhs, rs, beta, done, s);
+    cg_update_p<T>(P->p.ptr, P->r.ptr, beta, nrhs, M, done, s);
+  }
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+template <typename T>
+int pcg_finish_x(hgp_plan* P) {
+  if (P->cg_layout == HGP_LAYOUT_COLS) transpose<T>(P->cg_x, P->cg_x_user, P->cg_nrhs, P->M, P->stream);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+#define DISPATCH(P, FN, ...) ((P)->dtype == HGP_F64 ? FN<double>(__VA_ARGS__) : FN<float>(__VA_ARGS__))
+
+int check_plan(const hgp_plan* P) {
+  if (P == nullptr) return fail(HGP_E_ARG, "null plan");
+  return 0;
+}
+
+int use_device(const hgp_plan* P) {
+  HIP_TRY(hipSetDevice(P->device));
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* hgp_last_error(void) { return g_err.c_str(); }
+
+const char* hgp_version(void) { return "hipgp-mi355x 0.1 (gfx950)"; }
+
+int hgp_plan_create(int device, int ndim, const int64_t* m, int dtype, int64_t max_rhs, void* hip_stream,
+                    hgp_plan** out) {
+  if (out == nullptr || m == nullptr) return fail(HGP_E_ARG, "null argument");
+  *out = nullptr;
+  if (ndim < 1 || ndim > 3) return fail(HGP_E_ARG, "ndim must be 1..3 (torch.fft signal_ndim limit)");
+  if (dtype != HGP_F32 && dtype != HGP_F64) return fail(HGP_E_ARG, "dtype must be HGP_F32 or HGP_F64");
+  (void)max_rhs;
+  HIP_TRY(hipSetDevice(device));
+  hgp_plan* P = new hgp_plan();
+  P->device = device;
+  P->dtype = dtype;
+  P->stream = reinterpret_cast<hipStream_t>(hip_stream);
+  P->esz = dtype == HGP_F64 ? 8 : 4;
+  P->ndim_user = ndim;
+  int d = 0;
+  for (int a = 0; a < ndim; ++a) {
+    if (m[a] < 1) { delete P; return fail(HGP_E_ARG, "grid sizes must be >= 1"); }
+    if (m[a] == 1) continue;     // size-1 axes are identities (n = 1, hipgp.py:72)
+    P->m[d] = m[a];
+    P->n[d] = 2 * m[a] - 2;
+    P->LK[d] = next_pow2(2 * m[a] - 1);
+    P->LR[d] = next_pow2(4 * m[a] - 4);
+    ++d;
+  }
+  P->d = d;
+  if (d == 0) { delete P; return fail(HGP_E_UNSUPPORTED, "a grid with every axis of size 1 (M = 1) is not supported"); }
+  for (int a = 0; a < d; ++a) {
+    if (P->LR[a] / 2 > 8192) { delete P; return fail(HGP_E_UNSUPPORTED, "grid axis longer than 4097 points is not supported yet"); }
+    P->M *= P->m[a];
+    P->Mp *= P->n[a];
+    P->prodLK *= P->LK[a];
+    P->prodLR *= P->LR[a];
+  }
+  const char* wb = std::getenv("HGP_WS_MB");
+  if (wb) P->ws_budget = (int64_t)std::atoll(wb) << 20;
+  int rc = 0;
+  for (int a = 0; a < d && rc == 0; ++a) {
+    if (dtype == HGP_F64) {
+      rc = upload_twiddles<double>(P->twK[a], P->LK[a]);
+      if (!rc) rc = upload_twiddles<double>(P->twR[a], P->LR[a]);
+    } else {
+      rc = upload_twiddles<float>(P->twK[a], P->LK[a]);
+      if (!rc) rc = upload_twiddles<float>(P->twR[a], P->LR[a]);
+    }
+    if (!rc) rc = upload_twiddles<double>(P->tw64K[a], P->LK[a]);
+    if (!rc) rc = upload_twiddles<double>(P->tw64R[a], P->LR[a]);
+    if (!rc) rc = upload_dct(P->Wdct[a], P->m[a], P->n[a]);
+  }
+  if (rc) { delete P; return rc; }
+  *out = P;
+  return 0;
+}
+
+int hgp_plan_set_stream(hgp_plan* plan, void* hip_stream) {
+  HGP_TRY(check_plan(plan));
+  plan->stream = reinterpret_cast<hipStream_t>(hip_stream);
+  return 0;
+}
+
+int hgp_plan_set_column(hgp_plan* plan, const void* column, double jitter, double clamp_min, int64_t* n_clamped) {
+  HGP_TRY(check_plan(plan));
+  if (column == nullptr) return fail(HGP_E_ARG, "null column");
+  HGP_TRY(use_device(plan));
+  return DISPATCH(plan, set_column_t, plan, column, jitter, clamp_min, n_clamped);
+}
+
+int hgp_toeplitz_apply(hgp_plan* plan, int op, const void* x, void* y, int64_t nrhs) {
+  HGP_TRY(check_plan(plan));
+  if (!plan->have_spec) return fail(HGP_E_STATE, "hgp_plan_set_column has not been called");
+  if (op < HGP_OP_K || op > HGP_OP_R) return fail(HGP_E_ARG, "bad op");
+  if (nrhs < 0 || (nrhs > 0 && (x == nullptr || y == nullptr))) return fail(HGP_E_ARG, "bad x/y/nrhs");
+  if (x == y) return fail(HGP_E_ARG, "x and y must not alias");
+  if (nrhs == 0) return 0;
+  HGP_TRY(use_device(plan));
+  return DISPATCH(plan, run_op, plan, op, x, y, nrhs, nullptr, nullptr, nullptr);
+}
+
+int hgp_toeplitz_apply_pass(hgp_plan* plan, int op, const void* x, void* y, int64_t nrhs, int pass) {
+  HGP_TRY(check_plan(plan));
+  if (!plan->have_spec) return fail(HGP_E_STATE, "hgp_plan_set_column has not been called");
+  if (op < HGP_OP_K || op > HGP_OP_R || pass < -1) return fail(HGP_E_ARG, "bad op/pass");
+  if (nrhs <= 0 || x == nullptr || y == nullptr || x == y) return fail(HGP_E_ARG, "bad x/y/nrhs");
+  HGP_TRY(use_device(plan));
+  return DISPATCH(plan, run_op, plan, op, x, y, nrhs, nullptr, nullptr, nullptr, pass);
+}
+
+int hgp_op_pass_count(const hgp_plan* plan) {
+  if (plan == nullptr) return fail(HGP_E_ARG, "null plan");
+  return plan->d == 1 ? 1 : (plan->d == 2 ? 3 : 5);
+}
+
+int hgp_pcg_begin(hgp_plan* plan, const void* b, void* x, int64_t nrhs, int use_precond, int layout) {
+  HGP_TRY(check_plan(plan));
+  if (!plan->have_spec) return fail(HGP_E_STATE, "hgp_plan_set_column has not been called");
+  if (nrhs <= 0 || b == nullptr || x == nullptr) return fail(HGP_E_ARG, "bad b/x/nrhs");
+  if (layout != HGP_LAYOUT_ROWS && layout != HGP_LAYOUT_COLS) return fail(HGP_E_ARG, "bad layout");
+  HGP_TRY(use_device(plan));
+  return DISPATCH(plan, pcg_begin_t, plan, b, x, nrhs, use_precond ? 1 : 0, layout);
+}
+
+int hgp_pcg_step(hgp_plan* plan, double tol, int* converged) {
+  HGP_TRY(check_plan(plan));
+  if (!plan->cg_active) return fail(HGP_E_STATE, "hgp_pcg_begin has not been called");
+  HGP_TRY(use_device(plan));
+  HGP_TRY(DISPATCH(plan, pcg_step_t, plan, tol));
+  HGP_TRY(DISPATCH(plan, pcg_finish_x, plan));
+  if (converged) {
+    int h = 0;
+    HIP_TRY(hipMemcpyAsync(&h, plan->flags.ptr, sizeof(int), hipMemcpyDeviceToHost, plan->stream));
+    HIP_TRY(hipStreamSynchronize(plan->stream));
+    *converged = h;
+  }
+  return 0;
+}
+
+int hgp_pcg_solve(hgp_plan* plan, const void* b, void* x, int64_t nrhs, int maxiter, double tol, int use_precond,
+                  int layout, int* iters_done) {
+  HGP_TRY(hgp_pcg_begin(plan, b, x, nrhs, use_precond, layout));
+  for (int it = 0; it < maxiter; ++it) HGP_TRY(DISPATCH(plan, pcg_step_t, plan, tol));
+  HGP_TRY(DISPATCH(plan, pcg_finish_x, plan));
+  if (iters_done) {
+    int h[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(h, plan->flags.ptr, sizeof(h), hipMemcpyDeviceToHost, plan->stream));
+    HIP_TRY(hipStreamSynchronize(plan->stream));
+    *iters_done = h[1];
+  }
+  return 0;
+}
+
+int hgp_get_spectrum(hgp_plan* plan, int which, void* out) {
+  HGP_TRY(check_plan(plan));
+  if (!plan->have_spec) return fail(HGP_E_STATE, "hgp_plan_set_column has not been called");
+  if (which < 0 || which > 2 || out == nullptr) return fail(HGP_E_ARG, "bad which/out");
+  HGP_TRY(use_device(plan));
+  GridDims g;
+  g.d = plan->d;
+  for (int a = 0; a < 3; ++a) { g.m[a] = plan->m[a]; g.n[a] = plan->n[a]; g.L[a] = plan->LK[a]; }
+  const int sel = which == HGP_SPEC_D ? 0 : (which == HGP_SPEC_DI ? 1 : 2);   // Dm3 = [D | 1/D | sqrt D]
+  const double* src = reinterpret_cast<const double*>(plan->Dm3.ptr) + sel * plan->M;
+  if (plan->dtype == HGP_F64) expand_spec<double>(src, out, g, plan->stream);
+  else expand_spec<float>(src, out, g, plan->stream);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+int hgp_rowdot(int dtype, const void* a, const void* c, void* out, int64_t nrhs, int64_t M, void* hip_stream) {
+  if (nrhs <= 0 || M <= 0) return 0;
+  if (a == nullptr || c == nullptr || out == nullptr) return fail(HGP_E_ARG, "null pointer");
+  hipStream_t s = reinterpret_cast<hipStream_t>(hip_stream);
+  const int np = update_np(M);
+  void* part = nullptr;
+  const size_t es = dtype == HGP_F64 ? 8 : 4;
+  HIP_TRY(hipMallocAsync(&part, (size_t)(nrhs * np) * es, s));
+  if (dtype == HGP_F64) { rowdot_part<double>(a, c, part, nrhs, M, np, s); reduce_rows<double>(part, np, (int)nrhs, out, s); }
+  else { rowdot_part<float>(a, c, part, nrhs, M, np, s); reduce_rows<float>(part, np, (int)nrhs, out, s); }
+  HIP_TRY(hipFreeAsync(part, s));
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+int hgp_plan_info(const hgp_plan* plan, int64_t* M, int64_t* Mprime, int64_t* L_K, int64_t* L_R) {
+  HGP_TRY(check_plan(plan));
+  if (M) *M = plan->M;
+  if (Mprime) *Mprime = plan->Mp;
+  for (int a = 0; a < 3; ++a) {
+    if (L_K) L_K[a] = a < plan->d ? plan->LK[a] : 1;
+    if (L_R) L_R[a] = a < plan->d ? plan->LR[a] : 1;
+  }
+  return 0;
+}
+
+int hgp_plan_destroy(hgp_plan* plan) {
+  if (plan == nullptr) return 0;
+  (void)hipSetDevice(plan->device);
+  (void)hipStreamSynchronize(plan->stream);
+  delete plan;
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,198 @@
+// hgp_fft.hpp — device FFT engine for the Toeplitz/BTTB operators (gfx950, wave64).
+//
+// What it computes.  Every Toeplitz-type operator of the reference (toeplitz_tensor.py:70-125)
+// is a per-axis-separable convolution  y = crop( IFFT_L( S ⊙ FFT_L( pad x ) ) )  with a
+// power-of-two length L per axis (see DESIGN.md §2 for why L replaces the reference's
+// circulant size n = 2m-2 exactly).  A length-L transform of a line is split into its even
+// and odd frequency halves, each an H = L/2 point FFT:
+//     X[2k]   = FFT_H( x[p] + x[p+H] )[k]
+//     X[2k+1] = FFT_H( (x[p] - x[p+H]) * W_L^p )[k]
+// which (a) prunes the zero padding for free (x[p+H] = 0 when the input fits in H) and
+// (b) halves the LDS footprint per line.  Frequencies are stored "half-major"
+// (index = half*H + k), and every pass/spectrum uses that same order.
+//
+// One H-point FFT = Stockham autosort stages of radix <= P, where each thread owns the P
+// positions {t + T*k, k < P} (T = H/P threads per line).  The first stage reads from
+// registers, intermediate stages exchange through LDS, and the last stage leaves the result
+// in registers in natural order at the SAME positions — so load, spectrum multiply and
+// store all happen in registers with coalesced global accesses.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace hgp {
+
+template <typename T> struct cx;
+template <> struct cx<float> { using t = float2; };
+template <> struct cx<double> { using t = double2; };
+template <typename T> using C2 = typename cx<T>::t;
+
+template <typename T> __device__ __forceinline__ C2<T> mk(T a, T b) { C2<T> r; r.x = a; r.y = b; return r; }
+template <typename T> __device__ __forceinline__ C2<T> cadd(C2<T> a, C2<T> b) { return mk<T>(a.x + b.x, a.y + b.y); }
+template <typename T> __device__ __forceinline__ C2<T> csub(C2<T> a, C2<T> b) { return mk<T>(a.x - b.x, a.y - b.y); }
+template <typename T> __device__ __forceinline__ C2<T> cmul(C2<T> a, C2<T> b) {
+  return mk<T>(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+// a * conj(b)
+template <typename T> __device__ __forceinline__ C2<T> cmulc(C2<T> a, C2<T> b) {
+  return mk<T>(a.x * b.x + a.y * b.y, a.y * b.x - a.x * b.y);
+}
+template <typename T> __device__ __forceinline__ C2<T> cscale(C2<T> a, T s) { return mk<T>(a.x * s, a.y * s); }
+
+// points per thread: 16 complex in fp32 (32 VGPRs), 8 in fp64 (32 VGPRs)
+template <typename T> struct PMax;
+template <> struct PMax<float> { static constexpr int v = 16; };
+template <> struct PMax<double> { static constexpr int v = 8; };
+
+template <int H, int P> struct Stages {
+  static constexpr int count() { int n = 0, rem = H; while (rem > 1) { int r = rem >= P ? P : rem; rem /= r; ++n; } return n; }
+  static constexpr int radix(int s) { int rem = H; for (int i = 0; i < s; ++i) rem /= (rem >= P ? P : rem); return rem >= P ? P : rem; }
+  static constexpr int ns(int s) { int ns = 1, rem = H; for (int i = 0; i < s; ++i) { int r = rem >= P ? P : rem; ns *= r; rem /= r; } return ns; }
+};
+
+// multiply by exp(DIR * 2*pi*i*Q/16), DIR = -1 forward / +1 inverse; Q a compile-time
+// constant after unrolling (the switch folds).
+template <typename T, int DIR>
+__device__ __forceinline__ C2<T> rot16(C2<T> v, int Q) {
+  const T c8 = (T)0.70710678118654752440, c1 = (T)0.92387953251128675613, s1 = (T)0.38268343236508977173;
+  Q &= 15;
+  if (DIR > 0) Q = (16 - Q) & 15;           // inverse: exp(+i th) = forward rotation by -Q
+  switch (Q) {                              // forward: multiply by (cos th, -sin th), th=2pi Q/16
+    case 0: return v;
+    case 4: return mk<T>(v.y, -v.x);
+    case 8: return mk<T>(-v.x, -v.y);
+    case 12: return mk<T>(-v.y, v.x);
+    case 2: return mk<T>(c8 * (v.x + v.y), c8 * (v.y - v.x));
+    case 6: return mk<T>(c8 * (v.y - v.x), -c8 * (v.x + v.y));
+    case 10: return mk<T>(-c8 * (v.x + v.y), c8 * (v.x - v.y));
+    case 14: return mk<T>(c8 * (v.x - v.y), c8 * (v.x + v.y));
+    case 1: return cmul<T>(v, mk<T>(c1, -s1));
+    case 3: return cmul<T>(v, mk<T>(s1, -c1));
+    case 5: return cmul<T>(v, mk<T>(-s1, -c1));
+    case 7: return cmul<T>(v, mk<T>(-c1, -s1));
+    case 9: return cmul<T>(v, mk<T>(-c1, s1));
+    case 11: return cmul<T>(v, mk<T>(-s1, c1));
+    case 13: return cmul<T>(v, mk<T>(s1, c1));
+    default: return cmul<T>(v, mk<T>(c1, s1));   // 15
+  }
+}
+
+// In-register DFT of size R (natural order in and out), R in {1,2,4,8,16}.
+template <typename T, int R, int DIR>
+__device__ __forceinline__ void dft(C2<T>* v) {
+  if constexpr (R == 1) {
+    return;
+  } else if constexpr (R == 2) {
+    C2<T> a = v[0], b = v[1];
+    v[0] = cadd<T>(a, b);
+    v[1] = csub<T>(a, b);
+  } else if constexpr (R == 4) {
+    C2<T> s02 = cadd<T>(v[0], v[2]), d02 = csub<T>(v[0], v[2]);
+    C2<T> s13 = cadd<T>(v[1], v[3]), d13 = csub<T>(v[1], v[3]);
+    // forward: d13 * (-i) = (y, -x); inverse: d13 * (+i) = (-y, x)
+    C2<T> rd = (DIR < 0) ? mk<T>(d13.y, -d13.x) : mk<T>(-d13.y, d13.x);
+    v[0] = cadd<T>(s02, s13);
+    v[2] = csub<T>(s02, s13);
+    v[1] = cadd<T>(d02, rd);
+    v[3] = csub<T>(d02, rd);
+  } else {
+    constexpr int R1 = 4, R2 = R / 4;
+    C2<T> y[R];
+#pragma unroll
+    for (int n2 = 0; n2 < R2; ++n2) {
+      C2<T> a[R1];
+#pragma unroll
+      for (int n1 = 0; n1 < R1; ++n1) a[n1] = v[R2 * n1 + n2];
+      dft<T, R1, DIR>(a);
+#pragma unroll
+      for (int k1 = 0; k1 < R1; ++k1) y[n2 * R1 + k1] = rot16<T, DIR>(a[k1], (n2 * k1 * (16 / R)) & 15);
+    }
+#pragma unroll
+    for (int k1 = 0; k1 < R1; ++k1) {
+      C2<T> b[R2];
+#pragma unroll
+      for (int n2 = 0; n2 < R2; ++n2) b[n2] = y[n2 * R1 + k1];
+      dft<T, R2, DIR>(b);
+#pragma unroll
+      for (int k2 = 0; k2 < R2; ++k2) v[k1 + R1 * k2] = b[k2];
+    }
+  }
+}
+
+// LDS address of logical element e (padding breaks the power-of-two strides of the
+// Stockham write pattern: one complex slot per 16).
+__device__ __forceinline__ int lds_phys(int e) { return e + (e >> 4); }
+
+// phys(base + x) for a compile-time x: exact split into phys(base) + x*17/16 whenever x is a
+// multiple of 16, or when base is 16-aligned and x < 16 (then the pad term is unchanged).
+// (x is a constant after loop unrolling, so the branches fold.)
+__device__ __forceinline__ int lds_at(int pbase, int base, int x, bool base16) {
+  if (x % 16 == 0) return pbase + x + x / 16;
+  if (base16 && x < 16) return pbase + x;
+  return lds_phys(base + x);
+}
+
+// One H-point FFT of the line whose P values this thread holds in v (positions t + T*k,
+// k = register index).  Result in v, natural order, same positions.  Line element e of the
+// block's LDS image lives at lds_phys(base + e*STRIDE) (STRIDE = 1: line-contiguous image;
+// STRIDE = C: lines interleaved).  twL: W_L^q table (L = 2H, forward sign), so
+// W_H^e = twL[2e].  All threads of the block must call it when T > 1 (block barriers).
+template <typename T, int H, int P, int DIR, int STRIDE, int S>
+__device__ __forceinline__ void fft_stage(C2<T> (&v)[P], C2<T>* lds, int base, int t,
+                                          const C2<T>* __restrict__ twL) {
+  using St = Stages<H, P>;
+  constexpr int NST = St::count();
+  if constexpr (S < NST) {
+    constexpr int R = St::radix(S), NS = St::ns(S), TT = H / P, NB = P / R;
+    C2<T> a[NB][R];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) a[b][r] = v[b + r * NB];
+      if constexpr (NS > 1) {
+        const int j = t + b * TT;
+        const int kk = j & (NS - 1);
+#pragma unroll
+        for (int r = 1; r < R; ++r) {
+          // W_H^{kk*r*H/(NS*R)} = twL[2*kk*r*H/(NS*R)]
+          const C2<T> w = twL[(2 * (H / (NS * R))) * kk * r];
+          a[b][r] = (DIR < 0) ? cmul<T>(a[b][r], w) : cmulc<T>(a[b][r], w);
+        }
+      }
+      dft<T, R, DIR>(a[b]);
+    }
+    if constexpr (S + 1 < NST) {
+      // TT is a multiple of NS at every non-last stage, so butterfly b of this thread
+      // writes at idxD(t) + b*TT*R + r*NS.
+      const int idxD = (t / NS) * NS * R + (t & (NS - 1));
+      const int wb = base + idxD * STRIDE;
+      const int pwb = lds_phys(wb);
+      constexpr bool WB16 = (STRIDE == 1) && (NS == 1) && (R == 16);   // base 16-aligned
+      __syncthreads();   // previous readers of this LDS region are done
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+          lds[lds_at(pwb, wb, (b * TT * R + r * NS) * STRIDE, WB16)] = a[b][r];
+      __syncthreads();
+      const int rb = base + t * STRIDE;
+      const int prb = lds_phys(rb);
+#pragma unroll
+      for (int k = 0; k < P; ++k) v[k] = lds[lds_at(prb, rb, TT * k * STRIDE, false)];
+      fft_stage<T, H, P, DIR, STRIDE, S + 1>(v, lds, base, t, twL);
+    } else {
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int r = 0; r < R; ++r) v[b + r * NB] = a[b][r];
+    }
+  }
+}
+
+template <typename T, int H, int P, int DIR, int STRIDE>
+__device__ __forceinline__ void fft_line(C2<T> (&v)[P], C2<T>* lds, int base, int t,
+                                         const C2<T>* __restrict__ twL) {
+  fft_stage<T, H, P, DIR, STRIDE, 0>(v, lds, base, t, twL);
+}
+
+}  // namespace hgp

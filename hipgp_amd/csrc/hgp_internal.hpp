@@ -1,0 +1,45 @@
+// hgp_internal.hpp — declarations shared by the kernel and API translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "hgp_pass.hpp"
+
+namespace hgp {
+
+struct GridDims { int d; int64_t m[3]; int64_t n[3]; int64_t L[3]; };
+
+struct PassGeom { int C; int threads; int lds; };
+template <typename T>
+hipError_t launch_pass(int H, int mode, int lay, const PassDesc& d, int64_t nblocks, hipStream_t s);
+template <typename T> PassGeom pass_geom(int H, int lay);
+
+// setup (fp64)
+void dct_axis(const double* W, const double* in, double* out, int m, int64_t I, int64_t ncols, double scale,
+              hipStream_t s);
+template <typename T> void to_f64(const void* src, double* dst, int64_t n, double add0, hipStream_t s);
+void clamp_spectrum(const double* Draw, double* out3, int64_t M, double clamp_min, unsigned long long* nclamp,
+                    hipStream_t s);
+void embed_K(const double* cK, const double* cI, double2* out, const GridDims& g, hipStream_t s);
+void embed_R(const double* sv, double2* out, const GridDims& g, hipStream_t s);
+template <typename T> void extract_pair(const double2* F, void* a, void* b, int64_t n, double scale, hipStream_t s);
+template <typename T> void extract_cplx(const double2* F, void* o, int64_t n, double scale, hipStream_t s);
+template <typename T> void expand_spec(const double* src, void* out, const GridDims& g, hipStream_t s);
+
+// CG
+int update_np(int64_t M);
+template <typename T> void cg_init(const void* b, void* x, void* r, int64_t n, hipStream_t s);
+template <typename T> void vcopy(const void* src, void* dst, int64_t n, const int* done, hipStream_t s);
+template <typename T> void transpose(const void* in, void* out, int64_t rows, int64_t cols, hipStream_t s);
+template <typename T> void rowdot_part(const void* a, const void* c, void* part, int64_t nrhs, int64_t M, int np, hipStream_t s);
+template <typename T> void reduce_rows(const void* part, int np, int nrhs, void* out, hipStream_t s);
+template <typename T> void cg_alpha(const void* part, int np, int nrhs, const void* rs, void* alpha, const int* done, hipStream_t s);
+template <typename T> void cg_update_xr(void* x, void* r, const void* p, const void* Ap, const void* alpha, void* part,
+                                        int64_t nrhs, int64_t M, const int* done, hipStream_t s);
+template <typename T> void cg_check(const void* part, int np, int nrhs, double tol, void* rnew, int* done, int* iters,
+                                    hipStream_t s);
+template <typename T> void cg_beta(const void* part, int np, int nrhs, void* rs, void* beta, const int* done, hipStream_t s);
+template <typename T> void cg_update_p(void* p, const void* z, const void* beta, int64_t nrhs, int64_t M, const int* done,
+                                       hipStream_t s);
+
+}  // namespace hgp

@@ -1,0 +1,490 @@
+// hgp_kernels.hip — pass dispatch, spectrum-setup kernels and batched-CG kernels.
+#include "hgp_internal.hpp"
+
+namespace hgp {
+
+// ------------------------------------------------------------------------------------------
+// spectrum setup (fp64)
+// ------------------------------------------------------------------------------------------
+
+// out(k, j) = scale * sum_t W[k*m + t] * in(t, j);   (t,j) -> o*(m*I) + t*I + i, j = o*I + i.
+// LDS-tiled DGEMM: 64x64 output tile, 16-deep k-steps, 256 threads, 4x4 outputs each.
+__global__ __launch_bounds__(256) void k_dct_gemm(const double* __restrict__ W, const double* __restrict__ in,
+                                                  double* __restrict__ out, int m, int64_t I, int64_t ncols,
+                                                  double scale) {
+  __shared__ double As[16][65];
+  __shared__ double Bs[16][65];
+  const int tid = threadIdx.x;
+  const int tx = tid & 15, ty = tid >> 4;
+  const int64_t j0 = (int64_t)blockIdx.x * 64;
+  const int k0 = blockIdx.y * 64;
+  double acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = 0.0;
+  for (int t0 = 0; t0 < m; t0 += 16) {
+    // A tile: As[tt][kk] = W[(k0+kk)*m + t0+tt]
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int e = tid + 256 * c;       // 0..1023
+      const int tt = e & 15, kk = e >> 4;
+      const int k = k0 + kk, tcol = t0 + tt;
+      As[tt][kk] = (k < m && tcol < m) ? W[(int64_t)k * m + tcol] : 0.0;
+    }
+    // B tile: Bs[tt][jj] = in(t0+tt, j0+jj)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int e = tid + 256 * c;
+      int tt, jj;
+      if (I == 1) { tt = e & 15; jj = e >> 4; } else { jj = e & 63; tt = e >> 6; }
+      const int64_t j = j0 + jj;
+      const int tcol = t0 + tt;
+      double val = 0.0;
+      if (j < ncols && tcol < m) {
+        const int64_t o = j / I, i = j - o * I;
+        val = in[o * (int64_t)m * I + (int64_t)tcol * I + i];
+      }
+      Bs[tt][jj] = val;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int tt = 0; tt < 16; ++tt) {
+      double av[4], bv[4];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) av[a] = As[tt][ty + 16 * a];
+#pragma unroll
+      for (int b = 0; b < 4; ++b) bv[b] = Bs[tt][tx + 16 * b];
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = fma(av[a], bv[b], acc[a][b]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const int k = k0 + ty + 16 * a;
+    if (k >= m) continue;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int64_t j = j0 + tx + 16 * b;
+      if (j >= ncols) continue;
+      const int64_t o = j / I, i = j - o * I;
+      out[o * (int64_t)m * I + (int64_t)k * I + i] = acc[a][b] * scale;
+    }
+  }
+}
+
+void dct_axis(const double* W, const double* in, double* out, int m, int64_t I, int64_t ncols, double scale,
+              hipStream_t s) {
+  dim3 grid((unsigned)((ncols + 63) / 64), (unsigned)((m + 63) / 64));
+  hipLaunchKernelGGL(k_dct_gemm, grid, dim3(256), 0, s, W, in, out, m, I, ncols, scale);
+}
+
+template <typename T>
+__global__ void k_to_f64(const T* __restrict__ src, double* __restrict__ dst, int64_t n, double add0) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = (double)src[i] + (i == 0 ? add0 : 0.0);
+}
+
+template <typename T>
+void to_f64(const void* src, double* dst, int64_t n, double add0, hipStream_t s) {
+  hipLaunchKernelGGL((k_to_f64<T>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (const T*)src, dst, n, add0);
+}
+template void to_f64<float>(const void*, double*, int64_t, double, hipStream_t);
+template void to_f64<double>(const void*, double*, int64_t, double, hipStream_t);
+
+// D = max(Draw, clamp); write [D | 1/D | sqrt(D)] (3 x M) and count clamped entries.
+__global__ void k_clamp(const double* __restrict__ Draw, double* __restrict__ out3, int64_t M, double clamp_min,
+                        unsigned long long* nclamp) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M) return;
+  double d = Draw[i];
+  if (!(d >= clamp_min)) {      // torch.clamp(min=) semantics: values below min (NaN stays NaN)
+    if (d < clamp_min) { d = clamp_min; atomicAdd(nclamp, 1ull); }
+  }
+  out3[i] = d;
+  out3[M + i] = 1.0 / d;
+  out3[2 * M + i] = sqrt(d);
+}
+
+void clamp_spectrum(const double* Draw, double* out3, int64_t M, double clamp_min, unsigned long long* nclamp,
+                    hipStream_t s) {
+  hipLaunchKernelGGL(k_clamp, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, s, Draw, out3, M, clamp_min, nclamp);
+}
+
+// K-type embedding (L >= 2m-1): G[u] = c[|t|], t = u (u < m) or u - L (u > L - m); complex
+// pair (re = cK, im = cInv).
+__global__ void k_embed_K(const double* __restrict__ cK, const double* __restrict__ cI, double2* __restrict__ out,
+                          GridDims g, int64_t total) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  int64_t rem = idx, src = 0, mstride = 1;
+  bool ok = true;
+  for (int a = g.d - 1; a >= 0; --a) {
+    const int64_t u = rem % g.L[a];
+    rem /= g.L[a];
+    int64_t t;
+    if (u < g.m[a]) t = u;
+    else if (u > g.L[a] - g.m[a]) t = g.L[a] - u;
+    else { ok = false; t = 0; }
+    src += t * mstride;
+    mstride *= g.m[a];
+  }
+  double2 v;
+  v.x = ok ? cK[src] : 0.0;
+  v.y = ok ? cI[src] : 0.0;
+  out[idx] = v;
+}
+
+// R-type embedding (L >= n + m - 1): filter s_per(t) on t in [-(m-1), n-1], s_per even and
+// n-periodic, unique values s[0..m-1].
+__global__ void k_embed_R(const double* __restrict__ s, double2* __restrict__ out, GridDims g, int64_t total) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  int64_t rem = idx, src = 0, mstride = 1;
+  bool ok = true;
+  for (int a = g.d - 1; a >= 0; --a) {
+    const int64_t u = rem % g.L[a];
+    rem /= g.L[a];
+    const int64_t m = g.m[a], n = g.n[a], L = g.L[a];
+    int64_t t;
+    if (u < n) t = (u <= m - 1) ? u : n - u;
+    else if (u >= L - m + 1) t = L - u;
+    else { ok = false; t = 0; }
+    src += t * mstride;
+    mstride *= m;
+  }
+  double2 v;
+  v.x = ok ? s[src] : 0.0;
+  v.y = 0.0;
+  out[idx] = v;
+}
+
+void embed_K(const double* cK, const double* cI, double2* out, const GridDims& g, hipStream_t s) {
+  int64_t total = 1;
+  for (int a = 0; a < g.d; ++a) total *= g.L[a];
+  hipLaunchKernelGGL(k_embed_K, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, cK, cI, out, g, total);
+}
+void embed_R(const double* sv, double2* out, const GridDims& g, hipStream_t s) {
+  int64_t total = 1;
+  for (int a = 0; a < g.d; ++a) total *= g.L[a];
+  hipLaunchKernelGGL(k_embed_R, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, sv, out, g, total);
+}
+
+template <typename T>
+__global__ void k_extract_pair(const double2* __restrict__ F, T* __restrict__ a, T* __restrict__ b, int64_t n,
+                               double scale) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double2 f = F[i];
+  a[i] = (T)(f.x * scale);
+  b[i] = (T)(f.y * scale);
+}
+template <typename T>
+__global__ void k_extract_cplx(const double2* __restrict__ F, C2<T>* __restrict__ o, int64_t n, double scale) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double2 f = F[i];
+  o[i] = mk<T>((T)(f.x * scale), (T)(f.y * scale));
+}
+template <typename T>
+void extract_pair(const double2* F, void* a, void* b, int64_t n, double scale, hipStream_t s) {
+  hipLaunchKernelGGL((k_extract_pair<T>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, F, (T*)a, (T*)b, n, scale);
+}
+template <typename T>
+void extract_cplx(const double2* F, void* o, int64_t n, double scale, hipStream_t s) {
+  hipLaunchKernelGGL((k_extract_cplx<T>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, F, (C2<T>*)o, n, scale);
+}
+template void extract_pair<float>(const double2*, void*, void*, int64_t, double, hipStream_t);
+template void extract_pair<double>(const double2*, void*, void*, int64_t, double, hipStream_t);
+template void extract_cplx<float>(const double2*, void*, int64_t, double, hipStream_t);
+template void extract_cplx<double>(const double2*, void*, int64_t, double, hipStream_t);
+
+// full expanded-grid spectrum from the unique m-grid values: u -> min(u, n-u) per axis
+template <typename T>
+__global__ void k_expand_spec(const double* __restrict__ src, T* __restrict__ out, GridDims g, int64_t total) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  int64_t rem = idx, s = 0, mstride = 1;
+  for (int a = g.d - 1; a >= 0; --a) {
+    const int64_t u = rem % g.n[a];
+    rem /= g.n[a];
+    const int64_t t = (u < g.n[a] - u) ? u : g.n[a] - u;
+    s += t * mstride;
+    mstride *= g.m[a];
+  }
+  out[idx] = (T)src[s];
+}
+template <typename T>
+void expand_spec(const double* src, void* out, const GridDims& g, hipStream_t s) {
+  int64_t total = 1;
+  for (int a = 0; a < g.d; ++a) total *= g.n[a];
+  hipLaunchKernelGGL((k_expand_spec<T>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, src, (T*)out, g,
+                     total);
+}
+template void expand_spec<float>(const double*, void*, const GridDims&, hipStream_t);
+template void expand_spec<double>(const double*, void*, const GridDims&, hipStream_t);
+
+// ------------------------------------------------------------------------------------------
+// batched CG kernels (cg.py:44-80 / 5-41).  Per-RHS scalars live on the device; every
+// kernel returns early once the device flag `done` is set by the convergence test.
+// Reductions are fixed-order (deterministic across runs and across RHS sharding).
+// ------------------------------------------------------------------------------------------
+constexpr int UPD_THREADS = 256;
+constexpr int UPD_PER_THREAD = 8;
+constexpr int UPD_CHUNK = UPD_THREADS * UPD_PER_THREAD;
+
+int update_np(int64_t M) { return (int)((M + UPD_CHUNK - 1) / UPD_CHUNK); }
+
+template <typename T>
+__device__ __forceinline__ T block_sum_det(T v, T* red) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  T s = 0;
+  if (threadIdx.x == 0)
+    for (int k = 0; k < nw; ++k) s += red[k];
+  return s;
+}
+
+// x <- 0, r <- b (row layout)
+template <typename T>
+__global__ void k_cg_init(const T* __restrict__ b, T* __restrict__ x, T* __restrict__ r, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) { x[i] = (T)0; r[i] = b[i]; }
+}
+
+template <typename T>
+__global__ void k_copy(const T* __restrict__ s, T* __restrict__ d, int64_t n, const int* done) {
+  if (done && *done) return;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) d[i] = s[i];
+}
+
+// out[c][r] = in[r][c]  (in: rows x cols)
+template <typename T>
+__global__ void k_transpose(const T* __restrict__ in, T* __restrict__ out, int64_t rows, int64_t cols) {
+  __shared__ T tile[32][33];
+  const int64_t c0 = (int64_t)blockIdx.x * 32, r0 = (int64_t)blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 256 threads: 32 x 8
+  for (int k = ty; k < 32; k += 8) {
+    const int64_t r = r0 + k, c = c0 + tx;
+    if (r < rows && c < cols) tile[k][tx] = in[r * cols + c];
+  }
+  __syncthreads();
+  for (int k = ty; k < 32; k += 8) {
+    const int64_t c = c0 + k, r = r0 + tx;
+    if (r < rows && c < cols) out[c * rows + r] = tile[tx][k];
+  }
+}
+
+// per-row dot partials: part[b*np + chunk]
+template <typename T>
+__global__ __launch_bounds__(UPD_THREADS) void k_rowdot_part(const T* __restrict__ a, const T* __restrict__ c,
+                                                             T* __restrict__ part, int64_t M, int np) {
+  __shared__ T red[UPD_THREADS / 64];
+  const int chunk = blockIdx.x, b = blockIdx.y;
+  const int64_t base = (int64_t)b * M;
+  T s = 0;
+#pragma unroll
+  for (int k = 0; k < UPD_PER_THREAD; ++k) {
+    const int64_t j = (int64_t)chunk * UPD_CHUNK + k * UPD_THREADS + threadIdx.x;
+    if (j < M) s += a[base + j] * c[base + j];
+  }
+  s = block_sum_det<T>(s, red);
+  if (threadIdx.x == 0) part[(int64_t)b * np + chunk] = s;
+}
+
+// out[b] = sum_g part[b*np + g]   (one wave per RHS, fixed tree)
+template <typename T>
+__global__ void k_reduce_rows(const T* __restrict__ part, int np, int nrhs, T* __restrict__ out) {
+  const int b = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (b >= nrhs) return;
+  T s = 0;
+  for (int g = lane; g < np; g += 64) s += part[(int64_t)b * np + g];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if (lane == 0) out[b] = s;
+}
+
+// per RHS: alpha = rs / sum(part)   (cg.py:66)
+template <typename T>
+__global__ void k_cg_alpha(const T* __restrict__ part, int np, int nrhs, const T* __restrict__ rs,
+                           T* __restrict__ alpha, const int* done) {
+  if (*done) return;
+  const int b = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (b >= nrhs) return;
+  T s = 0;
+  for (int g = lane; g < np; g += 64) s += part[(int64_t)b * np + g];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if (lane == 0) alpha[b] = rs[b] / s;
+}
+
+// x += alpha p ; r -= alpha Ap ; partial r.r    (cg.py:67-69)
+template <typename T>
+__global__ __launch_bounds__(UPD_THREADS) void k_cg_update_xr(T* __restrict__ x, T* __restrict__ r,
+                                                              const T* __restrict__ p, const T* __restrict__ Ap,
+                                                              const T* __restrict__ alpha, T* __restrict__ part,
+                                                              int64_t M, int np, const int* done) {
+  if (*done) return;
+  __shared__ T red[UPD_THREADS / 64];
+  const int chunk = blockIdx.x, b = blockIdx.y;
+  const int64_t base = (int64_t)b * M;
+  const T al = alpha[b];
+  T s = 0;
+#pragma unroll
+  for (int k = 0; k < UPD_PER_THREAD; ++k) {
+    const int64_t j = (int64_t)chunk * UPD_CHUNK + k * UPD_THREADS + threadIdx.x;
+    if (j < M) {
+      const int64_t o = base + j;
+      x[o] = x[o] + al * p[o];
+      const T rn = r[o] - al * Ap[o];
+      r[o] = rn;
+      s += rn * rn;
+    }
+  }
+  s = block_sum_det<T>(s, red);
+  if (threadIdx.x == 0) part[(int64_t)b * np + chunk] = s;
+}
+
+// rnew = sum(part); done |= all(sqrt(rnew) < tol); iters++ (cg.py:69-71)
+template <typename T>
+__global__ __launch_bounds__(1024) void k_cg_check(const T* __restrict__ part, int np, int nrhs, double tol,
+                                                   T* __restrict__ rnew, int* done, int* iters) {
+  if (*done) return;
+  __shared__ int any_not;
+  if (threadIdx.x == 0) any_not = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  int local_not = 0;
+  for (int b = w; b < nrhs; b += nw) {
+    T s = 0;
+    for (int g = lane; g < np; g += 64) s += part[(int64_t)b * np + g];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+    if (lane == 0) {
+      rnew[b] = s;
+      // torch.all(torch.sqrt(rnew) < tol): NaN compares false -> not converged
+      if (!(sqrt(s) < (T)tol)) local_not = 1;
+    }
+  }
+  if (lane == 0 && local_not) atomicOr(&any_not, 1);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    *iters += 1;
+    if (!any_not) *done = 1;
+  }
+}
+
+// zr = sum(part); beta = zr / rs; rs = zr   (cg.py:74 and next iteration's rs, cg.py:64)
+template <typename T>
+__global__ void k_cg_beta(const T* __restrict__ part, int np, int nrhs, T* __restrict__ rs, T* __restrict__ beta,
+                          const int* done) {
+  if (*done) return;
+  const int b = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (b >= nrhs) return;
+  T s = 0;
+  for (int g = lane; g < np; g += 64) s += part[(int64_t)b * np + g];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if (lane == 0) {
+    beta[b] = s / rs[b];
+    rs[b] = s;
+  }
+}
+
+// p = z + beta p   (cg.py:75)
+template <typename T>
+__global__ __launch_bounds__(UPD_THREADS) void k_cg_update_p(T* __restrict__ p, const T* __restrict__ z,
+                                                             const T* __restrict__ beta, int64_t M, const int* done) {
+  if (*done) return;
+  const int chunk = blockIdx.x, b = blockIdx.y;
+  const int64_t base = (int64_t)b * M;
+  const T be = beta[b];
+#pragma unroll
+  for (int k = 0; k < UPD_PER_THREAD; ++k) {
+    const int64_t j = (int64_t)chunk * UPD_CHUNK + k * UPD_THREADS + threadIdx.x;
+    if (j < M) {
+      const int64_t o = base + j;
+      p[o] = z[o] + be * p[o];
+    }
+  }
+}
+
+// ---- host launchers ------------------------------------------------------------------------
+template <typename T>
+void cg_init(const void* b, void* x, void* r, int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL((k_cg_init<T>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (const T*)b, (T*)x, (T*)r, n);
+}
+template <typename T>
+void vcopy(const void* src, void* dst, int64_t n, const int* done, hipStream_t s) {
+  hipLaunchKernelGGL((k_copy<T>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (const T*)src, (T*)dst, n, done);
+}
+template <typename T>
+void transpose(const void* in, void* out, int64_t rows, int64_t cols, hipStream_t s) {
+  dim3 grid((unsigned)((cols + 31) / 32), (unsigned)((rows + 31) / 32));
+  hipLaunchKernelGGL((k_transpose<T>), grid, dim3(256), 0, s, (const T*)in, (T*)out, rows, cols);
+}
+template <typename T>
+void rowdot_part(const void* a, const void* c, void* part, int64_t nrhs, int64_t M, int np, hipStream_t s) {
+  dim3 grid((unsigned)np, (unsigned)nrhs);
+  hipLaunchKernelGGL((k_rowdot_part<T>), grid, dim3(UPD_THREADS), 0, s, (const T*)a, (const T*)c, (T*)part, M, np);
+}
+template <typename T>
+void reduce_rows(const void* part, int np, int nrhs, void* out, hipStream_t s) {
+  hipLaunchKernelGGL((k_reduce_rows<T>), dim3((unsigned)((nrhs + 3) / 4)), dim3(256), 0, s, (const T*)part, np, nrhs,
+                     (T*)out);
+}
+template <typename T>
+void cg_alpha(const void* part, int np, int nrhs, const void* rs, void* alpha, const int* done, hipStream_t s) {
+  hipLaunchKernelGGL((k_cg_alpha<T>), dim3((unsigned)((nrhs + 3) / 4)), dim3(256), 0, s, (const T*)part, np, nrhs,
+                     (const T*)rs, (T*)alpha, done);
+}
+template <typename T>
+void cg_update_xr(void* x, void* r, const void* p, const void* Ap, const void* alpha, void* part, int64_t nrhs,
+                  int64_t M, const int* done, hipStream_t s) {
+  const int np = update_np(M);
+  dim3 grid((unsigned)np, (unsigned)nrhs);
+  hipLaunchKernelGGL((k_cg_update_xr<T>), grid, dim3(UPD_THREADS), 0, s, (T*)x, (T*)r, (const T*)p, (const T*)Ap,
+                     (const T*)alpha, (T*)part, M, np, done);
+}
+template <typename T>
+void cg_check(const void* part, int np, int nrhs, double tol, void* rnew, int* done, int* iters, hipStream_t s) {
+  hipLaunchKernelGGL((k_cg_check<T>), dim3(1), dim3(1024), 0, s, (const T*)part, np, nrhs, tol, (T*)rnew, done, iters);
+}
+template <typename T>
+void cg_beta(const void* part, int np, int nrhs, void* rs, void* beta, const int* done, hipStream_t s) {
+  hipLaunchKernelGGL((k_cg_beta<T>), dim3((unsigned)((nrhs + 3) / 4)), dim3(256), 0, s, (const T*)part, np, nrhs,
+                     (T*)rs, (T*)beta, done);
+}
+template <typename T>
+void cg_update_p(void* p, const void* z, const void* beta, int64_t nrhs, int64_t M, const int* done, hipStream_t s) {
+  dim3 grid((unsigned)update_np(M), (unsigned)nrhs);
+  hipLaunchKernelGGL((k_cg_update_p<T>), grid, dim3(UPD_THREADS), 0, s, (T*)p, (const T*)z, (const T*)beta, M, done);
+}
+
+#define HGP_INST(T)                                                                                            \
+  template void cg_init<T>(const void*, void*, void*, int64_t, hipStream_t);                                 \
+  template void vcopy<T>(const void*, void*, int64_t, const int*, hipStream_t);                              \
+  template void transpose<T>(const void*, void*, int64_t, int64_t, hipStream_t);                             \
+  template void rowdot_part<T>(const void*, const void*, void*, int64_t, int64_t, int, hipStream_t);         \
+  template void reduce_rows<T>(const void*, int, int, void*, hipStream_t);                                   \
+  template void cg_alpha<T>(const void*, int, int, const void*, void*, const int*, hipStream_t);             \
+  template void cg_update_xr<T>(void*, void*, const void*, const void*, const void*, void*, int64_t, int64_t, \
+                                const int*, hipStream_t);                                                    \
+  template void cg_check<T>(const void*, int, int, double, void*, int*, int*, hipStream_t);                  \
+  template void cg_beta<T>(const void*, int, int, void*, void*, const int*, hipStream_t);                    \
+  template void cg_update_p<T>(void*, const void*, const void*, int64_t, int64_t, const int*, hipStream_t);
+HGP_INST(float)
+HGP_INST(double)
+#undef HGP_INST
+
+}  // namespace hgp

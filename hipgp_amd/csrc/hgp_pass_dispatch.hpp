@@ -1,0 +1,72 @@
+// hgp_pass_dispatch.hpp — instantiation + launch of k_pass for one dtype (included by
+// hgp_pass_f32.hip / hgp_pass_f64.hip so the two compile in parallel).
+#pragma once
+#include "hgp_internal.hpp"
+
+namespace hgp {
+
+template <typename T, int H, int MODE, int LAY>
+static hipError_t launch_one(const PassDesc& d, int64_t nblocks, hipStream_t s) {
+  using Cfg = PassCfg<T, H, LAY>;
+  static bool attr_set = false;   // opt in to > 64 KB dynamic LDS once per instance
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)k_pass<T, H, MODE, LAY>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((k_pass<T, H, MODE, LAY>), dim3((unsigned)nblocks), dim3(Cfg::THREADS), Cfg::LDS, s, d);
+  return hipGetLastError();
+}
+
+template <typename T, int H>
+static hipError_t launch_h(int mode, int lay, const PassDesc& d, int64_t nblocks, hipStream_t s) {
+  if (mode == PASS_FWD) {
+    if (lay == LAY_STRIDED) return launch_one<T, H, PASS_FWD, LAY_STRIDED>(d, nblocks, s);
+    if (lay == LAY_CONTIG) return launch_one<T, H, PASS_FWD, LAY_CONTIG>(d, nblocks, s);
+    return launch_one<T, H, PASS_FWD, LAY_RP>(d, nblocks, s);
+  }
+  if (mode == PASS_INV) {
+    if (lay == LAY_STRIDED) return launch_one<T, H, PASS_INV, LAY_STRIDED>(d, nblocks, s);
+    if (lay == LAY_CONTIG) return launch_one<T, H, PASS_INV, LAY_CONTIG>(d, nblocks, s);
+    return launch_one<T, H, PASS_INV, LAY_RP>(d, nblocks, s);
+  }
+  if (lay == LAY_STRIDED) return launch_one<T, H, PASS_CONV, LAY_STRIDED>(d, nblocks, s);
+  if (lay == LAY_RP) return launch_one<T, H, PASS_CONV, LAY_RP>(d, nblocks, s);
+  return hipErrorInvalidValue;
+}
+
+template <typename T, int H>
+static PassGeom geom_h(int lay) {
+  PassGeom g;
+  if (lay == LAY_STRIDED) { g.C = PassCfg<T, H, LAY_STRIDED>::C; g.threads = PassCfg<T, H, LAY_STRIDED>::THREADS; g.lds = PassCfg<T, H, LAY_STRIDED>::LDS; }
+  else if (lay == LAY_CONTIG) { g.C = PassCfg<T, H, LAY_CONTIG>::C; g.threads = PassCfg<T, H, LAY_CONTIG>::THREADS; g.lds = PassCfg<T, H, LAY_CONTIG>::LDS; }
+  else { g.C = PassCfg<T, H, LAY_RP>::C; g.threads = PassCfg<T, H, LAY_RP>::THREADS; g.lds = PassCfg<T, H, LAY_RP>::LDS; }
+  return g;
+}
+
+#define HGP_H_SWITCH(FN, ...)                                                                        \
+  switch (H) {                                                                                       \
+    case 2: return FN<T, 2>(__VA_ARGS__);       case 4: return FN<T, 4>(__VA_ARGS__);               \
+    case 8: return FN<T, 8>(__VA_ARGS__);       case 16: return FN<T, 16>(__VA_ARGS__);             \
+    case 32: return FN<T, 32>(__VA_ARGS__);     case 64: return FN<T, 64>(__VA_ARGS__);             \
+    case 128: return FN<T, 128>(__VA_ARGS__);   case 256: return FN<T, 256>(__VA_ARGS__);           \
+    case 512: return FN<T, 512>(__VA_ARGS__);   case 1024: return FN<T, 1024>(__VA_ARGS__);         \
+    case 2048: return FN<T, 2048>(__VA_ARGS__); case 4096: return FN<T, 4096>(__VA_ARGS__);         \
+    case 8192: return FN<T, 8192>(__VA_ARGS__);                                                      \
+    default: break;                                                                                  \
+  }
+
+template <typename T>
+hipError_t launch_pass(int H, int mode, int lay, const PassDesc& d, int64_t nblocks, hipStream_t s) {
+  HGP_H_SWITCH(launch_h, mode, lay, d, nblocks, s)
+  return hipErrorInvalidValue;
+}
+
+template <typename T>
+PassGeom pass_geom(int H, int lay) {
+  HGP_H_SWITCH(geom_h, lay)
+  return PassGeom{0, 0, 0};
+}
+
+}  // namespace hgp

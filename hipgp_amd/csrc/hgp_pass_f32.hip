@@ -1,0 +1,5 @@
+#include "hgp_pass_dispatch.hpp"
+namespace hgp {
+template hipError_t launch_pass<float>(int, int, int, const PassDesc&, int64_t, hipStream_t);
+template PassGeom pass_geom<float>(int, int);
+}

@@ -1,0 +1,144 @@
+"""Python handle on one libhipgp plan (one gridded inducing mesh on one device).
+
+Thin: it turns torch tensors into device pointers and calls the C ABI on torch's current
+stream.  All arithmetic runs in the HIP kernels of libhipgp.so.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check, lib
+
+
+def expanded_dims(dims):
+    """n_i = 2 m_i - 2 (m_i > 1) else m_i  (`hipgp.py:72`)."""
+    return tuple(2 * m - 2 if m > 1 else m for m in dims)
+
+
+class ToeplitzPlan:
+    """Spectra + workspaces for the BTTB operators of one grid (`toeplitz_tensor.py:9-45`)."""
+
+    def __init__(self, dims, dtype=torch.float32, device=None):
+        device = torch.device("cuda") if device is None else torch.device(device)
+        if device.type != "cuda":
+            raise _lib.HipgpError(f"ToeplitzPlan needs a GPU device, got {device} (no CPU fallback)")
+        if device.index is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        self.device = device
+        self.dtype = dtype
+        self.dims = tuple(int(m) for m in dims)
+        self.ndims = expanded_dims(self.dims)
+        self.M = int(np.prod(self.dims))
+        self.Mprime = int(np.prod(self.ndims))
+        m = (ctypes.c_int64 * len(self.dims))(*self.dims)
+        h = ctypes.c_void_p()
+        check(lib().hgp_plan_create(device.index, len(self.dims), m, _lib.dtype_code(dtype), 0,
+                                    _lib.stream_ptr(device), ctypes.byref(h)))
+        self._h = h
+        LK = (ctypes.c_int64 * 3)()
+        LR = (ctypes.c_int64 * 3)()
+        check(lib().hgp_plan_info(h, None, None, LK, LR))
+        self.L_K = tuple(LK)
+        self.L_R = tuple(LR)
+        self.n_clamped = None
+
+    # -- plumbing --------------------------------------------------------------------------
+    def _bind_stream(self):
+        check(lib().hgp_plan_set_stream(self._h, _lib.stream_ptr(self.device)))
+
+    def _vec(self, t, name, ncols):
+        _lib.require_device_tensor(t, name)
+        if t.dtype != self.dtype:
+            raise TypeError(f"{name} has dtype {t.dtype}, plan dtype is {self.dtype}")
+        if t.device != self.device:
+            raise ValueError(f"{name} is on {t.device}, plan on {self.device}")
+        if t.dim() != 2 or t.shape[1] != ncols:
+            raise ValueError(f"{name} must be (nrhs, {ncols}), got {tuple(t.shape)}")
+        return t.contiguous()
+
+    # -- spectrum ----------------------------------------------------------------------------
+    def set_column(self, column, jitter=0.0, clamp_min=1e-6, count_clamped=False):
+        """column: kernel-evaluated first row k(x0, x_j), (M,) on the plan device."""
+        _lib.require_device_tensor(column, "column")
+        col = column.detach().reshape(-1).to(self.dtype).contiguous()
+        if col.numel() != self.M:
+            raise ValueError(f"column has {col.numel()} values, grid has M={self.M}")
+        self._bind_stream()
+        n = ctypes.c_int64(-1)
+        check(lib().hgp_plan_set_column(self._h, ctypes.c_void_p(col.data_ptr()), float(jitter),
+                                        float(clamp_min), ctypes.byref(n) if count_clamped else None))
+        self._col_keepalive = col
+        if count_clamped:
+            self.n_clamped = int(n.value)
+        return self.n_clamped
+
+    def spectrum(self, which=_lib.SPEC_D):
+        """Real clamped spectrum on the expanded grid (shape ndims): D, sqrt(D) or 1/D."""
+        self._bind_stream()
+        out = torch.empty(self.ndims, dtype=self.dtype, device=self.device)
+        check(lib().hgp_get_spectrum(self._h, int(which), ctypes.c_void_p(out.data_ptr())))
+        return out
+
+    # -- operators ---------------------------------------------------------------------------
+    def apply(self, op, x, out=None):
+        nin = self.Mprime if op == _lib.OP_R else self.M
+        nout = self.Mprime if op == _lib.OP_RT else self.M
+        x = self._vec(x, "x", nin)
+        if out is None:
+            out = torch.empty((x.shape[0], nout), dtype=self.dtype, device=self.device)
+        self._bind_stream()
+        check(lib().hgp_toeplitz_apply(self._h, int(op), ctypes.c_void_p(x.data_ptr()),
+                                       ctypes.c_void_p(out.data_ptr()), x.shape[0]))
+        return out
+
+    # -- PCG ---------------------------------------------------------------------------------
+    def pcg(self, b, maxiter, tol, precond=True, out=None, return_iters=False):
+        """Batched PCG with the conj_grad2 recurrence (`cg.py:44-80`), row layout (nrhs, M)."""
+        b = self._vec(b, "b", self.M)
+        x = torch.empty_like(b) if out is None else out
+        self._bind_stream()
+        iters = ctypes.c_int(0)
+        check(lib().hgp_pcg_solve(self._h, ctypes.c_void_p(b.data_ptr()), ctypes.c_void_p(x.data_ptr()),
+                                  b.shape[0], int(maxiter), float(tol), int(bool(precond)),
+                                  _lib.LAYOUT_ROWS, ctypes.byref(iters) if return_iters else None))
+        return (x, iters.value) if return_iters else x
+
+    def pcg_steps(self, b, maxiter, tol, precond=True, callback=None):
+        """Stepwise PCG for the callback form (`cg.py:77-78`): callback(n, x) after every
+        iteration that did not meet the break test; returns x (updated in place)."""
+        b = self._vec(b, "b", self.M)
+        x = torch.empty_like(b)
+        self._bind_stream()
+        check(lib().hgp_pcg_begin(self._h, ctypes.c_void_p(b.data_ptr()), ctypes.c_void_p(x.data_ptr()),
+                                  b.shape[0], int(bool(precond)), _lib.LAYOUT_ROWS))
+        conv = ctypes.c_int(0)
+        for n in range(int(maxiter)):
+            check(lib().hgp_pcg_step(self._h, float(tol), ctypes.byref(conv)))
+            if conv.value:
+                break
+            if callback is not None:
+                callback(n, x)
+        return x
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and _lib._lib is not None:
+            try:
+                lib().hgp_plan_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+
+def rowdot(a, c):
+    """out[b] = sum_j a[b, j] c[b, j] on the device (`cg.py:64` style dots)."""
+    _lib.require_device_tensor(a, "a")
+    a = a.contiguous()
+    c = c.contiguous()
+    out = torch.empty(a.shape[0], dtype=a.dtype, device=a.device)
+    check(lib().hgp_rowdot(_lib.dtype_code(a.dtype), ctypes.c_void_p(a.data_ptr()),
+                           ctypes.c_void_p(c.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                           a.shape[0], a.shape[1], _lib.stream_ptr(a.device)))
+    return out

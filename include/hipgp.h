@@ -1,0 +1,117 @@
+/*
+ * hipgp.h — C ABI of libhipgp.so, the MI355X (gfx950) native structured-kernel PCG path of
+ * HIP-GP (`suyashk12/hipgp`, package `ziggy`).
+ *
+ * The reference has no FFI: its operator boundary is duck-typed Python.
+ * Each entry point below replaces the reference interface named next to it; the Python
+ * drop-in (`hipgp_amd/ziggy/...`, re-exported as `ziggy`) binds them through ctypes
+ * (INTEGRATION.md shows the binding).
+ *
+ * Conventions
+ *  - All data pointers are DEVICE pointers on the plan's device, C-contiguous, in the plan's
+ *    dtype (HGP_F32 = float, HGP_F64 = double).  Caller owns them; nothing is freed across
+ *    the ABI.  Vectors are row layout (nrhs, M) unless a `layout` argument says otherwise.
+ *  - M = prod(m_i); M' = prod(n_i) with n_i = 2 m_i - 2 (m_i > 1) else 1  (`hipgp.py:72`).
+ *  - Calls are asynchronous w.r.t. the host and ordered on the plan's stream, except where a
+ *    host output pointer is passed (that call synchronises the stream).
+ *  - Every function returns 0 on success or a negative HGP_E* code, and sets a thread-local
+ *    message readable with hgp_last_error().  No C++ exception crosses the ABI.
+ */
+#ifndef HIPGP_H
+#define HIPGP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct hgp_plan hgp_plan;
+
+enum { HGP_F32 = 0, HGP_F64 = 1 };
+enum { HGP_OP_K = 0, HGP_OP_CINV = 1, HGP_OP_RT = 2, HGP_OP_R = 3 };
+enum { HGP_SPEC_D = 0, HGP_SPEC_DSQRT = 1, HGP_SPEC_DI = 2 };
+enum { HGP_LAYOUT_ROWS = 0, HGP_LAYOUT_COLS = 1 };
+enum {
+  HGP_OK = 0, HGP_E_ARG = -1, HGP_E_HIP = -2, HGP_E_STATE = -3, HGP_E_UNSUPPORTED = -4,
+  HGP_E_OOM = -5
+};
+
+/* Plan for one gridded inducing mesh m[0..ndim-1] (ndim 1..3, C order, last axis fastest).
+ * Replaces the shape/state part of `ToeplitzTensor.__init__` (toeplitz_tensor.py:9-45) and
+ * `ToeplitzMatmul.__init__` (toeplitz_expanded.py:82-127).  `hip_stream` may be NULL (null
+ * stream).  max_rhs is a capacity hint; workspaces grow on demand. */
+int hgp_plan_create(int device, int ndim, const int64_t* m, int dtype, int64_t max_rhs,
+                    void* hip_stream, hgp_plan** out);
+
+/* Change the stream later calls are ordered on. */
+int hgp_plan_set_stream(hgp_plan* plan, void* hip_stream);
+
+/* Spectrum setup from the kernel-evaluated Toeplitz first column (device, M values):
+ * column[0] += jitter (toeplitz_tensor.py:132; pass 0 when already included), circulant
+ * embedding (toeplitz_tensor.py:135-143), D = clamp(Re FFT(C), clamp_min) (:25-31), and the
+ * operator spectra for K, C^-1 and R/R^T.  Replaces toeplitz_tensor.py:12-33.
+ * If n_clamped != NULL it receives the number of clamped eigenvalues (synchronises). */
+int hgp_plan_set_column(hgp_plan* plan, const void* column, double jitter, double clamp_min,
+                        int64_t* n_clamped);
+
+/* y = op(x) for nrhs right-hand sides, row layout.
+ *   HGP_OP_K    : K v            x:(nrhs,M)  -> y:(nrhs,M)    toeplitz_tensor.py:70-83
+ *   HGP_OP_CINV : C^-1 block v   x:(nrhs,M)  -> y:(nrhs,M)    toeplitz_tensor.py:114-125
+ *   HGP_OP_RT   : R^T v          x:(nrhs,M)  -> y:(nrhs,M')   toeplitz_tensor.py:85-97
+ *   HGP_OP_R    : R w            x:(nrhs,M') -> y:(nrhs,M)    toeplitz_tensor.py:99-112
+ * (same four ops as ToeplitzMatmul.forward "gram"/"circ_inv"/"RTv"/"Rv",
+ *  toeplitz_expanded.py:139-189).  x and y must not alias. */
+int hgp_toeplitz_apply(hgp_plan* plan, int op, const void* x, void* y, int64_t nrhs);
+
+/* Batched PCG, exactly the recurrence of conj_grad2 (cg.py:44-80) for layout ROWS
+ * (b,x:(nrhs,M)) and conj_grad (cg.py:5-41) for layout COLS (b,x:(M,nrhs)): A = K,
+ * preconditioner C^-1 if use_precond, x0 = 0, per-RHS alpha/beta, stop when ALL
+ * sqrt(r.r) < tol after the x/r update.  The early-exit test runs on the device (a flag read
+ * by every later kernel), so the host is not synchronised per iteration.
+ * iters_done (host, may be NULL): number of iterations executed (synchronises).
+ * Replaces ToeplitzTensor._solve (toeplitz_tensor.py:54-68) / InvMatmul.forward. */
+int hgp_pcg_solve(hgp_plan* plan, const void* b, void* x, int64_t nrhs, int maxiter,
+                  double tol, int use_precond, int layout, int* iters_done);
+
+/* Profiling: run only pass `pass` (0-based; -1 = all) of the op's pass sequence (the
+ * intermediate workspace is whatever the previous call left).  hgp_op_pass_count returns the
+ * number of passes (1 for 1-D, 3 for 2-D, 5 for 3-D).  Used by bench.py to time each kernel
+ * with HIP events. */
+int hgp_toeplitz_apply_pass(hgp_plan* plan, int op, const void* x, void* y, int64_t nrhs, int pass);
+int hgp_op_pass_count(const hgp_plan* plan);
+
+/* Stepwise PCG for the callback form of conj_grad/conj_grad2 (cg.py:77-78): begin() sets
+ * x0 = 0, r = b, z = P r, p = z; step() runs one iteration and, if `converged` != NULL,
+ * reports (synchronising) whether the break test fired on it.  x is updated in place in the
+ * caller's buffer given to begin(). */
+int hgp_pcg_begin(hgp_plan* plan, const void* b, void* x, int64_t nrhs, int use_precond,
+                  int layout);
+int hgp_pcg_step(hgp_plan* plan, double tol, int* converged);
+
+/* The clamped spectrum D (which=HGP_SPEC_D), sqrt(D) or 1/D on the full expanded grid
+ * (device, M' reals) — the real parts of ToeplitzTensor.D / D_sqrt / Di
+ * (toeplitz_tensor.py:28-31). */
+int hgp_get_spectrum(hgp_plan* plan, int which, void* out);
+
+/* Per-row dot products out[b] = sum_j a[b,j] c[b,j] (device), used by the generic
+ * conj_grad2 path with caller-supplied A_mul callables (cg.py:64,66,69,74). */
+int hgp_rowdot(int dtype, const void* a, const void* c, void* out, int64_t nrhs, int64_t M,
+               void* hip_stream);
+
+/* Sizes of a plan: M, M' and the padded FFT lengths per axis (K-type and R-type ops). */
+int hgp_plan_info(const hgp_plan* plan, int64_t* M, int64_t* Mprime, int64_t* L_K,
+                  int64_t* L_R);
+
+int hgp_plan_destroy(hgp_plan* plan);
+
+const char* hgp_last_error(void);
+
+/* Library/ABI version string. */
+const char* hgp_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HIPGP_H */

@@ -1,0 +1,200 @@
+"""GPU parity: the HIP path (through the C ABI, via the ziggy drop-in) against the
+reference's golden vectors (tests/golden, made by running /root/reference) and against the
+CPU oracle.  Tolerances:
+  fp32 ops  : max|y - y_ref| <= 1e-5 max|y_ref| + 1e-7, or no worse than 4x the reference's
+              own fp32 error vs fp64 (ops near the clamp, see golden_cases.op_ok)
+  fp32 PCG  : ||x - x64|| <= 4 ||x_ref32 - x64|| + 1e-6 ||x64||
+  fp64      : ops 1e-9 relative to max; PCG 1e-8 (clamped long solves: chaotic, see CLAMPED)
+"""
+import numpy as np
+import pytest
+import torch
+
+from golden_cases import GRID_CASES, CLAMPED, load, grids_of, rel_err, op_ok, pcg_ok
+from oracle import ziggy_oracle as zo
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _kernel(kind, nu, dtype):
+    import ziggy.kernels as zk
+    return zk.SqExp(dtype=dtype) if kind == "sqexp" else zk.Matern(nu=nu, dtype=dtype)
+
+
+def _tt(fx, name, dtype):
+    from ziggy.misc.toeplitz_tensor import ToeplitzTensor
+    kind, nu, params, jit = GRID_CASES[name]
+    k = _kernel(kind, nu, dtype)
+    grids = [torch.tensor(g, dtype=dtype, device=DEV) for g in grids_of(fx)]
+    return ToeplitzTensor(grids, lambda x, y: k.forward(x, y, params=params), jitter_val=jit)
+
+
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+@pytest.mark.parametrize("name", sorted(GRID_CASES))
+@pytest.mark.parametrize("tag", ["f64", "f32"])
+def test_ops_vs_golden(name, tag):
+    dtype = torch.float64 if tag == "f64" else torch.float32
+    fx = load(name, tag)
+    f64 = load(name, "f64")
+    T = _tt(fx, name, dtype)
+    assert rel_err(_np(T.column), fx["column"]) < (1e-12 if tag == "f64" else 2e-6)
+    np.testing.assert_array_equal(_np(T.C), fx["C"])
+    # spectrum (computed in fp64 on the device for both plan dtypes)
+    dtol = 1e-12 if tag == "f64" else 1e-6
+    assert rel_err(_np(T.D[..., 0]), f64["D"]) < dtol
+    assert rel_err(_np(T.D_sqrt[..., 0]).astype(np.float64) ** 2, f64["D_sqrt"] ** 2) < dtol
+    assert rel_err(1 / _np(T.Di[..., 0]).astype(np.float64), 1 / f64["Di"]) < dtol
+    if tag == "f64":
+        assert np.array_equal(_np(T.D[..., 0]) <= 1e-6, fx["D"] <= 1e-6)
+    v = torch.tensor(fx["v"], device=DEV)
+    w = torch.tensor(fx["w"], device=DEV)
+    T.set_batch_shape(v.shape[:-1])
+    for key, fn, x in (("Kv", T._matmul_by_K, v), ("Cinv_v", T._matmul_by_Cinv, v),
+                       ("RTv", T._matmul_by_RT, v), ("Rw", T._matmul_by_R, w)):
+        y = _np(fn(x))
+        assert y.shape == fx[key].shape, key
+        if tag == "f64":
+            assert rel_err(y, fx[key]) < 1e-9, (key, rel_err(y, fx[key]))
+        else:
+            assert op_ok(y, fx[key], f64[key]), (key, rel_err(y, f64[key]), rel_err(fx[key], f64[key]))
+
+
+@pytest.mark.parametrize("name", sorted(GRID_CASES))
+@pytest.mark.parametrize("tag", ["f64", "f32"])
+def test_solves_vs_golden(name, tag):
+    dtype = torch.float64 if tag == "f64" else torch.float32
+    fx = load(name, tag)
+    f64 = load(name, "f64")
+    f32 = load(name, "f32")
+    T = _tt(fx, name, dtype)
+    v = torch.tensor(fx["v"], device=DEV)
+    for mi in (1, 2, 5, 20):
+        key = f"solve_p1_it{mi}"
+        x = _np(T._solve(v, do_precond=True, maxiter=mi, tol=1e-8))
+        chaotic = name in CLAMPED and mi == 20
+        if tag == "f64":
+            assert rel_err(x, f64[key]) < (0.25 if chaotic else 1e-8), (key, rel_err(x, f64[key]))
+        else:
+            ok, (e, eref) = pcg_ok(x, f32[key], f64[key])
+            assert ok or chaotic, (key, e, eref)
+    x = _np(T._solve(v, do_precond=False, maxiter=5, tol=1e-8))
+    if tag == "f64":
+        assert rel_err(x, f64["solve_p0_it5"]) < 1e-8
+    else:
+        assert pcg_ok(x, f32["solve_p0_it5"], f64["solve_p0_it5"])[0]
+    kn = _np(T._matmul_by_RT(T.inv_matmul(v, do_precond=True, maxiter=20, tol=1e-8)))
+    if tag == "f64":
+        assert rel_err(kn, f64["kn_it20"]) < (0.25 if name in CLAMPED else 1e-8)
+    elif name not in CLAMPED:
+        assert pcg_ok(kn, f32["kn_it20"], f64["kn_it20"])[0]
+
+
+@pytest.mark.parametrize("tag", ["f64", "f32"])
+def test_gram_solve_config1(tag):
+    import ziggy.kernels as zk
+    from ziggy.misc import toeplitz_expanded as te
+    dtype = torch.float64 if tag == "f64" else torch.float32
+    fx = load("G1", tag)
+    f64 = load("G1", "f64")
+    k = zk.Matern(nu=2.5, dtype=dtype)
+    kf = lambda x, y: k.forward(x, y, params=(1., .1))
+    g = torch.tensor(fx["grid0"], device=DEV)
+    vec = torch.tensor(fx["vec"], device=DEV)
+    for pre in (0, 1):
+        for rt in (0, 1):
+            for mi in (1, 5, 20):
+                key = f"gram_p{pre}_rt{rt}_it{mi}"
+                its = []
+                res = _np(te.gram_solve([g], kf, vec, maxiter=mi, do_precond=bool(pre), tol=1e-10,
+                                        callback=lambda n, x: its.append(n), mult_RT=bool(rt)))
+                assert res.shape == fx[key].shape
+                if tag == "f64":
+                    # unpreconditioned CG on this ill-conditioned K amplifies rounding
+                    tol = 1e-6 if pre else 1e-3
+                    assert rel_err(res, fx[key]) < tol, (key, rel_err(res, fx[key]))
+                    assert len(its) == int(fx[key + "_ncb"]), (key, len(its))
+                else:
+                    ok, (e, eref) = pcg_ok(res, fx[key], f64[key])
+                    assert ok, (key, e, eref)
+
+
+def test_compute_kn_model_G5():
+    """kn = R^T K^{-1} Knm^T as `hipgp.compute_kn` (hipgp.py:139-146), model-level fixture."""
+    fx = load("G5", "f64")
+    import ziggy.kernels as zk
+    from ziggy.misc.toeplitz_tensor import ToeplitzTensor
+    k = zk.Matern(nu=1.5, dtype=torch.float64)
+    kf = lambda x, y: k.forward(x, y, params=(1., .1))
+    grids = [torch.tensor(fx["grid0"], device=DEV), torch.tensor(fx["grid1"], device=DEV)]
+    T = ToeplitzTensor(grids, kf, batch_shape=None, jitter_val=1e-3)
+    Knm = torch.tensor(fx["Knm"], device=DEV)
+    kn = T._matmul_by_RT(T.inv_matmul(Knm, do_precond=True, maxiter=20, tol=1e-8))
+    assert rel_err(_np(kn), fx["kn"]) < 1e-8
+
+
+# ---- oracle comparisons at sizes the golden set does not cover -----------------------------
+ORACLE_CASES = [
+    ((300,), "matern", 2.5, (1., .05)),
+    ((64, 48), "sqexp", None, (1., .08)),
+    ((33, 17), "matern", 1.5, (1., .2)),
+    ((16, 12, 10), "matern", .5, (1., .3)),
+    ((9, 1, 7), "sqexp", None, (1., .3)),
+]
+
+
+@pytest.mark.parametrize("case", ORACLE_CASES, ids=lambda c: "x".join(map(str, c[0])))
+def test_ops_and_solve_vs_oracle_f64(case):
+    from hipgp_amd import _lib
+    from hipgp_amd.plan import ToeplitzPlan
+    dims, kind, nu, params = case
+    grids = [np.linspace(-1, 1, m) for m in dims]
+    kf = lambda x, y: zo.kernel_eval(kind, x, y, params, nu=nu)
+    col = zo.toeplitz_column(grids, kf, 1e-3)
+    T = zo.ToeplitzOracle(col, dims)
+    P = ToeplitzPlan(dims, torch.float64, DEV)
+    P.set_column(torch.tensor(col, device=DEV))
+    rs = np.random.RandomState(3)
+    B = 5
+    v = rs.randn(B, T.M)
+    w = rs.randn(B, T.Mp)
+    vt = torch.tensor(v, device=DEV)
+    for op, ref in ((_lib.OP_K, T.matmul_K(v)), (_lib.OP_CINV, T.matmul_Cinv(v)), (_lib.OP_RT, T.matmul_RT(v))):
+        assert rel_err(_np(P.apply(op, vt)), ref) < 1e-10, op
+    assert rel_err(_np(P.apply(_lib.OP_R, torch.tensor(w, device=DEV))), T.matmul_R(w)) < 1e-10
+    x = _np(P.pcg(vt, 10, 1e-8, precond=True))
+    assert rel_err(x, T.solve(v, True, 10, 1e-8)) < 1e-7
+
+
+# ---- size-independent properties at BASELINE sizes ------------------------------------------
+@pytest.mark.parametrize("dims", [(1024, 1024), (256, 256, 128)], ids=["C2_1024x1024", "C5_256x256x128"])
+def test_properties_full_size(dims):
+    """R (R^T v) = K v (same clamped spectrum), symmetry <u,Kv> = <Ku,v>, linearity, and PCG
+    residual decrease — at the headline grid sizes, fp32."""
+    import ziggy.kernels as zk
+    from ziggy.misc.toeplitz_tensor import ToeplitzTensor
+    k = zk.SqExp(dtype=torch.float32) if len(dims) == 2 else zk.Matern(nu=2.5, dtype=torch.float32)
+    params = (1., .01) if len(dims) == 2 else (.1, .1)
+    grids = [torch.linspace(-1, 1, m, device=DEV) for m in dims]
+    T = ToeplitzTensor(grids, lambda x, y: k.forward(x, y, params=params), jitter_val=1e-3)
+    g = torch.Generator(device=DEV).manual_seed(0)
+    B = 4
+    u = torch.randn(B, T.M, device=DEV, generator=g)
+    v = torch.randn(B, T.M, device=DEV, generator=g)
+    T.set_batch_shape((B,))
+    Kv = T._matmul_by_K(v)
+    RRv = T._matmul_by_R(T._matmul_by_RT(v))
+    assert float((RRv - Kv).abs().max() / Kv.abs().max()) < 1e-4
+    Ku = T._matmul_by_K(u)
+    lhs = (u.double() * Kv.double()).sum(1)
+    rhs = (Ku.double() * v.double()).sum(1)
+    assert float(((lhs - rhs).abs() / (u.norm(dim=1) * Kv.norm(dim=1)).double()).max()) < 1e-5
+    K2 = T._matmul_by_K(2.0 * u - 3.0 * v)
+    assert float((K2 - (2.0 * Ku - 3.0 * Kv)).abs().max() / K2.abs().max()) < 1e-5
+    x = T._solve(Kv, do_precond=True, maxiter=20, tol=1e-8)
+    res = (T._matmul_by_K(x) - Kv).norm(dim=1) / Kv.norm(dim=1)
+    assert float(res.max()) < 1e-2
