@@ -147,25 +147,32 @@ PassDesc base_desc() {
   return d;
 }
 
-// y = op(x) on RHS [0, nrhs); optional fused dot with `dotv` into partial[b][Rn_last].
+int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
+
+// compact half-spectrum row length of the last (real) axis: >= H+1, 64-byte aligned rows
+int64_t compact_stride(int64_t L) { return round_up(L / 2 + 1, 8); }
+
+// y = op(x) on RHS [0, nrhs); optional fused dot with `dotv` into partial[b][rn_last].
+// Every RHS is processed on its own (no two RHS share an FFT).  only_pass >= 0 runs a single
+// pass of the sequence (profiling).
 template <typename T>
 int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void* dotv, void* partial,
            const int* done, int only_pass = -1) {
   const OpGeom g = op_geom(P, op);
   const int d = P->d;
-  const int64_t Q = (nrhs + 1) / 2;
   const size_t cs = sizeof(C2<T>);
-  // per-pair workspace (complex elements)
+  const int64_t Sl = compact_stride(g.L[d - 1]);
+  // per-RHS workspace (complex elements)
   int64_t B1 = 0, B2 = 0;
-  if (d == 2) B1 = std::max(g.in[0], g.out[0]) * g.L[1];
+  if (d == 2) B1 = std::max(g.in[0], g.out[0]) * Sl;
   if (d == 3) {
-    B1 = std::max(g.in[0] * g.in[1], g.out[0] * g.out[1]) * g.L[2];
-    B2 = std::max(g.in[0], g.out[0]) * g.L[1] * g.L[2];
+    B1 = std::max(g.in[0] * g.in[1], g.out[0] * g.out[1]) * Sl;
+    B2 = std::max(g.in[0], g.out[0]) * g.L[1] * Sl;
   }
-  int64_t Qc = Q;
+  int64_t Qc = nrhs;
   if (B1 + B2 > 0) {
     const int64_t per = (B1 + B2) * (int64_t)cs;
-    Qc = std::max<int64_t>(1, std::min<int64_t>(Q, P->ws_budget / per));
+    Qc = std::max<int64_t>(1, std::min<int64_t>(nrhs, P->ws_budget / per));
     HGP_TRY(P->ws1.ensure((size_t)(B1 * Qc) * cs));
     if (B2) HGP_TRY(P->ws2.ensure((size_t)(B2 * Qc) * cs));
   }
@@ -173,16 +180,21 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
   T* yout = reinterpret_cast<T*>(y);
   const T* dv = reinterpret_cast<const T*>(dotv);
   T* part = reinterpret_cast<T*>(partial);
-  int64_t rn_last = (d == 1) ? 1 : (d == 2 ? g.out[0] : g.out[0] * g.out[1]);
+  const int64_t rows_out = (d == 1) ? 1 : (d == 2 ? g.out[0] : g.out[0] * g.out[1]);
+  const int64_t rn_last = (d == 1) ? 1 : (rows_out + 1) / 2;
 
-  for (int64_t q0 = 0; q0 < Q; q0 += Qc) {
+  for (int64_t q0 = 0; q0 < nrhs; q0 += Qc) {
     int pass_no = 0;
-    const int64_t qn = std::min(Qc, Q - q0);
-    const int nr = (int)std::min<int64_t>(nrhs - 2 * q0, 2 * qn);
-    const T* xi = xin + 2 * q0 * g.in_M;
-    T* yo = yout + 2 * q0 * g.out_M;
-    const T* dvc = dv ? dv + 2 * q0 * g.out_M : nullptr;
-    T* pc = part ? part + 2 * q0 * rn_last : nullptr;
+    auto run = [&](int H, int mode, int lay, PassDesc& D, int64_t lines) -> int {
+      const int me = pass_no++;
+      if (only_pass >= 0 && only_pass != me) return 0;
+      return launch<T>(H, mode, lay, D, lines, P->stream);
+    };
+    const int qn = (int)std::min(Qc, nrhs - q0);
+    const T* xi = xin + q0 * g.in_M;
+    T* yo = yout + q0 * g.out_M;
+    const T* dvc = dv ? dv + q0 * g.out_M : nullptr;
+    T* pc = part ? part + q0 * rn_last : nullptr;
 
     if (d == 1) {
       PassDesc D = base_desc();
@@ -190,75 +202,68 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
       D.out = View{yo, g.out_M, 0, 1, (int)g.out[0]};
       D.dot = dvc; D.partial = pc;
       D.spec = g.spec; D.spec_kind = g.spec_kind; D.spec_i = 0; D.spec_r = 0; D.spec_p = 1;
-      D.tw = g.tw[0].ptr; D.nrhs = nr; D.Q = (int)qn; D.Rn = 1; D.In = 1; D.done = done;
-      if (only_pass < 0 || only_pass == pass_no) HGP_TRY(launch<T>((int)(g.L[0] / 2), PASS_CONV, LAY_RP, D, qn, P->stream));
-      ++pass_no;
+      D.tw = g.tw[0].ptr; D.Q = qn; D.Rn = 1; D.In = 1; D.done = done;
+      HGP_TRY(run((int)(g.L[0] / 2), PASS_CONV, LAY_R1, D, qn));
     } else if (d == 2) {
       C2<T>* w1 = reinterpret_cast<C2<T>*>(P->ws1.ptr);
-      // A: FWD along axis 1 (rows of the real pair) -> w1 [q][i0][k1]
+      const int64_t H1 = g.L[1] / 2;
+      // A: FWD along axis 1, row pairs of each RHS -> compact half spectra w1 [q][i0][c1]
       PassDesc A = base_desc();
       A.in = View{(void*)xi, g.in_M, g.in[1], 1, (int)g.in[1]};
-      A.out = View{w1, B1, g.L[1], 1, (int)g.L[1]};
-      A.tw = g.tw[1].ptr; A.nrhs = nr; A.Q = (int)qn; A.Rn = (int)g.in[0]; A.In = 1; A.done = done;
-      if (only_pass < 0 || only_pass == pass_no) HGP_TRY(launch<T>((int)(g.L[1] / 2), PASS_FWD, LAY_RP, A, qn * g.in[0], P->stream));
-      ++pass_no;
-      // B: CONV along axis 0 (strided columns), in place
+      A.out = View{w1, B1, Sl, 1, 0};
+      A.tw = g.tw[1].ptr; A.Q = qn; A.Rn = (int)((g.in[0] + 1) / 2); A.nrows = (int)g.in[0]; A.done = done;
+      HGP_TRY(run((int)H1, PASS_FWD, LAY_RP, A, (int64_t)qn * A.Rn));
+      // B: CONV along axis 0 (strided columns c1 = 0..H1), in place
       PassDesc Bd = base_desc();
-      Bd.in = View{w1, B1, 0, g.L[1], (int)g.in[0]};
-      Bd.out = View{w1, B1, 0, g.L[1], (int)g.out[0]};
-      Bd.spec = g.spec; Bd.spec_kind = g.spec_kind; Bd.spec_i = 1; Bd.spec_p = g.L[1]; Bd.spec_r = 0;
-      Bd.tw = g.tw[0].ptr; Bd.nrhs = nr; Bd.Q = (int)qn; Bd.Rn = 1; Bd.In = (int)g.L[1]; Bd.done = done;
-      if (only_pass < 0 || only_pass == pass_no) HGP_TRY(launch<T>((int)(g.L[0] / 2), PASS_CONV, LAY_STRIDED, Bd, 0, P->stream));
-      ++pass_no;
-      // C: INV along axis 1 -> real pair rows, crop, fused dot
+      Bd.in = View{w1, B1, 0, Sl, (int)g.in[0]};
+      Bd.out = View{w1, B1, 0, Sl, (int)g.out[0]};
+      Bd.spec = g.spec; Bd.spec_kind = g.spec_kind; Bd.spec_i = 1; Bd.spec_p = Sl; Bd.spec_r = 0;
+      Bd.tw = g.tw[0].ptr; Bd.Q = qn; Bd.Rn = 1; Bd.In = (int)(H1 + 1); Bd.done = done;
+      HGP_TRY(run((int)(g.L[0] / 2), PASS_CONV, LAY_STRIDED, Bd, 0));
+      // C: INV along axis 1: rebuild row pairs, crop, fused dot
       PassDesc Cd = base_desc();
-      Cd.in = View{w1, B1, g.L[1], 1, (int)g.L[1]};
+      Cd.in = View{w1, B1, Sl, 1, (int)g.L[1]};
       Cd.out = View{yo, g.out_M, g.out[1], 1, (int)g.out[1]};
       Cd.dot = dvc; Cd.partial = pc;
-      Cd.tw = g.tw[1].ptr; Cd.nrhs = nr; Cd.Q = (int)qn; Cd.Rn = (int)g.out[0]; Cd.In = 1; Cd.done = done;
-      if (only_pass < 0 || only_pass == pass_no) HGP_TRY(launch<T>((int)(g.L[1] / 2), PASS_INV, LAY_RP, Cd, qn * g.out[0], P->stream));
-      ++pass_no;
+      Cd.tw = g.tw[1].ptr; Cd.Q = qn; Cd.Rn = (int)((g.out[0] + 1) / 2); Cd.nrows = (int)g.out[0]; Cd.done = done;
+      HGP_TRY(run((int)H1, PASS_INV, LAY_RP, Cd, (int64_t)qn * Cd.Rn));
     } else {
       C2<T>* w1 = reinterpret_cast<C2<T>*>(P->ws1.ptr);
       C2<T>* w2 = reinterpret_cast<C2<T>*>(P->ws2.ptr);
-      const int64_t L1 = g.L[1], L2 = g.L[2];
-      // P1: FWD axis 2: real pair rows (i0,i1) -> w1 [q][i0][i1][k2]
+      const int64_t L1 = g.L[1], H2 = g.L[2] / 2;
+      const int64_t rows_in = g.in[0] * g.in[1];
+      // P1: FWD axis 2, row pairs -> w1 [q][i0][i1][c2]
       PassDesc P1 = base_desc();
       P1.in = View{(void*)xi, g.in_M, g.in[2], 1, (int)g.in[2]};
-      P1.out = View{w1, B1, L2, 1, (int)L2};
-      P1.tw = g.tw[2].ptr; P1.nrhs = nr; P1.Q = (int)qn; P1.Rn = (int)(g.in[0] * g.in[1]); P1.In = 1; P1.done = done;
-      if (only_pass < 0 || only_pass == pass_no) HGP_TRY(launch<T>((int)(L2 / 2), PASS_FWD, LAY_RP, P1, qn * g.in[0] * g.in[1], P->stream));
-      ++pass_no;
-      // P2: FWD axis 1 (strided): lines (i0, k2) -> w2 [q][i0][k1][k2]
+      P1.out = View{w1, B1, Sl, 1, 0};
+      P1.tw = g.tw[2].ptr; P1.Q = qn; P1.Rn = (int)((rows_in + 1) / 2); P1.nrows = (int)rows_in; P1.done = done;
+      HGP_TRY(run((int)H2, PASS_FWD, LAY_RP, P1, (int64_t)qn * P1.Rn));
+      // P2: FWD axis 1 (strided): lines (i0, c2) -> w2 [q][i0][k1][c2]
       PassDesc P2 = base_desc();
-      P2.in = View{w1, B1, g.in[1] * L2, L2, (int)g.in[1]};
-      P2.out = View{w2, B2, L1 * L2, L2, (int)L1};
-      P2.tw = g.tw[1].ptr; P2.nrhs = nr; P2.Q = (int)qn; P2.Rn = (int)g.in[0]; P2.In = (int)L2; P2.done = done;
-      if (only_pass < 0 || only_pass == pass_no) HGP_TRY(launch<T>((int)(L1 / 2), PASS_FWD, LAY_STRIDED, P2, 0, P->stream));
-      ++pass_no;
-      // P3: CONV axis 0 (strided, in place): lines (k1,k2)
+      P2.in = View{w1, B1, g.in[1] * Sl, Sl, (int)g.in[1]};
+      P2.out = View{w2, B2, L1 * Sl, Sl, (int)L1};
+      P2.tw = g.tw[1].ptr; P2.Q = qn; P2.Rn = (int)g.in[0]; P2.In = (int)(H2 + 1); P2.done = done;
+      HGP_TRY(run((int)(L1 / 2), PASS_FWD, LAY_STRIDED, P2, 0));
+      // P3: CONV axis 0 (strided, in place): lines (k1, c2)
       PassDesc P3 = base_desc();
-      P3.in = View{w2, B2, 0, L1 * L2, (int)g.in[0]};
-      P3.out = View{w2, B2, 0, L1 * L2, (int)g.out[0]};
-      P3.spec = g.spec; P3.spec_kind = g.spec_kind; P3.spec_i = 1; P3.spec_p = L1 * L2; P3.spec_r = 0;
-      P3.tw = g.tw[0].ptr; P3.nrhs = nr; P3.Q = (int)qn; P3.Rn = 1; P3.In = (int)(L1 * L2); P3.done = done;
-      if (only_pass < 0 || only_pass == pass_no) HGP_TRY(launch<T>((int)(g.L[0] / 2), PASS_CONV, LAY_STRIDED, P3, 0, P->stream));
-      ++pass_no;
-      // P4: INV axis 1 (strided): lines (o0, k2) -> w1 [q][o0][o1][k2]
+      P3.in = View{w2, B2, Sl, L1 * Sl, (int)g.in[0]};
+      P3.out = View{w2, B2, Sl, L1 * Sl, (int)g.out[0]};
+      P3.spec = g.spec; P3.spec_kind = g.spec_kind; P3.spec_i = 1; P3.spec_r = Sl; P3.spec_p = L1 * Sl;
+      P3.tw = g.tw[0].ptr; P3.Q = qn; P3.Rn = (int)L1; P3.In = (int)(H2 + 1); P3.done = done;
+      HGP_TRY(run((int)(g.L[0] / 2), PASS_CONV, LAY_STRIDED, P3, 0));
+      // P4: INV axis 1 (strided): lines (o0, c2) -> w1 [q][o0][o1][c2]
       PassDesc P4 = base_desc();
-      P4.in = View{w2, B2, L1 * L2, L2, (int)L1};
-      P4.out = View{w1, B1, g.out[1] * L2, L2, (int)g.out[1]};
-      P4.tw = g.tw[1].ptr; P4.nrhs = nr; P4.Q = (int)qn; P4.Rn = (int)g.out[0]; P4.In = (int)L2; P4.done = done;
-      if (only_pass < 0 || only_pass == pass_no) HGP_TRY(launch<T>((int)(L1 / 2), PASS_INV, LAY_STRIDED, P4, 0, P->stream));
-      ++pass_no;
-      // P5: INV axis 2: rows (o0,o1) -> real pair, crop, fused dot
+      P4.in = View{w2, B2, L1 * Sl, Sl, (int)L1};
+      P4.out = View{w1, B1, g.out[1] * Sl, Sl, (int)g.out[1]};
+      P4.tw = g.tw[1].ptr; P4.Q = qn; P4.Rn = (int)g.out[0]; P4.In = (int)(H2 + 1); P4.done = done;
+      HGP_TRY(run((int)(L1 / 2), PASS_INV, LAY_STRIDED, P4, 0));
+      // P5: INV axis 2: rebuild row pairs, crop, fused dot
       PassDesc P5 = base_desc();
-      P5.in = View{w1, B1, L2, 1, (int)L2};
+      P5.in = View{w1, B1, Sl, 1, (int)g.L[2]};
       P5.out = View{yo, g.out_M, g.out[2], 1, (int)g.out[2]};
       P5.dot = dvc; P5.partial = pc;
-      P5.tw = g.tw[2].ptr; P5.nrhs = nr; P5.Q = (int)qn; P5.Rn = (int)(g.out[0] * g.out[1]); P5.In = 1; P5.done = done;
-      if (only_pass < 0 || only_pass == pass_no) HGP_TRY(launch<T>((int)(L2 / 2), PASS_INV, LAY_RP, P5, qn * g.out[0] * g.out[1], P->stream));
-      ++pass_no;
+      P5.tw = g.tw[2].ptr; P5.Q = qn; P5.Rn = (int)((rows_out + 1) / 2); P5.nrows = (int)rows_out; P5.done = done;
+      HGP_TRY(run((int)H2, PASS_INV, LAY_RP, P5, (int64_t)qn * P5.Rn));
     }
   }
   return 0;
@@ -272,36 +277,36 @@ int fwd_grid_f64(hgp_plan* P, const int64_t* L, const DevBuf* tw64, double2* a, 
     PassDesc D = base_desc();
     D.in = View{a, L[0], 0, 1, (int)L[0]};
     D.out = View{b, L[0], 0, 1, (int)L[0]};
-    D.tw = tw64[0].ptr; D.Q = 1; D.Rn = 1; D.In = 1; D.nrhs = 2;
+    D.tw = tw64[0].ptr; D.Q = 1; D.Rn = 1; D.In = 1;
     HGP_TRY(launch<double>((int)(L[0] / 2), PASS_FWD, LAY_CONTIG, D, 1, s));
     *result = b;
   } else if (d == 2) {
     PassDesc A = base_desc();
     A.in = View{a, 0, L[1], 1, (int)L[1]};
     A.out = View{b, 0, L[1], 1, (int)L[1]};
-    A.tw = tw64[1].ptr; A.Q = 1; A.Rn = (int)L[0]; A.In = 1; A.nrhs = 2;
+    A.tw = tw64[1].ptr; A.Q = 1; A.Rn = (int)L[0]; A.In = 1;
     HGP_TRY(launch<double>((int)(L[1] / 2), PASS_FWD, LAY_CONTIG, A, L[0], s));
     PassDesc Bd = base_desc();
     Bd.in = View{b, 0, 0, L[1], (int)L[0]};
     Bd.out = View{a, 0, 0, L[1], (int)L[0]};
-    Bd.tw = tw64[0].ptr; Bd.Q = 1; Bd.Rn = 1; Bd.In = (int)L[1]; Bd.nrhs = 2;
+    Bd.tw = tw64[0].ptr; Bd.Q = 1; Bd.Rn = 1; Bd.In = (int)L[1];
     HGP_TRY(launch<double>((int)(L[0] / 2), PASS_FWD, LAY_STRIDED, Bd, 0, s));
     *result = a;
   } else {
     PassDesc A = base_desc();
     A.in = View{a, 0, L[2], 1, (int)L[2]};
     A.out = View{b, 0, L[2], 1, (int)L[2]};
-    A.tw = tw64[2].ptr; A.Q = 1; A.Rn = (int)(L[0] * L[1]); A.In = 1; A.nrhs = 2;
+    A.tw = tw64[2].ptr; A.Q = 1; A.Rn = (int)(L[0] * L[1]); A.In = 1;
     HGP_TRY(launch<double>((int)(L[2] / 2), PASS_FWD, LAY_CONTIG, A, L[0] * L[1], s));
     PassDesc Bd = base_desc();
     Bd.in = View{b, 0, L[1] * L[2], L[2], (int)L[1]};
     Bd.out = View{a, 0, L[1] * L[2], L[2], (int)L[1]};
-    Bd.tw = tw64[1].ptr; Bd.Q = 1; Bd.Rn = (int)L[0]; Bd.In = (int)L[2]; Bd.nrhs = 2;
+    Bd.tw = tw64[1].ptr; Bd.Q = 1; Bd.Rn = (int)L[0]; Bd.In = (int)L[2];
     HGP_TRY(launch<double>((int)(L[1] / 2), PASS_FWD, LAY_STRIDED, Bd, 0, s));
     PassDesc Cd = base_desc();
     Cd.in = View{a, 0, 0, L[1] * L[2], (int)L[0]};
     Cd.out = View{b, 0, 0, L[1] * L[2], (int)L[0]};
-    Cd.tw = tw64[0].ptr; Cd.Q = 1; Cd.Rn = 1; Cd.In = (int)(L[1] * L[2]); Cd.nrhs = 2;
+    Cd.tw = tw64[0].ptr; Cd.Q = 1; Cd.Rn = 1; Cd.In = (int)(L[1] * L[2]);
     HGP_TRY(launch<double>((int)(L[0] / 2), PASS_FWD, LAY_STRIDED, Cd, 0, s));
     *result = b;
   }
@@ -384,14 +389,18 @@ int set_column_t(hgp_plan* P, const void* column, double jitter, double clamp_mi
   embed_K(cK, cI, g1, gd, s);
   double2* F = nullptr;
   HGP_TRY(fwd_grid_f64(P, P->LK, P->tw64K, g1, g2, &F));
-  HGP_TRY(P->specK.ensure((size_t)P->prodLK * sizeof(T)));
-  HGP_TRY(P->specI.ensure((size_t)P->prodLK * sizeof(T)));
-  extract_pair<T>(F, P->specK.ptr, P->specI.ptr, P->prodLK, 1.0 / (double)P->prodLK, s);
+  const int compact = d > 1 ? 1 : 0;
+  const int64_t LKl = P->LK[d - 1], LRl = P->LR[d - 1];
+  const int64_t SK = compact ? compact_stride(LKl) : LKl, SR = compact ? compact_stride(LRl) : LRl;
+  const int64_t nK = P->prodLK / LKl * SK, nR = P->prodLR / LRl * SR;
+  HGP_TRY(P->specK.ensure((size_t)nK * sizeof(T)));
+  HGP_TRY(P->specI.ensure((size_t)nK * sizeof(T)));
+  extract_pair<T>(F, P->specK.ptr, P->specI.ptr, nK, LKl, SK, compact, 1.0 / (double)P->prodLK, s);
   for (int ax = 0; ax < 3; ++ax) gd.L[ax] = P->LR[ax];
   embed_R(sv, g1, gd, s);
   HGP_TRY(fwd_grid_f64(P, P->LR, P->tw64R, g1, g2, &F));
-  HGP_TRY(P->specR.ensure((size_t)P->prodLR * sizeof(C2<T>)));
-  extract_cplx<T>(F, P->specR.ptr, P->prodLR, 1.0 / (double)P->prodLR, s);
+  HGP_TRY(P->specR.ensure((size_t)nR * sizeof(C2<T>)));
+  extract_cplx<T>(F, P->specR.ptr, nR, LRl, SR, compact, 1.0 / (double)P->prodLR, s);
   HIP_TRY(hipGetLastError());
   P->have_spec = true;
   if (n_clamped) {
@@ -406,8 +415,8 @@ int set_column_t(hgp_plan* P, const void* column, double jitter, double clamp_mi
 // ---- PCG -------------------------------------------------------------------------------------
 int rn_last(const hgp_plan* P) {
   if (P->d == 1) return 1;
-  if (P->d == 2) return (int)P->m[0];
-  return (int)(P->m[0] * P->m[1]);
+  if (P->d == 2) return (int)((P->m[0] + 1) / 2);
+  return (int)((P->m[0] * P->m[1] + 1) / 2);
 }
 
 template <typename T>

@@ -22,8 +22,10 @@ void clamp_spectrum(const double* Draw, double* out3, int64_t M, double clamp_mi
                     hipStream_t s);
 void embed_K(const double* cK, const double* cI, double2* out, const GridDims& g, hipStream_t s);
 void embed_R(const double* sv, double2* out, const GridDims& g, hipStream_t s);
-template <typename T> void extract_pair(const double2* F, void* a, void* b, int64_t n, double scale, hipStream_t s);
-template <typename T> void extract_cplx(const double2* F, void* o, int64_t n, double scale, hipStream_t s);
+template <typename T> void extract_pair(const double2* F, void* a, void* b, int64_t n, int64_t L, int64_t S, int compact,
+                                        double scale, hipStream_t s);
+template <typename T> void extract_cplx(const double2* F, void* o, int64_t n, int64_t L, int64_t S, int compact, double scale,
+                                        hipStream_t s);
 template <typename T> void expand_spec(const double* src, void* out, const GridDims& g, hipStream_t s);
 
 // CG

@@ -1,47 +1,52 @@
 // hgp_pass.hpp — one axis pass of a batched multi-dimensional Toeplitz convolution.
 //
 // A "pass" runs length-L = 2H transforms along one axis for a batch of lines:
-//   FWD  : load (pad/fold) -> forward FFT -> store both frequency halves      (first axes)
-//   INV  : load both halves -> inverse FFT -> combine, crop -> store           (last axes)
-//   CONV : load -> forward -> x spectrum -> inverse -> crop -> store           (axis 0)
-// Two right-hand sides b = 2q, 2q+1 travel together as the real and imaginary parts of one
-// complex line ("real pair"): every operator here is a convolution with a REAL filter, so
-// the two never mix (Re -> op(v_2q), Im -> op(v_2q+1)).
+//   FWD  : load (pad/fold) -> forward FFT -> store the frequencies                (first axes)
+//   INV  : load frequencies -> inverse FFT -> combine halves, crop -> store         (last axes)
+//   CONV : load -> forward -> x spectrum -> inverse -> crop -> store                (axis 0)
+//
+// Real data never shares a complex FFT with another right-hand side: the last (real) axis
+// packs two ROWS OF THE SAME RHS as Re/Im (rows 2j, 2j+1), splits them after the forward
+// transform by Hermitian symmetry and stores each row's half spectrum ("compact" columns
+// c = 0..H: even frequencies 2c for c <= H/2, odd 2(c-H/2-1)+1 after).  The inverse rebuilds
+// the pair from the two half spectra.  Rounding therefore only couples values of one RHS
+// (error ~ eps*||v_b||, like a plain 2-D FFT), never two RHS.
 //
 // Layouts (compile time):
 //   LAY_STRIDED : complex lines along a non-last axis; C adjacent lines per block, threads
 //                 line-fast so each position is one coalesced C*8-byte row segment.
-//   LAY_CONTIG  : complex lines along the last axis; threads position-fast.
-//   LAY_RP      : last axis of the (nrhs, M) real vectors: the pair (2q, 2q+1) is loaded
-//                 /stored as two real rows (input of FWD/CONV, output of INV/CONV).
+//   LAY_CONTIG  : complex lines along the last axis; threads position-fast (setup grids).
+//   LAY_RP      : last axis of (nrhs, M) real vectors, row pair (2j, 2j+1) of RHS q
+//                 <-> two compact half-spectrum rows (FWD input / INV output).
+//   LAY_R1      : 1-D: one real line per RHS (z = x + 0i), CONV only.
 #pragma once
 #include "hgp_fft.hpp"
 
 namespace hgp {
 
 enum { PASS_FWD = 0, PASS_INV = 1, PASS_CONV = 2 };
-enum { LAY_STRIDED = 0, LAY_CONTIG = 1, LAY_RP = 2 };
+enum { LAY_STRIDED = 0, LAY_CONTIG = 1, LAY_RP = 2, LAY_R1 = 3 };
 enum { SPEC_REAL = 0, SPEC_CPLX = 1, SPEC_CPLX_CONJ = 2 };
 
 struct View {
   void* ptr;
-  int64_t q_stride;           // per pair (complex elems) / per RHS row (reals, LAY_RP: row b)
-  int64_t r_stride;           // per outer line index r
-  int64_t p_stride;           // per position (complex views; 1 for contiguous)
+  int64_t q_stride;           // per RHS (LAY_RP/R1 real side: M; complex side: rows*S)
+  int64_t r_stride;           // per outer line index r (LAY_RP: per ROW, not per pair)
+  int64_t p_stride;           // per position (strided complex views; 1 otherwise)
   int len;                    // valid length along the axis (input: in_len, output: out_len)
 };
 
 struct PassDesc {
   View in, out;
-  const void* dot;            // optional: second operand (same layout as `out`, LAY_RP only)
-  void* partial;              // fused dot partials [b][Rn]
+  const void* dot;            // optional: second operand (same layout as the real `out`)
+  void* partial;              // fused dot partials [q][Rn]
   const void* spec;           // CONV: spectrum at i*spec_i + r*spec_r + kperm*spec_p
   int64_t spec_i, spec_p, spec_r;
   int spec_kind;
   const void* tw;             // W_L^q, q < L (forward sign)
-  int nrhs;                   // valid RHS count (pairs: b = 2q, 2q+1)
-  int Q;                      // pairs
-  int Rn, In;                 // lines per pair: r in [0,Rn) (outer), i in [0,In) (inner, strided)
+  int Q;                      // right-hand sides (setup grids: 1)
+  int Rn, In;                 // lines per RHS: r in [0,Rn) (outer), i in [0,In) (inner, strided)
+  int nrows;                  // LAY_RP: real rows per RHS (the pair (2r, 2r+1) needs 2r+1 < nrows)
   const int* done;            // optional device flag: skip the pass when *done != 0
 };
 
@@ -61,7 +66,7 @@ template <typename T, int H, int LAY> struct PassCfg {
   }
   static constexpr int C = (LAY == LAY_STRIDED) ? c_strided() : c_contig();
   static constexpr int THREADS = C * TT;
-  static constexpr int LDS_FFT = (TT > 1) ? lds_bytes_for(C) : 0;
+  static constexpr int LDS_FFT = (TT > 1 || LAY == LAY_RP) ? lds_bytes_for(C) : 0;
   static constexpr int LDS_RED = THREADS * 2 * (int)sizeof(T);
   static constexpr int LDS = LDS_FFT > LDS_RED ? LDS_FFT : LDS_RED;
 };
@@ -77,7 +82,7 @@ __device__ __forceinline__ C2<T> spec_mul(int kind, const void* spec, int64_t so
 }
 
 // Bijective XCD-aware remap: blocks dealt to the same XCD (b mod 8) get consecutive logical
-// ids, so the pairs q of one strided line group (same spectrum slab) run on one XCD and share
+// ids, so the RHS q of one strided line group (same spectrum slab) run on one XCD and share
 // its L2.  Speed only, never correctness.
 __device__ __forceinline__ int xcd_remap(int b, int nb) {
   const int x = b & 7, qq = nb >> 3, rr = nb & 7;
@@ -85,12 +90,20 @@ __device__ __forceinline__ int xcd_remap(int b, int nb) {
   return start + (b >> 3);
 }
 
+// compact half-spectrum column of frequency half h, position p (valid for the stored range)
+template <int H>
+__device__ __forceinline__ int compact_col(int h, int p) { return h == 0 ? p : H / 2 + 1 + p; }
+
 template <typename T, int H, int MODE, int LAY>
 __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS)) void k_pass(const PassDesc d) {
   using Cfg = PassCfg<T, H, LAY>;
   constexpr int P = Cfg::P, TT = Cfg::TT, C = Cfg::C;
-  constexpr bool RP_IN = (LAY == LAY_RP) && (MODE != PASS_INV);
-  constexpr bool RP_OUT = (LAY == LAY_RP) && (MODE != PASS_FWD);
+  constexpr bool RP_IN = (LAY == LAY_RP) && (MODE == PASS_FWD);     // real row pair in
+  constexpr bool RP_OUT = (LAY == LAY_RP) && (MODE == PASS_INV);    // real row pair out
+  constexpr bool HERM_IN = RP_OUT;                                   // compact half spectra in
+  constexpr bool HERM_OUT = RP_IN;                                   // compact half spectra out
+  constexpr bool R1 = (LAY == LAY_R1);
+  constexpr bool REAL_OUT = RP_OUT || R1;
   if (d.done != nullptr && *d.done) return;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   C2<T>* lds = reinterpret_cast<C2<T>*>(smem_raw);
@@ -102,7 +115,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS)) void k_pass(const Pa
   if constexpr (LAY == LAY_STRIDED) { t = tid / C; l = tid - t * C; lbase = l; }
   else { l = tid / TT; t = tid - l * TT; lbase = l * H; }
 
-  // ---- line coordinates (q, r, i) ----
+  // ---- line coordinates (q = RHS, r = outer line, i = inner line) ----
   int q, r, i;
   bool valid;
   if constexpr (LAY == LAY_STRIDED) {
@@ -122,20 +135,32 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS)) void k_pass(const Pa
     valid = q < d.Q;
     if (!valid) { q = 0; r = 0; }
   }
-  const bool has_b = (2 * q + 1 < d.nrhs);   // second member of the pair exists
+  const bool has2 = (LAY == LAY_RP) ? (2 * r + 1 < d.nrows) : false;   // second row of the pair
 
-  // ---- base pointers (64-bit, per line) ----
-  const T* in_re = nullptr; const T* in_im = nullptr; const C2<T>* in_c = nullptr;
+  // ---- base pointers ----
+  const T* in_re = nullptr; const T* in_im = nullptr;       // real inputs
+  const C2<T>* in_c = nullptr; const C2<T>* in_c2 = nullptr; // complex inputs (row b: in_c2)
   if constexpr (RP_IN) {
-    in_re = reinterpret_cast<const T*>(d.in.ptr) + (int64_t)(2 * q) * d.in.q_stride + (int64_t)r * d.in.r_stride;
-    in_im = in_re + d.in.q_stride;
+    in_re = reinterpret_cast<const T*>(d.in.ptr) + (int64_t)q * d.in.q_stride + (int64_t)(2 * r) * d.in.r_stride;
+    in_im = has2 ? in_re + d.in.r_stride : in_re;
+  } else if constexpr (R1) {
+    in_re = reinterpret_cast<const T*>(d.in.ptr) + (int64_t)q * d.in.q_stride;
+  } else if constexpr (HERM_IN) {
+    in_c = reinterpret_cast<const C2<T>*>(d.in.ptr) + (int64_t)q * d.in.q_stride + (int64_t)(2 * r) * d.in.r_stride;
+    in_c2 = has2 ? in_c + d.in.r_stride : in_c;
   } else {
     in_c = reinterpret_cast<const C2<T>*>(d.in.ptr) + (int64_t)q * d.in.q_stride + (int64_t)r * d.in.r_stride + i;
   }
-  T* out_re = nullptr; T* out_im = nullptr; C2<T>* out_c = nullptr;
+  T* out_re = nullptr; T* out_im = nullptr;
+  C2<T>* out_c = nullptr; C2<T>* out_c2 = nullptr;
   if constexpr (RP_OUT) {
-    out_re = reinterpret_cast<T*>(d.out.ptr) + (int64_t)(2 * q) * d.out.q_stride + (int64_t)r * d.out.r_stride;
-    out_im = out_re + d.out.q_stride;
+    out_re = reinterpret_cast<T*>(d.out.ptr) + (int64_t)q * d.out.q_stride + (int64_t)(2 * r) * d.out.r_stride;
+    out_im = out_re + d.out.r_stride;
+  } else if constexpr (R1) {
+    out_re = reinterpret_cast<T*>(d.out.ptr) + (int64_t)q * d.out.q_stride;
+  } else if constexpr (HERM_OUT) {
+    out_c = reinterpret_cast<C2<T>*>(d.out.ptr) + (int64_t)q * d.out.q_stride + (int64_t)(2 * r) * d.out.r_stride;
+    out_c2 = out_c + d.out.r_stride;
   } else {
     out_c = reinterpret_cast<C2<T>*>(d.out.ptr) + (int64_t)q * d.out.q_stride + (int64_t)r * d.out.r_stride + i;
   }
@@ -144,21 +169,33 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS)) void k_pass(const Pa
 
   // Loads are unconditional on clamped (always in-bounds) addresses and zeroed afterwards:
   // a per-element branch around a load makes hipcc wait vmcnt(0) per element.
-  const T* in_im_safe = nullptr;
-  if constexpr (RP_IN) in_im_safe = has_b ? in_im : in_re;
   auto load_in = [&](int p) -> C2<T> {
     if constexpr (RP_IN) {
       const T re = in_re[p];
-      const T im = in_im_safe[p];
-      return mk<T>(re, has_b ? im : (T)0);
+      const T im = in_im[p];
+      return mk<T>(re, has2 ? im : (T)0);
+    } else if constexpr (R1) {
+      return mk<T>(in_re[p], (T)0);
     } else {
       return in_c[(int64_t)p * ips];
     }
   };
+  // Hermitian rebuild of Z = A + iB at frequency half h, position p from the two compact rows
+  auto load_herm = [&](int h, int p) -> C2<T> {
+    bool cj;
+    int c;
+    if (h == 0) { cj = p > H / 2; c = cj ? H - p : p; }
+    else { cj = p >= H / 2; c = H / 2 + 1 + (cj ? H - 1 - p : p); }
+    C2<T> A = in_c[c];
+    C2<T> B = in_c2[c];
+    if (!has2) B = mk<T>(0, 0);
+    if (cj) { A.y = -A.y; B.y = -B.y; }
+    return mk<T>(A.x - B.y, A.y + B.x);
+  };
 
   C2<T> v[P];
   C2<T> keep[P];   // FWD/CONV: odd-half input; INV/CONV: even-half output
-  T dsum_a = 0, dsum_b = 0;
+  T dsum = 0;
 
   if constexpr (MODE == PASS_FWD || MODE == PASS_CONV) {
     const int in_len = d.in.len;
@@ -186,7 +223,10 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS)) void k_pass(const Pa
     }
   } else {
 #pragma unroll
-    for (int k = 0; k < P; ++k) v[k] = load_in(t + TT * k);
+    for (int k = 0; k < P; ++k) {
+      if constexpr (HERM_IN) v[k] = load_herm(0, t + TT * k);
+      else v[k] = load_in(t + TT * k);
+    }
   }
 
 #pragma unroll 1
@@ -197,7 +237,27 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS)) void k_pass(const Pa
         for (int k = 0; k < P; ++k) v[k] = keep[k];
       }
       fft_line<T, H, P, -1, LSTRIDE>(v, lds, lbase, t, twL);
-      if (valid) {
+      if constexpr (HERM_OUT) {
+        // split Z = X_a + i X_b by Hermitian symmetry: partner of position p is
+        // (H - p) mod H in the even half and H - 1 - p in the odd half.
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < P; ++k) lds[lds_phys(lbase + t + TT * k)] = v[k];
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+          const int p = t + TT * k;
+          const int pp = (half == 0) ? ((H - p) & (H - 1)) : (H - 1 - p);
+          const C2<T> zp = lds[lds_phys(lbase + pp)];
+          const bool store = (half == 0) ? (p <= H / 2) : (p < H / 2);
+          if (valid && store) {
+            const int c = compact_col<H>(half, p);
+            const T hf = (T)0.5;
+            out_c[c] = mk<T>(hf * (v[k].x + zp.x), hf * (v[k].y - zp.y));               // (Z + conj Zp)/2
+            if (has2) out_c2[c] = mk<T>(hf * (v[k].y + zp.y), -hf * (v[k].x - zp.x));  // (Z - conj Zp)/2i
+          }
+        }
+      } else if (valid) {
 #pragma unroll
         for (int k = 0; k < P; ++k) out_c[(int64_t)(half * H + t + TT * k) * ops] = v[k];
       }
@@ -212,7 +272,8 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS)) void k_pass(const Pa
 #pragma unroll
           for (int k = 0; k < P; ++k) {
             keep[k] = v[k];
-            v[k] = load_in(H + t + TT * k);
+            if constexpr (HERM_IN) v[k] = load_herm(1, t + TT * k);
+            else v[k] = load_in(H + t + TT * k);
           }
         }
       }
@@ -226,10 +287,10 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS)) void k_pass(const Pa
         // y[p] = ye + conj(W_L^p) yo ;  y[p+H] = ye - conj(W_L^p) yo ; crop to out_len
         const int out_len = d.out.len;
         const T* dot_re = nullptr; const T* dot_im = nullptr;
-        if constexpr (RP_OUT) {
+        if constexpr (REAL_OUT) {
           if (d.partial != nullptr) {
-            dot_re = reinterpret_cast<const T*>(d.dot) + (int64_t)(2 * q) * d.out.q_stride + (int64_t)r * d.out.r_stride;
-            dot_im = dot_re + d.out.q_stride;
+            dot_re = reinterpret_cast<const T*>(d.dot) + (out_re - reinterpret_cast<T*>(d.out.ptr));
+            dot_im = dot_re + d.out.r_stride;
           }
         }
 #pragma unroll
@@ -243,12 +304,14 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS)) void k_pass(const Pa
             const int pp = p + s2 * H;
             const C2<T> y = s2 ? y1 : y0;
             if (valid && pp < out_len) {
-              if constexpr (RP_OUT) {
+              if constexpr (REAL_OUT) {
                 out_re[pp] = y.x;
-                if (has_b) out_im[pp] = y.y;
-                if (dot_re != nullptr) {
-                  dsum_a += y.x * dot_re[pp];
-                  if (has_b) dsum_b += y.y * dot_im[pp];
+                if (dot_re != nullptr) dsum += y.x * dot_re[pp];
+                if constexpr (RP_OUT) {
+                  if (has2) {
+                    out_im[pp] = y.y;
+                    if (dot_re != nullptr) dsum += y.y * dot_im[pp];
+                  }
                 }
               } else {
                 out_c[(int64_t)pp * ops] = y;
@@ -260,21 +323,18 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS)) void k_pass(const Pa
     }
   }
 
-  if constexpr (RP_OUT) {
+  if constexpr (REAL_OUT) {
     if (d.partial != nullptr) {
-      // per-line fused dot: every thread parks its two partial sums, the line's first
-      // thread adds them in fixed order (deterministic) and writes partial[b][r].
+      // per-line fused dot: every thread parks its partial sum, the line's first thread adds
+      // them in fixed order (deterministic) and writes partial[q][r].
       T* red = reinterpret_cast<T*>(smem_raw);
       __syncthreads();
-      red[2 * tid] = dsum_a;
-      red[2 * tid + 1] = dsum_b;
+      red[tid] = dsum;
       __syncthreads();
       if (t == 0 && valid) {
-        T sa = 0, sb = 0;
-        for (int k = 0; k < TT; ++k) { sa += red[2 * (tid + k)]; sb += red[2 * (tid + k) + 1]; }
-        T* part = reinterpret_cast<T*>(d.partial);
-        part[(int64_t)(2 * q) * d.Rn + r] = sa;
-        if (has_b) part[(int64_t)(2 * q + 1) * d.Rn + r] = sb;
+        T s = 0;
+        for (int k = 0; k < TT; ++k) s += red[tid + k];
+        reinterpret_cast<T*>(d.partial)[(int64_t)q * d.Rn + r] = s;
       }
     }
   }

@@ -24,25 +24,28 @@ static hipError_t launch_h(int mode, int lay, const PassDesc& d, int64_t nblocks
   if (mode == PASS_FWD) {
     if (lay == LAY_STRIDED) return launch_one<T, H, PASS_FWD, LAY_STRIDED>(d, nblocks, s);
     if (lay == LAY_CONTIG) return launch_one<T, H, PASS_FWD, LAY_CONTIG>(d, nblocks, s);
-    return launch_one<T, H, PASS_FWD, LAY_RP>(d, nblocks, s);
-  }
-  if (mode == PASS_INV) {
+    if (lay == LAY_RP) return launch_one<T, H, PASS_FWD, LAY_RP>(d, nblocks, s);
+  } else if (mode == PASS_INV) {
     if (lay == LAY_STRIDED) return launch_one<T, H, PASS_INV, LAY_STRIDED>(d, nblocks, s);
-    if (lay == LAY_CONTIG) return launch_one<T, H, PASS_INV, LAY_CONTIG>(d, nblocks, s);
-    return launch_one<T, H, PASS_INV, LAY_RP>(d, nblocks, s);
+    if (lay == LAY_RP) return launch_one<T, H, PASS_INV, LAY_RP>(d, nblocks, s);
+  } else {
+    if (lay == LAY_STRIDED) return launch_one<T, H, PASS_CONV, LAY_STRIDED>(d, nblocks, s);
+    if (lay == LAY_R1) return launch_one<T, H, PASS_CONV, LAY_R1>(d, nblocks, s);
   }
-  if (lay == LAY_STRIDED) return launch_one<T, H, PASS_CONV, LAY_STRIDED>(d, nblocks, s);
-  if (lay == LAY_RP) return launch_one<T, H, PASS_CONV, LAY_RP>(d, nblocks, s);
   return hipErrorInvalidValue;
+}
+
+template <typename T, int H, int LAY>
+static PassGeom geom_one() {
+  return PassGeom{PassCfg<T, H, LAY>::C, PassCfg<T, H, LAY>::THREADS, PassCfg<T, H, LAY>::LDS};
 }
 
 template <typename T, int H>
 static PassGeom geom_h(int lay) {
-  PassGeom g;
-  if (lay == LAY_STRIDED) { g.C = PassCfg<T, H, LAY_STRIDED>::C; g.threads = PassCfg<T, H, LAY_STRIDED>::THREADS; g.lds = PassCfg<T, H, LAY_STRIDED>::LDS; }
-  else if (lay == LAY_CONTIG) { g.C = PassCfg<T, H, LAY_CONTIG>::C; g.threads = PassCfg<T, H, LAY_CONTIG>::THREADS; g.lds = PassCfg<T, H, LAY_CONTIG>::LDS; }
-  else { g.C = PassCfg<T, H, LAY_RP>::C; g.threads = PassCfg<T, H, LAY_RP>::THREADS; g.lds = PassCfg<T, H, LAY_RP>::LDS; }
-  return g;
+  if (lay == LAY_STRIDED) return geom_one<T, H, LAY_STRIDED>();
+  if (lay == LAY_CONTIG) return geom_one<T, H, LAY_CONTIG>();
+  if (lay == LAY_RP) return geom_one<T, H, LAY_RP>();
+  return geom_one<T, H, LAY_R1>();
 }
 
 #define HGP_H_SWITCH(FN, ...)                                                                        \
