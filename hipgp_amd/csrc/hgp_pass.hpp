@@ -53,22 +53,32 @@ struct PassDesc {
 template <typename T, int H, int LAY> struct PassCfg {
   static constexpr int P = (H < PMax<T>::v) ? H : PMax<T>::v;
   static constexpr int TT = H / P;
-  static constexpr int lds_bytes_for(int c) { return (c * H + ((c * H) >> 4)) * (int)sizeof(C2<T>); }
+  // LDS image of C lines of one frequency half (H complex each, 1 pad slot per 16)
+  static constexpr int half_elems(int c) { return c * H + ((c * H) >> 4); }
+  static constexpr int lds_bytes_for(int c) { return 2 * half_elems(c) * (int)sizeof(C2<T>); }
   static constexpr int c_strided() {
     int c = 64;
-    while (c > 1 && (c * TT > 512 || lds_bytes_for(c) > 140 * 1024)) c >>= 1;
+    while (c > 1 && (2 * c * TT > 1024 || lds_bytes_for(c) > 140 * 1024)) c >>= 1;
     return c;
   }
   static constexpr int c_contig() {
-    int c = (TT >= 256) ? 1 : 256 / TT;
-    while (c > 1 && lds_bytes_for(c) > 64 * 1024) c >>= 1;
+    int c = (2 * TT >= 512) ? 1 : 512 / (2 * TT);
+    while (c > 1 && lds_bytes_for(c) > 72 * 1024) c >>= 1;
     return c;
   }
   static constexpr int C = (LAY == LAY_STRIDED) ? c_strided() : c_contig();
-  static constexpr int THREADS = C * TT;
-  static constexpr int LDS_FFT = (TT > 1 || LAY == LAY_RP) ? lds_bytes_for(C) : 0;
-  static constexpr int LDS_RED = THREADS * 2 * (int)sizeof(T);
+  static constexpr int GROUP = C * TT;           // threads of one frequency half
+  static constexpr int THREADS = 2 * GROUP;      // even-half group + odd-half group
+  static constexpr int HALF_ELEMS = half_elems(C);
+  static constexpr int LDS_FFT = lds_bytes_for(C);
+  static constexpr int LDS_RED = THREADS * (int)sizeof(T);
   static constexpr int LDS = LDS_FFT > LDS_RED ? LDS_FFT : LDS_RED;
+  // occupancy hint (waves per SIMD) -> register budget 512/MINW per lane: aim at 128 VGPRs
+  // (4 waves/SIMD) where the LDS footprint lets that many blocks share a CU.
+  static constexpr int WAVES_PER_BLOCK = (THREADS + 63) / 64;
+  static constexpr int BLOCKS_BY_LDS = LDS > 0 ? (160 * 1024) / LDS : 16;
+  static constexpr int MINW_LDS = (BLOCKS_BY_LDS * WAVES_PER_BLOCK) / 4;
+  static constexpr int MINW = MINW_LDS < 1 ? 1 : (MINW_LDS > 4 ? 4 : MINW_LDS);
 };
 
 template <typename T>
@@ -95,7 +105,7 @@ template <int H>
 __device__ __forceinline__ int compact_col(int h, int p) { return h == 0 ? p : H / 2 + 1 + p; }
 
 template <typename T, int H, int MODE, int LAY>
-__global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS)) void k_pass(const PassDesc d) {
+__global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>::MINW)) void k_pass(const PassDesc d) {
   using Cfg = PassCfg<T, H, LAY>;
   constexpr int P = Cfg::P, TT = Cfg::TT, C = Cfg::C;
   constexpr bool RP_IN = (LAY == LAY_RP) && (MODE == PASS_FWD);     // real row pair in
@@ -106,10 +116,14 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS)) void k_pass(const Pa
   constexpr bool REAL_OUT = RP_OUT || R1;
   if (d.done != nullptr && *d.done) return;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  C2<T>* lds = reinterpret_cast<C2<T>*>(smem_raw);
   const C2<T>* __restrict__ twL = reinterpret_cast<const C2<T>*>(d.tw);
 
-  const int tid = threadIdx.x;
+  // Each block = two thread groups of C lines: group `half` runs the length-H FFT of the
+  // even (half=0) or odd (half=1) frequencies of the same lines, in its own LDS image.
+  const int half = threadIdx.x / Cfg::GROUP;
+  const int tid = threadIdx.x - half * Cfg::GROUP;
+  C2<T>* lds = reinterpret_cast<C2<T>*>(smem_raw) + half * Cfg::HALF_ELEMS;
+  C2<T>* lds_other = reinterpret_cast<C2<T>*>(smem_raw) + (1 - half) * Cfg::HALF_ELEMS;
   int l, t, lbase;
   constexpr int LSTRIDE = (LAY == LAY_STRIDED) ? C : 1;
   if constexpr (LAY == LAY_STRIDED) { t = tid / C; l = tid - t * C; lbase = l; }
@@ -119,10 +133,13 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS)) void k_pass(const Pa
   int q, r, i;
   bool valid;
   if constexpr (LAY == LAY_STRIDED) {
+    // logical block = (q, g) with g fastest; the XCD remap keeps consecutive g (adjacent
+    // column groups: the two halves of each 128-B line) on one XCD.
     const int lb = xcd_remap(blockIdx.x, gridDim.x);
-    const int g = lb / d.Q;
-    q = lb - g * d.Q;
     const int GI = (d.In + C - 1) / C;
+    const int G = d.Rn * GI;
+    q = lb / G;
+    const int g = lb - q * G;
     r = g / GI;
     i = (g - r * GI) * C + l;
     valid = (r < d.Rn) && (i < d.In);
@@ -194,9 +211,9 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS)) void k_pass(const Pa
   };
 
   C2<T> v[P];
-  C2<T> keep[P];   // FWD/CONV: odd-half input; INV/CONV: even-half output
   T dsum = 0;
 
+  // ---- load this group's half: even x[p]+x[p+H], odd (x[p]-x[p+H]) W_L^p; or frequencies
   if constexpr (MODE == PASS_FWD || MODE == PASS_CONV) {
     const int in_len = d.in.len;
     const int lim = in_len - 1;
@@ -208,8 +225,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS)) void k_pass(const Pa
         C2<T> a = load_in(p);
         C2<T> c = load_in(p2 < in_len ? p2 : lim);
         if (p2 >= in_len) c = mk<T>(0, 0);
-        v[k] = cadd<T>(a, c);
-        keep[k] = cmul<T>(csub<T>(a, c), twL[p]);
+        v[k] = half == 0 ? cadd<T>(a, c) : cmul<T>(csub<T>(a, c), twL[p]);
       }
     } else {
 #pragma unroll
@@ -217,107 +233,87 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS)) void k_pass(const Pa
         const int p = t + TT * k;
         C2<T> a = load_in(p < in_len ? p : lim);
         if (p >= in_len) a = mk<T>(0, 0);
-        v[k] = a;
-        keep[k] = cmul<T>(a, twL[p]);
+        v[k] = half == 0 ? a : cmul<T>(a, twL[p]);
       }
     }
   } else {
 #pragma unroll
     for (int k = 0; k < P; ++k) {
-      if constexpr (HERM_IN) v[k] = load_herm(0, t + TT * k);
-      else v[k] = load_in(t + TT * k);
+      if constexpr (HERM_IN) v[k] = load_herm(half, t + TT * k);
+      else v[k] = load_in(half * H + t + TT * k);
     }
   }
 
-#pragma unroll 1
-  for (int half = 0; half < 2; ++half) {
-    if constexpr (MODE == PASS_FWD) {
-      if (half == 1) {
+  if constexpr (MODE == PASS_FWD) {
+    fft_line<T, H, P, -1, LSTRIDE>(v, lds, lbase, t, twL);
+    if constexpr (HERM_OUT) {
+      // split Z = X_a + i X_b by Hermitian symmetry: partner of position p is
+      // (H - p) mod H in the even half and H - 1 - p in the odd half (same group).
+      __syncthreads();
 #pragma unroll
-        for (int k = 0; k < P; ++k) v[k] = keep[k];
+      for (int k = 0; k < P; ++k) lds[lds_phys(lbase + t + TT * k)] = v[k];
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < P; ++k) {
+        const int p = t + TT * k;
+        const int pp = (half == 0) ? ((H - p) & (H - 1)) : (H - 1 - p);
+        const C2<T> zp = lds[lds_phys(lbase + pp)];
+        const bool store = (half == 0) ? (p <= H / 2) : (p < H / 2);
+        if (valid && store) {
+          const int c = compact_col<H>(half, p);
+          const T hf = (T)0.5;
+          out_c[c] = mk<T>(hf * (v[k].x + zp.x), hf * (v[k].y - zp.y));               // (Z + conj Zp)/2
+          if (has2) out_c2[c] = mk<T>(hf * (v[k].y + zp.y), -hf * (v[k].x - zp.x));  // (Z - conj Zp)/2i
+        }
       }
+    } else if (valid) {
+#pragma unroll
+      for (int k = 0; k < P; ++k) out_c[(int64_t)(half * H + t + TT * k) * ops] = v[k];
+    }
+  } else {
+    if constexpr (MODE == PASS_CONV) {
       fft_line<T, H, P, -1, LSTRIDE>(v, lds, lbase, t, twL);
-      if constexpr (HERM_OUT) {
-        // split Z = X_a + i X_b by Hermitian symmetry: partner of position p is
-        // (H - p) mod H in the even half and H - 1 - p in the odd half.
-        __syncthreads();
+      const int64_t sb = (int64_t)i * d.spec_i + (int64_t)r * d.spec_r + (int64_t)(half * H + t) * d.spec_p;
 #pragma unroll
-        for (int k = 0; k < P; ++k) lds[lds_phys(lbase + t + TT * k)] = v[k];
-        __syncthreads();
+      for (int k = 0; k < P; ++k) v[k] = spec_mul<T>(d.spec_kind, d.spec, sb + (int64_t)(TT * k) * d.spec_p, v[k]);
+    }
+    fft_line<T, H, P, +1, LSTRIDE>(v, lds, lbase, t, twL);
+    // combine halves through LDS: y[p] = ye + conj(W_L^p) yo (even group stores),
+    // y[p+H] = ye - conj(W_L^p) yo (odd group stores); crop to out_len.
+    if (half == 1) {
 #pragma unroll
-        for (int k = 0; k < P; ++k) {
-          const int p = t + TT * k;
-          const int pp = (half == 0) ? ((H - p) & (H - 1)) : (H - 1 - p);
-          const C2<T> zp = lds[lds_phys(lbase + pp)];
-          const bool store = (half == 0) ? (p <= H / 2) : (p < H / 2);
-          if (valid && store) {
-            const int c = compact_col<H>(half, p);
-            const T hf = (T)0.5;
-            out_c[c] = mk<T>(hf * (v[k].x + zp.x), hf * (v[k].y - zp.y));               // (Z + conj Zp)/2
-            if (has2) out_c2[c] = mk<T>(hf * (v[k].y + zp.y), -hf * (v[k].x - zp.x));  // (Z - conj Zp)/2i
-          }
-        }
-      } else if (valid) {
+      for (int k = 0; k < P; ++k) v[k] = cmulc<T>(v[k], twL[t + TT * k]);
+    }
+    __syncthreads();
 #pragma unroll
-        for (int k = 0; k < P; ++k) out_c[(int64_t)(half * H + t + TT * k) * ops] = v[k];
+    for (int k = 0; k < P; ++k) lds[lds_phys(lbase + (t + TT * k) * LSTRIDE)] = v[k];
+    __syncthreads();
+    const int out_len = d.out.len;
+    const T* dot_re = nullptr; const T* dot_im = nullptr;
+    if constexpr (REAL_OUT) {
+      if (d.partial != nullptr) {
+        dot_re = reinterpret_cast<const T*>(d.dot) + (out_re - reinterpret_cast<T*>(d.out.ptr));
+        dot_im = dot_re + d.out.r_stride;
       }
-    } else {
-      if constexpr (MODE == PASS_CONV) {
-        fft_line<T, H, P, -1, LSTRIDE>(v, lds, lbase, t, twL);
-        const int64_t sb = (int64_t)i * d.spec_i + (int64_t)r * d.spec_r + (int64_t)(half * H + t) * d.spec_p;
+    }
 #pragma unroll
-        for (int k = 0; k < P; ++k) v[k] = spec_mul<T>(d.spec_kind, d.spec, sb + (int64_t)(TT * k) * d.spec_p, v[k]);
-      } else {  // INV: half 0 input loaded above; half 1 loads the odd frequencies
-        if (half == 1) {
-#pragma unroll
-          for (int k = 0; k < P; ++k) {
-            keep[k] = v[k];
-            if constexpr (HERM_IN) v[k] = load_herm(1, t + TT * k);
-            else v[k] = load_in(H + t + TT * k);
-          }
-        }
-      }
-      fft_line<T, H, P, +1, LSTRIDE>(v, lds, lbase, t, twL);
-      if (half == 0) {
-        if constexpr (MODE == PASS_CONV) {
-#pragma unroll
-          for (int k = 0; k < P; ++k) { C2<T> tmp = v[k]; v[k] = keep[k]; keep[k] = tmp; }
-        }
-      } else {
-        // y[p] = ye + conj(W_L^p) yo ;  y[p+H] = ye - conj(W_L^p) yo ; crop to out_len
-        const int out_len = d.out.len;
-        const T* dot_re = nullptr; const T* dot_im = nullptr;
+    for (int k = 0; k < P; ++k) {
+      const int p = t + TT * k;
+      const C2<T> o = lds_other[lds_phys(lbase + p * LSTRIDE)];
+      const C2<T> y = half == 0 ? cadd<T>(v[k], o) : csub<T>(o, v[k]);
+      const int pp = p + half * H;
+      if (valid && pp < out_len) {
         if constexpr (REAL_OUT) {
-          if (d.partial != nullptr) {
-            dot_re = reinterpret_cast<const T*>(d.dot) + (out_re - reinterpret_cast<T*>(d.out.ptr));
-            dot_im = dot_re + d.out.r_stride;
-          }
-        }
-#pragma unroll
-        for (int k = 0; k < P; ++k) {
-          const int p = t + TT * k;
-          const C2<T> yo = cmulc<T>(v[k], twL[p]);
-          const C2<T> y0 = cadd<T>(keep[k], yo);
-          const C2<T> y1 = csub<T>(keep[k], yo);
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) {
-            const int pp = p + s2 * H;
-            const C2<T> y = s2 ? y1 : y0;
-            if (valid && pp < out_len) {
-              if constexpr (REAL_OUT) {
-                out_re[pp] = y.x;
-                if (dot_re != nullptr) dsum += y.x * dot_re[pp];
-                if constexpr (RP_OUT) {
-                  if (has2) {
-                    out_im[pp] = y.y;
-                    if (dot_re != nullptr) dsum += y.y * dot_im[pp];
-                  }
-                }
-              } else {
-                out_c[(int64_t)pp * ops] = y;
-              }
+          out_re[pp] = y.x;
+          if (dot_re != nullptr) dsum += y.x * dot_re[pp];
+          if constexpr (RP_OUT) {
+            if (has2) {
+              out_im[pp] = y.y;
+              if (dot_re != nullptr) dsum += y.y * dot_im[pp];
             }
           }
+        } else {
+          out_c[(int64_t)pp * ops] = y;
         }
       }
     }
@@ -325,15 +321,16 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS)) void k_pass(const Pa
 
   if constexpr (REAL_OUT) {
     if (d.partial != nullptr) {
-      // per-line fused dot: every thread parks its partial sum, the line's first thread adds
-      // them in fixed order (deterministic) and writes partial[q][r].
+      // per-line fused dot: every thread parks its partial sum; the line's first thread of
+      // the even group adds both groups' sums in fixed order (deterministic) -> partial[q][r].
       T* red = reinterpret_cast<T*>(smem_raw);
       __syncthreads();
-      red[tid] = dsum;
+      red[threadIdx.x] = dsum;
       __syncthreads();
-      if (t == 0 && valid) {
+      if (half == 0 && t == 0 && valid) {
         T s = 0;
         for (int k = 0; k < TT; ++k) s += red[tid + k];
+        for (int k = 0; k < TT; ++k) s += red[Cfg::GROUP + tid + k];
         reinterpret_cast<T*>(d.partial)[(int64_t)q * d.Rn + r] = s;
       }
     }
