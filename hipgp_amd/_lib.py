@@ -11,7 +11,8 @@ import os
 import torch  # noqa: F401  (must precede the dlopen below, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libhipgp.so")
+# HGP_LIB selects an alternative in-tree build (block-shape variants for tuning runs)
+LIB_PATH = os.environ.get("HGP_LIB") or os.path.join(_HERE, "libhipgp.so")
 
 HGP_F32, HGP_F64 = 0, 1
 OP_K, OP_CINV, OP_RT, OP_R = 0, 1, 2, 3

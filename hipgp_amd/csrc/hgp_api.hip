@@ -131,6 +131,10 @@ template <typename T>
 int launch(int H, int mode, int lay, const PassDesc& d, int64_t lines_contig, hipStream_t s) {
   const PassGeom g = pass_geom<T>(H, lay);
   if (g.C == 0) return fail(HGP_E_UNSUPPORTED, "transform half-length " + std::to_string(H) + " not supported");
+  // only the fp64 forward transforms fold an input longer than H (hgp_pass.hpp CAN_FOLD)
+  const bool can_fold = sizeof(T) == 8 && mode == PASS_FWD;
+  if (mode != PASS_INV && !can_fold && d.in.len > H)
+    return fail(HGP_E_ARG, "internal: pass input length " + std::to_string(d.in.len) + " > H = " + std::to_string(H));
   int64_t nb;
   if (lay == LAY_STRIDED) nb = (int64_t)d.Q * d.Rn * ((d.In + g.C - 1) / g.C);
   else nb = (lines_contig + g.C - 1) / g.C;
@@ -160,11 +164,14 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
            const int* done, int only_pass = -1) {
   const OpGeom g = op_geom(P, op);
   const int d = P->d;
+  const int conv_mode = g.spec_kind == SPEC_REAL ? PASS_CONV : PASS_CONVC;
   const size_t cs = sizeof(C2<T>);
   const int64_t Sl = compact_stride(g.L[d - 1]);
   // per-RHS workspace (complex elements)
   int64_t B1 = 0, B2 = 0;
-  if (d == 2) B1 = std::max(g.in[0], g.out[0]) * Sl;
+  // 2-D: column-major intermediate W[q][c][i0], c < H1 + 1, column pitch S0 (hgp_rows.hpp)
+  const int64_t S0 = (d == 2) ? round_up(std::max(g.in[0], g.out[0]), 16) : 0;
+  if (d == 2) B1 = (g.L[1] / 2 + 1) * S0;
   if (d == 3) {
     B1 = std::max(g.in[0] * g.in[1], g.out[0] * g.out[1]) * Sl;
     B2 = std::max(g.in[0], g.out[0]) * g.L[1] * Sl;
@@ -203,30 +210,37 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
       D.dot = dvc; D.partial = pc;
       D.spec = g.spec; D.spec_kind = g.spec_kind; D.spec_i = 0; D.spec_r = 0; D.spec_p = 1;
       D.tw = g.tw[0].ptr; D.Q = qn; D.Rn = 1; D.In = 1; D.done = done;
-      HGP_TRY(run((int)(g.L[0] / 2), PASS_CONV, LAY_R1, D, qn));
+      HGP_TRY(run((int)(g.L[0] / 2), conv_mode, LAY_R1, D, qn));
     } else if (d == 2) {
       C2<T>* w1 = reinterpret_cast<C2<T>*>(P->ws1.ptr);
       const int64_t H1 = g.L[1] / 2;
-      // A: FWD along axis 1, row pairs of each RHS -> compact half spectra w1 [q][i0][c1]
+      auto run_rowt = [&](int inv, PassDesc& D) -> int {
+        const int me = pass_no++;
+        if (only_pass >= 0 && only_pass != me) return 0;
+        hipError_t e = launch_rowt<T>((int)H1, inv, D, P->stream);
+        if (e != hipSuccess) return fail(HGP_E_HIP, std::string("row pass launch: ") + hipGetErrorString(e));
+        return 0;
+      };
+      // A: FWD along axis 1, row pairs of each RHS -> column-major half spectra w1 [q][c1][i0]
       PassDesc A = base_desc();
       A.in = View{(void*)xi, g.in_M, g.in[1], 1, (int)g.in[1]};
-      A.out = View{w1, B1, Sl, 1, 0};
+      A.out = View{w1, B1, S0, 1, 0};
       A.tw = g.tw[1].ptr; A.Q = qn; A.Rn = (int)((g.in[0] + 1) / 2); A.nrows = (int)g.in[0]; A.done = done;
-      HGP_TRY(run((int)H1, PASS_FWD, LAY_RP, A, (int64_t)qn * A.Rn));
-      // B: CONV along axis 0 (strided columns c1 = 0..H1), in place
+      HGP_TRY(run_rowt(0, A));
+      // B: CONV along axis 0 = contiguous lines (q, c1), in place; spectrum [c1][k0]
       PassDesc Bd = base_desc();
-      Bd.in = View{w1, B1, 0, Sl, (int)g.in[0]};
-      Bd.out = View{w1, B1, 0, Sl, (int)g.out[0]};
-      Bd.spec = g.spec; Bd.spec_kind = g.spec_kind; Bd.spec_i = 1; Bd.spec_p = Sl; Bd.spec_r = 0;
-      Bd.tw = g.tw[0].ptr; Bd.Q = qn; Bd.Rn = 1; Bd.In = (int)(H1 + 1); Bd.done = done;
-      HGP_TRY(run((int)(g.L[0] / 2), PASS_CONV, LAY_STRIDED, Bd, 0));
-      // C: INV along axis 1: rebuild row pairs, crop, fused dot
+      Bd.in = View{w1, B1, S0, 1, (int)g.in[0]};
+      Bd.out = View{w1, B1, S0, 1, (int)g.out[0]};
+      Bd.spec = g.spec; Bd.spec_kind = g.spec_kind; Bd.spec_i = 0; Bd.spec_p = 1; Bd.spec_r = g.L[0];
+      Bd.tw = g.tw[0].ptr; Bd.Q = qn; Bd.Rn = (int)(H1 + 1); Bd.In = 1; Bd.done = done;
+      HGP_TRY(run((int)(g.L[0] / 2), conv_mode, LAY_CONTIG, Bd, (int64_t)qn * Bd.Rn));
+      // C: INV along axis 1: column-major tiles -> row pairs, crop, fused dot
       PassDesc Cd = base_desc();
-      Cd.in = View{w1, B1, Sl, 1, (int)g.L[1]};
+      Cd.in = View{w1, B1, S0, 1, 0};
       Cd.out = View{yo, g.out_M, g.out[1], 1, (int)g.out[1]};
       Cd.dot = dvc; Cd.partial = pc;
       Cd.tw = g.tw[1].ptr; Cd.Q = qn; Cd.Rn = (int)((g.out[0] + 1) / 2); Cd.nrows = (int)g.out[0]; Cd.done = done;
-      HGP_TRY(run((int)H1, PASS_INV, LAY_RP, Cd, (int64_t)qn * Cd.Rn));
+      HGP_TRY(run_rowt(1, Cd));
     } else {
       C2<T>* w1 = reinterpret_cast<C2<T>*>(P->ws1.ptr);
       C2<T>* w2 = reinterpret_cast<C2<T>*>(P->ws2.ptr);
@@ -250,7 +264,7 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
       P3.out = View{w2, B2, Sl, L1 * Sl, (int)g.out[0]};
       P3.spec = g.spec; P3.spec_kind = g.spec_kind; P3.spec_i = 1; P3.spec_r = Sl; P3.spec_p = L1 * Sl;
       P3.tw = g.tw[0].ptr; P3.Q = qn; P3.Rn = (int)L1; P3.In = (int)(H2 + 1); P3.done = done;
-      HGP_TRY(run((int)(g.L[0] / 2), PASS_CONV, LAY_STRIDED, P3, 0));
+      HGP_TRY(run((int)(g.L[0] / 2), conv_mode, LAY_STRIDED, P3, 0));
       // P4: INV axis 1 (strided): lines (o0, c2) -> w1 [q][o0][o1][c2]
       PassDesc P4 = base_desc();
       P4.in = View{w2, B2, L1 * Sl, Sl, (int)L1};
@@ -395,12 +409,14 @@ int set_column_t(hgp_plan* P, const void* column, double jitter, double clamp_mi
   const int64_t nK = P->prodLK / LKl * SK, nR = P->prodLR / LRl * SR;
   HGP_TRY(P->specK.ensure((size_t)nK * sizeof(T)));
   HGP_TRY(P->specI.ensure((size_t)nK * sizeof(T)));
-  extract_pair<T>(F, P->specK.ptr, P->specI.ptr, nK, LKl, SK, compact, 1.0 / (double)P->prodLK, s);
+  // 2-D: spectra transposed to [compact column c1][k0] for the contiguous column pass
+  extract_pair<T>(F, P->specK.ptr, P->specI.ptr, nK, LKl, SK, compact, 1.0 / (double)P->prodLK, s,
+                  d == 2 ? P->LK[0] : 0);
   for (int ax = 0; ax < 3; ++ax) gd.L[ax] = P->LR[ax];
   embed_R(sv, g1, gd, s);
   HGP_TRY(fwd_grid_f64(P, P->LR, P->tw64R, g1, g2, &F));
   HGP_TRY(P->specR.ensure((size_t)nR * sizeof(C2<T>)));
-  extract_cplx<T>(F, P->specR.ptr, nR, LRl, SR, compact, 1.0 / (double)P->prodLR, s);
+  extract_cplx<T>(F, P->specR.ptr, nR, LRl, SR, compact, 1.0 / (double)P->prodLR, s, d == 2 ? P->LR[0] : 0);
   HIP_TRY(hipGetLastError());
   P->have_spec = true;
   if (n_clamped) {

@@ -119,6 +119,30 @@ __device__ __forceinline__ void dft(C2<T>* v) {
   }
 }
 
+// Exchange synchronisation.  WAVE = true when every line of the block lives inside one
+// wavefront (position-fast layouts with H/P <= 64 threads per line): a wave's LDS
+// instructions execute in order, so only the compiler must be kept from moving LDS accesses
+// across the exchange -- no s_barrier.  Otherwise a block barrier.
+template <bool WAVE>
+__device__ __forceinline__ void xsync() {
+  if constexpr (WAVE) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  } else {
+    __syncthreads();
+  }
+}
+
+// W_L^q (forward sign), q in [0, L = 2H), from the LDS half table tab[q] = W_L^q, q < H:
+// W_L^{q+H} = -W_L^q.  Twiddles never come from global memory inside the FFT.
+template <typename T, int H>
+__device__ __forceinline__ C2<T> tw_at(const C2<T>* __restrict__ tab, int q) {
+  C2<T> w = tab[q & (H - 1)];
+  if (q & H) { w.x = -w.x; w.y = -w.y; }
+  return w;
+}
+
 // LDS address of logical element e (padding breaks the power-of-two strides of the
 // Stockham write pattern: one complex slot per 16).
 __device__ __forceinline__ int lds_phys(int e) { return e + (e >> 4); }
@@ -135,11 +159,11 @@ __device__ __forceinline__ int lds_at(int pbase, int base, int x, bool base16) {
 // One H-point FFT of the line whose P values this thread holds in v (positions t + T*k,
 // k = register index).  Result in v, natural order, same positions.  Line element e of the
 // block's LDS image lives at lds_phys(base + e*STRIDE) (STRIDE = 1: line-contiguous image;
-// STRIDE = C: lines interleaved).  twL: W_L^q table (L = 2H, forward sign), so
-// W_H^e = twL[2e].  All threads of the block must call it when T > 1 (block barriers).
-template <typename T, int H, int P, int DIR, int STRIDE, int S>
+// STRIDE = C: lines interleaved).  tab: LDS half table of W_L^q (L = 2H, see tw_at), so
+// W_H^e = W_L^{2e}.  All threads of the block must call it when T > 1 (block barriers).
+template <typename T, int H, int P, int DIR, int STRIDE, bool WAVE, int S>
 __device__ __forceinline__ void fft_stage(C2<T> (&v)[P], C2<T>* lds, int base, int t,
-                                          const C2<T>* __restrict__ twL) {
+                                          const C2<T>* __restrict__ tab) {
   using St = Stages<H, P>;
   constexpr int NST = St::count();
   if constexpr (S < NST) {
@@ -152,12 +176,18 @@ __device__ __forceinline__ void fft_stage(C2<T> (&v)[P], C2<T>* lds, int base, i
       if constexpr (NS > 1) {
         const int j = t + b * TT;
         const int kk = j & (NS - 1);
+        // w^r with w = W_H^{kk*H/(NS*R)}: one LDS lookup, powers by binary powering
+        // (at most 4 products deep, ~4 ulp) -- few LDS reads and few live registers.
+        C2<T> wp[R];
+        wp[1] = tw_at<T, H>(tab, (2 * (H / (NS * R))) * kk);
 #pragma unroll
-        for (int r = 1; r < R; ++r) {
-          // W_H^{kk*r*H/(NS*R)} = twL[2*kk*r*H/(NS*R)]
-          const C2<T> w = twL[(2 * (H / (NS * R))) * kk * r];
-          a[b][r] = (DIR < 0) ? cmul<T>(a[b][r], w) : cmulc<T>(a[b][r], w);
+        for (int r = 2; r < R; ++r) {
+          const int hi = (r & (r - 1)) == 0 ? r / 2 : (1 << (31 - __builtin_clz(r)));   // r = hi + lo
+          const int lo = r - hi;
+          wp[r] = cmul<T>(wp[hi], wp[lo]);
         }
+#pragma unroll
+        for (int r = 1; r < R; ++r) a[b][r] = (DIR < 0) ? cmul<T>(a[b][r], wp[r]) : cmulc<T>(a[b][r], wp[r]);
       }
       dft<T, R, DIR>(a[b]);
     }
@@ -168,18 +198,18 @@ __device__ __forceinline__ void fft_stage(C2<T> (&v)[P], C2<T>* lds, int base, i
       const int wb = base + idxD * STRIDE;
       const int pwb = lds_phys(wb);
       constexpr bool WB16 = (STRIDE == 1) && (NS == 1) && (R == 16);   // base 16-aligned
-      __syncthreads();   // previous readers of this LDS region are done
+      xsync<WAVE>();   // previous readers of this LDS region are done
 #pragma unroll
       for (int b = 0; b < NB; ++b)
 #pragma unroll
         for (int r = 0; r < R; ++r)
           lds[lds_at(pwb, wb, (b * TT * R + r * NS) * STRIDE, WB16)] = a[b][r];
-      __syncthreads();
+      xsync<WAVE>();
       const int rb = base + t * STRIDE;
       const int prb = lds_phys(rb);
 #pragma unroll
       for (int k = 0; k < P; ++k) v[k] = lds[lds_at(prb, rb, TT * k * STRIDE, false)];
-      fft_stage<T, H, P, DIR, STRIDE, S + 1>(v, lds, base, t, twL);
+      fft_stage<T, H, P, DIR, STRIDE, WAVE, S + 1>(v, lds, base, t, tab);
     } else {
 #pragma unroll
       for (int b = 0; b < NB; ++b)
@@ -189,10 +219,15 @@ __device__ __forceinline__ void fft_stage(C2<T> (&v)[P], C2<T>* lds, int base, i
   }
 }
 
-template <typename T, int H, int P, int DIR, int STRIDE>
+template <typename T, int H, int P, int DIR, int STRIDE, bool WAVE = false>
 __device__ __forceinline__ void fft_line(C2<T> (&v)[P], C2<T>* lds, int base, int t,
-                                         const C2<T>* __restrict__ twL) {
-  fft_stage<T, H, P, DIR, STRIDE, 0>(v, lds, base, t, twL);
+                                         const C2<T>* __restrict__ tab) {
+  // Opaque copy of t: every twiddle index below is recomputed and re-read from LDS, instead of
+  // the compiler keeping the previous transform's twiddles live in VGPRs (that CSE across the
+  // two FFTs of a line costs ~50 VGPRs and halves occupancy).
+  int tt = t;
+  asm volatile("" : "+v"(tt));
+  fft_stage<T, H, P, DIR, STRIDE, WAVE, 0>(v, lds, base, tt, tab);
 }
 
 }  // namespace hgp

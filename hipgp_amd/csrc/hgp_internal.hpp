@@ -13,6 +13,9 @@ struct PassGeom { int C; int threads; int lds; };
 template <typename T>
 hipError_t launch_pass(int H, int mode, int lay, const PassDesc& d, int64_t nblocks, hipStream_t s);
 template <typename T> PassGeom pass_geom(int H, int lay);
+// 2-D row-pair passes with the column-major intermediate (hgp_rows.hpp); inv = 0 FWD, 1 INV
+template <typename T>
+hipError_t launch_rowt(int H, int inv, const PassDesc& d, hipStream_t s);
 
 // setup (fp64)
 void dct_axis(const double* W, const double* in, double* out, int m, int64_t I, int64_t ncols, double scale,
@@ -23,9 +26,9 @@ void clamp_spectrum(const double* Draw, double* out3, int64_t M, double clamp_mi
 void embed_K(const double* cK, const double* cI, double2* out, const GridDims& g, hipStream_t s);
 void embed_R(const double* sv, double2* out, const GridDims& g, hipStream_t s);
 template <typename T> void extract_pair(const double2* F, void* a, void* b, int64_t n, int64_t L, int64_t S, int compact,
-                                        double scale, hipStream_t s);
+                                        double scale, hipStream_t s, int64_t L0t = 0);
 template <typename T> void extract_cplx(const double2* F, void* o, int64_t n, int64_t L, int64_t S, int compact, double scale,
-                                        hipStream_t s);
+                                        hipStream_t s, int64_t L0t = 0);
 template <typename T> void expand_spec(const double* src, void* out, const GridDims& g, hipStream_t s);
 
 // CG

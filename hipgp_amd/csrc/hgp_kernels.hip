@@ -177,9 +177,12 @@ void embed_R(const double* sv, double2* out, const GridDims& g, hipStream_t s) {
 // the layout the passes read: when `compact`, the last axis keeps only the S >= H+1 "compact"
 // half-spectrum columns c (even frequency 2c for c <= H/2, odd 2(c-H/2-1)+1 after; zero pad
 // beyond H) — the real-data passes store exactly these columns.
-__device__ __forceinline__ int64_t spec_src(int64_t idx, int64_t L, int64_t S, int compact) {
+__device__ __forceinline__ int64_t spec_src(int64_t idx, int64_t L, int64_t S, int compact, int64_t L0t) {
   if (!compact) return idx;
-  const int64_t o = idx / S, c = idx - o * S, H = L / 2;
+  int64_t o, c;
+  if (L0t > 0) { c = idx / L0t; o = idx - c * L0t; }     // transposed: [c][k0], k0 < L0t
+  else { o = idx / S; c = idx - o * S; }
+  const int64_t H = L / 2;
   if (c > H) return -1;
   const int64_t kp = (c <= H / 2) ? c : H + (c - H / 2 - 1);
   return o * L + kp;
@@ -187,38 +190,41 @@ __device__ __forceinline__ int64_t spec_src(int64_t idx, int64_t L, int64_t S, i
 
 template <typename T>
 __global__ void k_extract_pair(const double2* __restrict__ F, T* __restrict__ a, T* __restrict__ b, int64_t n,
-                               int64_t L, int64_t S, int compact, double scale) {
+                               int64_t L, int64_t S, int compact, double scale, int64_t L0t) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const int64_t src = spec_src(i, L, S, compact);
+  const int64_t src = spec_src(i, L, S, compact, L0t);
   const double2 f = src >= 0 ? F[src] : make_double2(0.0, 0.0);
   a[i] = (T)(f.x * scale);
   b[i] = (T)(f.y * scale);
 }
 template <typename T>
 __global__ void k_extract_cplx(const double2* __restrict__ F, C2<T>* __restrict__ o, int64_t n, int64_t L, int64_t S,
-                               int compact, double scale) {
+                               int compact, double scale, int64_t L0t) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const int64_t src = spec_src(i, L, S, compact);
+  const int64_t src = spec_src(i, L, S, compact, L0t);
   const double2 f = src >= 0 ? F[src] : make_double2(0.0, 0.0);
   o[i] = mk<T>((T)(f.x * scale), (T)(f.y * scale));
 }
+// L0t > 0: 2-D transposed layout [compact column c][axis-0 frequency k0 < L0t] read by the
+// column pass of the column-major intermediate (hgp_rows.hpp); else [outer][c] with pitch S.
 template <typename T>
 void extract_pair(const double2* F, void* a, void* b, int64_t n, int64_t L, int64_t S, int compact, double scale,
-                  hipStream_t s) {
+                  hipStream_t s, int64_t L0t) {
   hipLaunchKernelGGL((k_extract_pair<T>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, F, (T*)a, (T*)b, n, L, S,
-                     compact, scale);
+                     compact, scale, L0t);
 }
 template <typename T>
-void extract_cplx(const double2* F, void* o, int64_t n, int64_t L, int64_t S, int compact, double scale, hipStream_t s) {
+void extract_cplx(const double2* F, void* o, int64_t n, int64_t L, int64_t S, int compact, double scale, hipStream_t s,
+                  int64_t L0t) {
   hipLaunchKernelGGL((k_extract_cplx<T>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, F, (C2<T>*)o, n, L, S,
-                     compact, scale);
+                     compact, scale, L0t);
 }
-template void extract_pair<float>(const double2*, void*, void*, int64_t, int64_t, int64_t, int, double, hipStream_t);
-template void extract_pair<double>(const double2*, void*, void*, int64_t, int64_t, int64_t, int, double, hipStream_t);
-template void extract_cplx<float>(const double2*, void*, int64_t, int64_t, int64_t, int, double, hipStream_t);
-template void extract_cplx<double>(const double2*, void*, int64_t, int64_t, int64_t, int, double, hipStream_t);
+template void extract_pair<float>(const double2*, void*, void*, int64_t, int64_t, int64_t, int, double, hipStream_t, int64_t);
+template void extract_pair<double>(const double2*, void*, void*, int64_t, int64_t, int64_t, int, double, hipStream_t, int64_t);
+template void extract_cplx<float>(const double2*, void*, int64_t, int64_t, int64_t, int, double, hipStream_t, int64_t);
+template void extract_cplx<double>(const double2*, void*, int64_t, int64_t, int64_t, int, double, hipStream_t, int64_t);
 
 // full expanded-grid spectrum from the unique m-grid values: u -> min(u, n-u) per axis
 template <typename T>

@@ -4,6 +4,14 @@
 //   FWD  : load (pad/fold) -> forward FFT -> store the frequencies                (first axes)
 //   INV  : load frequencies -> inverse FFT -> combine halves, crop -> store         (last axes)
 //   CONV : load -> forward -> x spectrum -> inverse -> crop -> store                (axis 0)
+//          (PASS_CONV: real spectrum, prefetched with the data so the pass makes a single
+//          memory round trip; PASS_CONVC: complex spectrum of the R / R^T ops, loaded per half)
+//
+// One thread group of TT = H/P threads owns a line and runs its even-frequency half and then
+// its odd-frequency half (hgp_fft.hpp) one after the other, re-using one LDS exchange image:
+// the input stays in registers between the two halves, and the inverse halves are combined in
+// registers (both halves leave position p in the same thread).  The twiddle half-table W_L^q
+// (q < H) is staged in LDS once per block, so the FFT issues no global loads at all.
 //
 // Real data never shares a complex FFT with another right-hand side: the last (real) axis
 // packs two ROWS OF THE SAME RHS as Re/Im (rows 2j, 2j+1), splits them after the forward
@@ -14,17 +22,34 @@
 //
 // Layouts (compile time):
 //   LAY_STRIDED : complex lines along a non-last axis; C adjacent lines per block, threads
-//                 line-fast so each position is one coalesced C*8-byte row segment.
+//                 line-fast so each position is one coalesced C*sizeof(complex) row segment
+//                 (C = 16 fp32 lines = one 128-B line at H <= 1024).
 //   LAY_CONTIG  : complex lines along the last axis; threads position-fast (setup grids).
 //   LAY_RP      : last axis of (nrhs, M) real vectors, row pair (2j, 2j+1) of RHS q
 //                 <-> two compact half-spectrum rows (FWD input / INV output).
 //   LAY_R1      : 1-D: one real line per RHS (z = x + 0i), CONV only.
 #pragma once
+#include <type_traits>
+
 #include "hgp_fft.hpp"
+
+// Block-shape tunables (measured on MI355X):
+#ifndef HGP_ROW_THREADS
+#define HGP_ROW_THREADS 256      // target block size of the contiguous-line (row) passes
+#endif
+#ifndef HGP_CMAX_STRIDED
+#define HGP_CMAX_STRIDED 16      // max adjacent lines (columns) per strided-pass block
+#endif
+#ifndef HGP_MINW_STRIDED
+#define HGP_MINW_STRIDED 0       // waves/SIMD occupancy hint; 0 = from the LDS footprint
+#endif
+#ifndef HGP_MINW_ROW
+#define HGP_MINW_ROW 0
+#endif
 
 namespace hgp {
 
-enum { PASS_FWD = 0, PASS_INV = 1, PASS_CONV = 2 };
+enum { PASS_FWD = 0, PASS_INV = 1, PASS_CONV = 2, PASS_CONVC = 3 };   // CONV: real spectrum, CONVC: complex
 enum { LAY_STRIDED = 0, LAY_CONTIG = 1, LAY_RP = 2, LAY_R1 = 3 };
 enum { SPEC_REAL = 0, SPEC_CPLX = 1, SPEC_CPLX_CONJ = 2 };
 
@@ -43,42 +68,46 @@ struct PassDesc {
   const void* spec;           // CONV: spectrum at i*spec_i + r*spec_r + kperm*spec_p
   int64_t spec_i, spec_p, spec_r;
   int spec_kind;
-  const void* tw;             // W_L^q, q < L (forward sign)
+  const void* tw;             // W_L^q, q < L (forward sign); the kernel stages q < H in LDS
   int Q;                      // right-hand sides (setup grids: 1)
   int Rn, In;                 // lines per RHS: r in [0,Rn) (outer), i in [0,In) (inner, strided)
   int nrows;                  // LAY_RP: real rows per RHS (the pair (2r, 2r+1) needs 2r+1 < nrows)
   const int* done;            // optional device flag: skip the pass when *done != 0
 };
 
+constexpr int LDS_CAP = 160 * 1024;
+
 template <typename T, int H, int LAY> struct PassCfg {
   static constexpr int P = (H < PMax<T>::v) ? H : PMax<T>::v;
   static constexpr int TT = H / P;
-  // LDS image of C lines of one frequency half (H complex each, 1 pad slot per 16)
-  static constexpr int half_elems(int c) { return c * H + ((c * H) >> 4); }
-  static constexpr int lds_bytes_for(int c) { return 2 * half_elems(c) * (int)sizeof(C2<T>); }
+  // LDS: exchange image of C lines (H complex each, 1 pad slot per 16) + twiddle half table
+  static constexpr int ex_elems(int c) { return c * H + ((c * H) >> 4); }
+  static constexpr int TW_BYTES = H * (int)sizeof(C2<T>);
+  static constexpr int lds_bytes_for(int c) { return ex_elems(c) * (int)sizeof(C2<T>) + TW_BYTES; }
   static constexpr int c_strided() {
-    int c = 64;
-    while (c > 1 && (2 * c * TT > 1024 || lds_bytes_for(c) > 140 * 1024)) c >>= 1;
+    int c = TT >= 16 ? HGP_CMAX_STRIDED : 64;
+    while (c > 1 && (c * TT > 1024 || lds_bytes_for(c) > LDS_CAP)) c >>= 1;
     return c;
   }
   static constexpr int c_contig() {
-    int c = (2 * TT >= 512) ? 1 : 512 / (2 * TT);
-    while (c > 1 && lds_bytes_for(c) > 72 * 1024) c >>= 1;
+    int c = (TT >= HGP_ROW_THREADS) ? 1 : HGP_ROW_THREADS / TT;
+    while (c > 1 && (c * TT > 1024 || lds_bytes_for(c) > LDS_CAP / 2)) c >>= 1;
     return c;
   }
   static constexpr int C = (LAY == LAY_STRIDED) ? c_strided() : c_contig();
-  static constexpr int GROUP = C * TT;           // threads of one frequency half
-  static constexpr int THREADS = 2 * GROUP;      // even-half group + odd-half group
-  static constexpr int HALF_ELEMS = half_elems(C);
-  static constexpr int LDS_FFT = lds_bytes_for(C);
-  static constexpr int LDS_RED = THREADS * (int)sizeof(T);
-  static constexpr int LDS = LDS_FFT > LDS_RED ? LDS_FFT : LDS_RED;
-  // occupancy hint (waves per SIMD) -> register budget 512/MINW per lane: aim at 128 VGPRs
-  // (4 waves/SIMD) where the LDS footprint lets that many blocks share a CU.
+  // position-fast layouts keep each line inside one wavefront when TT <= 64: exchanges then
+  // need no block barrier (hgp_fft.hpp xsync)
+  static constexpr bool WAVE = (LAY != LAY_STRIDED) && TT <= 64;
+  static constexpr int THREADS = C * TT;
+  static constexpr int EX_ELEMS = ex_elems(C);
+  static constexpr int LDS = lds_bytes_for(C);
+  // occupancy hint (waves per SIMD) from the blocks the LDS footprint lets share a CU
   static constexpr int WAVES_PER_BLOCK = (THREADS + 63) / 64;
-  static constexpr int BLOCKS_BY_LDS = LDS > 0 ? (160 * 1024) / LDS : 16;
+  static constexpr int BLOCKS_BY_LDS = LDS_CAP / LDS;
   static constexpr int MINW_LDS = (BLOCKS_BY_LDS * WAVES_PER_BLOCK) / 4;
-  static constexpr int MINW = MINW_LDS < 1 ? 1 : (MINW_LDS > 4 ? 4 : MINW_LDS);
+  static constexpr int MINW_AUTO = MINW_LDS < 1 ? 1 : (MINW_LDS > 4 ? 4 : MINW_LDS);
+  static constexpr int MINW_SET = (LAY == LAY_STRIDED) ? HGP_MINW_STRIDED : HGP_MINW_ROW;
+  static constexpr int MINW = MINW_SET > 0 ? MINW_SET : MINW_AUTO;
 };
 
 template <typename T>
@@ -104,6 +133,28 @@ __device__ __forceinline__ int xcd_remap(int b, int nb) {
 template <int H>
 __device__ __forceinline__ int compact_col(int h, int p) { return h == 0 ? p : H / 2 + 1 + p; }
 
+// Deterministic sum over the TT consecutive threads of one line (fixed shuffle tree; lines of
+// more than one wave add their wave sums in wave order through `red`).  Valid in the line's
+// first thread.  Every thread of the block must call it (barriers when TT > 64).
+template <typename T, int TT>
+__device__ __forceinline__ T line_sum(T v, T* red) {
+  constexpr int W = TT < 64 ? TT : 64;
+#pragma unroll
+  for (int off = W / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  if constexpr (TT > 64) {
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x % TT == 0) {
+      T s = 0;
+      const int w0 = threadIdx.x >> 6;
+      for (int w = 0; w < TT / 64; ++w) s += red[w0 + w];
+      v = s;
+    }
+  }
+  return v;
+}
+
 template <typename T, int H, int MODE, int LAY>
 __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>::MINW)) void k_pass(const PassDesc d) {
   using Cfg = PassCfg<T, H, LAY>;
@@ -114,36 +165,43 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
   constexpr bool HERM_OUT = RP_IN;                                   // compact half spectra out
   constexpr bool R1 = (LAY == LAY_R1);
   constexpr bool REAL_OUT = RP_OUT || R1;
-  if (d.done != nullptr && *d.done) return;
+  // inputs longer than H (folded x[p] +- x[p+H]) occur only in the fp64 setup grids' forward
+  // transforms; every other pass has in_len <= H (checked on the host), so no second load.
+  constexpr bool CAN_FOLD = std::is_same<T, double>::value && MODE == PASS_FWD;
+  if (d.done != nullptr && *d.done) return;                          // uniform: before any barrier
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  const C2<T>* __restrict__ twL = reinterpret_cast<const C2<T>*>(d.tw);
+  C2<T>* lds = reinterpret_cast<C2<T>*>(smem_raw);
+  C2<T>* tab = lds + Cfg::EX_ELEMS;
+  {
+    const C2<T>* __restrict__ twg = reinterpret_cast<const C2<T>*>(d.tw);
+    for (int q = threadIdx.x; q < H; q += Cfg::THREADS) tab[q] = twg[q];
+  }
 
-  // Each block = two thread groups of C lines: group `half` runs the length-H FFT of the
-  // even (half=0) or odd (half=1) frequencies of the same lines, in its own LDS image.
-  const int half = threadIdx.x / Cfg::GROUP;
-  const int tid = threadIdx.x - half * Cfg::GROUP;
-  C2<T>* lds = reinterpret_cast<C2<T>*>(smem_raw) + half * Cfg::HALF_ELEMS;
-  C2<T>* lds_other = reinterpret_cast<C2<T>*>(smem_raw) + (1 - half) * Cfg::HALF_ELEMS;
+  const int tid = threadIdx.x;
   int l, t, lbase;
   constexpr int LSTRIDE = (LAY == LAY_STRIDED) ? C : 1;
   if constexpr (LAY == LAY_STRIDED) { t = tid / C; l = tid - t * C; lbase = l; }
   else { l = tid / TT; t = tid - l * TT; lbase = l * H; }
 
   // ---- line coordinates (q = RHS, r = outer line, i = inner line) ----
-  int q, r, i;
+  // Strided: q, r and the block's first column i0 are block-uniform (scalar registers); a lane
+  // adds a 32-bit element offset lc + p*stride to uniform base pointers, so no 64-bit address
+  // is held per position across the FFT.
+  int q, r, i, i0 = 0, lc = 0;
   bool valid;
   if constexpr (LAY == LAY_STRIDED) {
     // logical block = (q, g) with g fastest; the XCD remap keeps consecutive g (adjacent
-    // column groups: the two halves of each 128-B line) on one XCD.
+    // column groups) of one RHS on one XCD.
     const int lb = xcd_remap(blockIdx.x, gridDim.x);
     const int GI = (d.In + C - 1) / C;
     const int G = d.Rn * GI;
     q = lb / G;
     const int g = lb - q * G;
     r = g / GI;
-    i = (g - r * GI) * C + l;
-    valid = (r < d.Rn) && (i < d.In);
-    if (!valid) { r = 0; i = 0; }     // keep every (unconditional) load in bounds
+    i0 = (g - r * GI) * C;
+    i = i0 + l;
+    valid = i < d.In;               // (q, r, i0) of a launched block are always in range
+    lc = valid ? l : 0;             // keep every (unconditional) load in bounds
   } else {
     const int64_t line = (int64_t)blockIdx.x * C + l;
     q = (int)(line / d.Rn);
@@ -165,8 +223,10 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
   } else if constexpr (HERM_IN) {
     in_c = reinterpret_cast<const C2<T>*>(d.in.ptr) + (int64_t)q * d.in.q_stride + (int64_t)(2 * r) * d.in.r_stride;
     in_c2 = has2 ? in_c + d.in.r_stride : in_c;
+  } else if constexpr (LAY == LAY_STRIDED) {
+    in_c = reinterpret_cast<const C2<T>*>(d.in.ptr) + (int64_t)q * d.in.q_stride + (int64_t)r * d.in.r_stride + i0;
   } else {
-    in_c = reinterpret_cast<const C2<T>*>(d.in.ptr) + (int64_t)q * d.in.q_stride + (int64_t)r * d.in.r_stride + i;
+    in_c = reinterpret_cast<const C2<T>*>(d.in.ptr) + (int64_t)q * d.in.q_stride + (int64_t)r * d.in.r_stride;
   }
   T* out_re = nullptr; T* out_im = nullptr;
   C2<T>* out_c = nullptr; C2<T>* out_c2 = nullptr;
@@ -178,11 +238,16 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
   } else if constexpr (HERM_OUT) {
     out_c = reinterpret_cast<C2<T>*>(d.out.ptr) + (int64_t)q * d.out.q_stride + (int64_t)(2 * r) * d.out.r_stride;
     out_c2 = out_c + d.out.r_stride;
+  } else if constexpr (LAY == LAY_STRIDED) {
+    out_c = reinterpret_cast<C2<T>*>(d.out.ptr) + (int64_t)q * d.out.q_stride + (int64_t)r * d.out.r_stride + i0;
   } else {
-    out_c = reinterpret_cast<C2<T>*>(d.out.ptr) + (int64_t)q * d.out.q_stride + (int64_t)r * d.out.r_stride + i;
+    out_c = reinterpret_cast<C2<T>*>(d.out.ptr) + (int64_t)q * d.out.q_stride + (int64_t)r * d.out.r_stride;
   }
-  const int64_t ips = (LAY == LAY_STRIDED) ? d.in.p_stride : 1;
-  const int64_t ops = (LAY == LAY_STRIDED) ? d.out.p_stride : 1;
+  // element offset of position p in this lane's line (32-bit: one RHS slab < 2^31 elements)
+  const int ips = (LAY == LAY_STRIDED) ? (int)d.in.p_stride : 1;
+  const int ops = (LAY == LAY_STRIDED) ? (int)d.out.p_stride : 1;
+  auto in_at = [&](int p) -> int { return (LAY == LAY_STRIDED) ? lc + p * ips : p; };
+  auto out_at = [&](int p) -> int { return (LAY == LAY_STRIDED) ? lc + p * ops : p; };
 
   // Loads are unconditional on clamped (always in-bounds) addresses and zeroed afterwards:
   // a per-element branch around a load makes hipcc wait vmcnt(0) per element.
@@ -194,7 +259,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
     } else if constexpr (R1) {
       return mk<T>(in_re[p], (T)0);
     } else {
-      return in_c[(int64_t)p * ips];
+      return in_c[in_at(p)];
     }
   };
   // Hermitian rebuild of Z = A + iB at frequency half h, position p from the two compact rows
@@ -209,85 +274,112 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
     if (cj) { A.y = -A.y; B.y = -B.y; }
     return mk<T>(A.x - B.y, A.y + B.x);
   };
+  // second half of an input longer than H (only the fp64 setup grids): x[p + H], or 0
+  auto load_hi = [&](int p) -> C2<T> {
+    const int in_len = d.in.len;
+    const int p2 = p + H;
+    C2<T> c = load_in(p2 < in_len ? p2 : in_len - 1);
+    if (p2 >= in_len) c = mk<T>(0, 0);
+    return c;
+  };
 
-  C2<T> v[P];
-  T dsum = 0;
+  __syncthreads();   // twiddle table staged
 
-  // ---- load this group's half: even x[p]+x[p+H], odd (x[p]-x[p+H]) W_L^p; or frequencies
-  if constexpr (MODE == PASS_FWD || MODE == PASS_CONV) {
+  // FWD/CONV: both halves' inputs are formed up front (x dies at once): even x[p] + x[p+H],
+  // odd (x[p] - x[p+H]) W_L^p.  Peak live data is two P-arrays in every mode.
+  C2<T> va[P], vb[P];
+  constexpr bool CONV = MODE == PASS_CONV || MODE == PASS_CONVC;
+  // real spectrum of both halves, issued together with the data loads
+  T sre[2][P];
+  if constexpr (MODE == PASS_CONV) {
+    const T* sb = reinterpret_cast<const T*>(d.spec) + (int64_t)i0 * d.spec_i + (int64_t)r * d.spec_r;
+    const int sp = (int)d.spec_p;
+    const int so = (LAY == LAY_STRIDED ? lc * (int)d.spec_i : 0) + t * sp;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int k = 0; k < P; ++k) sre[h][k] = sb[so + (h * H + TT * k) * sp];
+  }
+  if constexpr (MODE == PASS_FWD || CONV) {
     const int in_len = d.in.len;
     const int lim = in_len - 1;
-    if (in_len > H) {                 // uniform: input longer than H -> fold x[p] and x[p+H]
-#pragma unroll
-      for (int k = 0; k < P; ++k) {
-        const int p = t + TT * k;
-        const int p2 = p + H;
-        C2<T> a = load_in(p);
-        C2<T> c = load_in(p2 < in_len ? p2 : lim);
-        if (p2 >= in_len) c = mk<T>(0, 0);
-        v[k] = half == 0 ? cadd<T>(a, c) : cmul<T>(csub<T>(a, c), twL[p]);
-      }
-    } else {
-#pragma unroll
-      for (int k = 0; k < P; ++k) {
-        const int p = t + TT * k;
-        C2<T> a = load_in(p < in_len ? p : lim);
-        if (p >= in_len) a = mk<T>(0, 0);
-        v[k] = half == 0 ? a : cmul<T>(a, twL[p]);
-      }
-    }
-  } else {
+    const bool fold = CAN_FOLD && in_len > H;
 #pragma unroll
     for (int k = 0; k < P; ++k) {
-      if constexpr (HERM_IN) v[k] = load_herm(half, t + TT * k);
-      else v[k] = load_in(half * H + t + TT * k);
+      const int p = t + TT * k;
+      C2<T> a = load_in(p < in_len ? p : lim);
+      if (p >= in_len) a = mk<T>(0, 0);
+      C2<T> c = mk<T>(0, 0);
+      if constexpr (CAN_FOLD) {
+        if (fold) c = load_hi(p);
+      }
+      va[k] = cadd<T>(a, c);
+      vb[k] = cmul<T>(csub<T>(a, c), tab[p]);
     }
   }
 
   if constexpr (MODE == PASS_FWD) {
-    fft_line<T, H, P, -1, LSTRIDE>(v, lds, lbase, t, twL);
-    if constexpr (HERM_OUT) {
-      // split Z = X_a + i X_b by Hermitian symmetry: partner of position p is
-      // (H - p) mod H in the even half and H - 1 - p in the odd half (same group).
-      __syncthreads();
+    auto fwd_half = [&](auto half_c, C2<T>(&v)[P]) {
+      constexpr int half = decltype(half_c)::value;
+      fft_line<T, H, P, -1, LSTRIDE, Cfg::WAVE>(v, lds, lbase, t, tab);
+      if constexpr (HERM_OUT) {
+        // split Z = X_a + i X_b by Hermitian symmetry: partner of position p is
+        // (H - p) mod H in the even half and H - 1 - p in the odd half.
+        xsync<Cfg::WAVE>();
 #pragma unroll
-      for (int k = 0; k < P; ++k) lds[lds_phys(lbase + t + TT * k)] = v[k];
-      __syncthreads();
+        for (int k = 0; k < P; ++k) lds[lds_phys(lbase + t + TT * k)] = v[k];
+        xsync<Cfg::WAVE>();
 #pragma unroll
-      for (int k = 0; k < P; ++k) {
-        const int p = t + TT * k;
-        const int pp = (half == 0) ? ((H - p) & (H - 1)) : (H - 1 - p);
-        const C2<T> zp = lds[lds_phys(lbase + pp)];
-        const bool store = (half == 0) ? (p <= H / 2) : (p < H / 2);
-        if (valid && store) {
-          const int c = compact_col<H>(half, p);
-          const T hf = (T)0.5;
-          out_c[c] = mk<T>(hf * (v[k].x + zp.x), hf * (v[k].y - zp.y));               // (Z + conj Zp)/2
-          if (has2) out_c2[c] = mk<T>(hf * (v[k].y + zp.y), -hf * (v[k].x - zp.x));  // (Z - conj Zp)/2i
+        for (int k = 0; k < P; ++k) {
+          const int p = t + TT * k;
+          const int pp = (half == 0) ? ((H - p) & (H - 1)) : (H - 1 - p);
+          const C2<T> zp = lds[lds_phys(lbase + pp)];
+          const bool store = (half == 0) ? (p <= H / 2) : (p < H / 2);
+          if (valid && store) {
+            const int c = compact_col<H>(half, p);
+            const T hf = (T)0.5;
+            out_c[c] = mk<T>(hf * (v[k].x + zp.x), hf * (v[k].y - zp.y));               // (Z + conj Zp)/2
+            if (has2) out_c2[c] = mk<T>(hf * (v[k].y + zp.y), -hf * (v[k].x - zp.x));  // (Z - conj Zp)/2i
+          }
+        }
+      } else if (valid) {
+#pragma unroll
+        for (int k = 0; k < P; ++k) out_c[out_at(half * H + t + TT * k)] = v[k];
+      }
+    };
+    fwd_half(std::integral_constant<int, 0>{}, va);
+    fwd_half(std::integral_constant<int, 1>{}, vb);
+  } else {
+    // va ends as the even half's inverse (ye), vb as the odd half's (yo)
+    auto inv_half = [&](auto half_c, C2<T>(&v)[P]) {
+      constexpr int half = decltype(half_c)::value;
+      if constexpr (MODE == PASS_CONV) {
+        fft_line<T, H, P, -1, LSTRIDE, Cfg::WAVE>(v, lds, lbase, t, tab);
+#pragma unroll
+        for (int k = 0; k < P; ++k) v[k] = mk<T>(v[k].x * sre[half][k], v[k].y * sre[half][k]);
+      } else if constexpr (MODE == PASS_CONVC) {
+        fft_line<T, H, P, -1, LSTRIDE, Cfg::WAVE>(v, lds, lbase, t, tab);
+        // complex spectrum at (i, r, kperm): block-uniform base + 32-bit lane offset
+        const C2<T>* sbase = reinterpret_cast<const C2<T>*>(d.spec) + (int64_t)i0 * d.spec_i + (int64_t)r * d.spec_r;
+        const int sp = (int)d.spec_p;
+        const int so = (LAY == LAY_STRIDED ? lc * (int)d.spec_i : 0) + (half * H + t) * sp;
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+          const C2<T> sv = sbase[so + TT * k * sp];
+          v[k] = d.spec_kind == SPEC_CPLX ? cmul<T>(v[k], sv) : cmulc<T>(v[k], sv);
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+          if constexpr (HERM_IN) v[k] = load_herm(half, t + TT * k);
+          else v[k] = load_in(half * H + t + TT * k);
         }
       }
-    } else if (valid) {
-#pragma unroll
-      for (int k = 0; k < P; ++k) out_c[(int64_t)(half * H + t + TT * k) * ops] = v[k];
-    }
-  } else {
-    if constexpr (MODE == PASS_CONV) {
-      fft_line<T, H, P, -1, LSTRIDE>(v, lds, lbase, t, twL);
-      const int64_t sb = (int64_t)i * d.spec_i + (int64_t)r * d.spec_r + (int64_t)(half * H + t) * d.spec_p;
-#pragma unroll
-      for (int k = 0; k < P; ++k) v[k] = spec_mul<T>(d.spec_kind, d.spec, sb + (int64_t)(TT * k) * d.spec_p, v[k]);
-    }
-    fft_line<T, H, P, +1, LSTRIDE>(v, lds, lbase, t, twL);
-    // combine halves through LDS: y[p] = ye + conj(W_L^p) yo (even group stores),
-    // y[p+H] = ye - conj(W_L^p) yo (odd group stores); crop to out_len.
-    if (half == 1) {
-#pragma unroll
-      for (int k = 0; k < P; ++k) v[k] = cmulc<T>(v[k], twL[t + TT * k]);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < P; ++k) lds[lds_phys(lbase + (t + TT * k) * LSTRIDE)] = v[k];
-    __syncthreads();
+      fft_line<T, H, P, +1, LSTRIDE, Cfg::WAVE>(v, lds, lbase, t, tab);
+    };
+    inv_half(std::integral_constant<int, 0>{}, va);
+    inv_half(std::integral_constant<int, 1>{}, vb);
+    // combine in registers: y[p] = ye + conj(W_L^p) yo, y[p+H] = ye - conj(W_L^p) yo; crop.
     const int out_len = d.out.len;
     const T* dot_re = nullptr; const T* dot_im = nullptr;
     if constexpr (REAL_OUT) {
@@ -296,43 +388,162 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
         dot_im = dot_re + d.out.r_stride;
       }
     }
+    T dsum = 0;
+    // opaque copies: positions/offsets are recomputed here instead of being kept live (in
+    // registers or scratch) from the loads at the top of the kernel
+    asm volatile("" : "+v"(t));
+    if constexpr (LAY == LAY_STRIDED) asm volatile("" : "+v"(lc));
 #pragma unroll
     for (int k = 0; k < P; ++k) {
       const int p = t + TT * k;
-      const C2<T> o = lds_other[lds_phys(lbase + p * LSTRIDE)];
-      const C2<T> y = half == 0 ? cadd<T>(v[k], o) : csub<T>(o, v[k]);
-      const int pp = p + half * H;
-      if (valid && pp < out_len) {
-        if constexpr (REAL_OUT) {
-          out_re[pp] = y.x;
-          if (dot_re != nullptr) dsum += y.x * dot_re[pp];
-          if constexpr (RP_OUT) {
-            if (has2) {
-              out_im[pp] = y.y;
-              if (dot_re != nullptr) dsum += y.y * dot_im[pp];
+      const C2<T> wo = cmulc<T>(vb[k], tab[p]);
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const C2<T> y = hh == 0 ? cadd<T>(va[k], wo) : csub<T>(va[k], wo);
+        const int pp = p + hh * H;
+        if (valid && pp < out_len) {
+          if constexpr (REAL_OUT) {
+            out_re[pp] = y.x;
+            if (dot_re != nullptr) dsum += y.x * dot_re[pp];
+            if constexpr (RP_OUT) {
+              if (has2) {
+                out_im[pp] = y.y;
+                if (dot_re != nullptr) dsum += y.y * dot_im[pp];
+              }
             }
+          } else {
+            out_c[out_at(pp)] = y;
           }
-        } else {
-          out_c[(int64_t)pp * ops] = y;
         }
       }
     }
-  }
-
-  if constexpr (REAL_OUT) {
-    if (d.partial != nullptr) {
-      // per-line fused dot: every thread parks its partial sum; the line's first thread of
-      // the even group adds both groups' sums in fixed order (deterministic) -> partial[q][r].
-      T* red = reinterpret_cast<T*>(smem_raw);
-      __syncthreads();
-      red[threadIdx.x] = dsum;
-      __syncthreads();
-      if (half == 0 && t == 0 && valid) {
-        T s = 0;
-        for (int k = 0; k < TT; ++k) s += red[tid + k];
-        for (int k = 0; k < TT; ++k) s += red[Cfg::GROUP + tid + k];
-        reinterpret_cast<T*>(d.partial)[(int64_t)q * d.Rn + r] = s;
+    if constexpr (REAL_OUT) {
+      if (d.partial != nullptr) {   // uniform over the block
+        const T s = line_sum<T, TT>(dsum, reinterpret_cast<T*>(smem_raw));
+        if (t == 0 && valid) reinterpret_cast<T*>(d.partial)[(int64_t)q * d.Rn + r] = s;
       }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Wave-split convolution along contiguous complex lines (the 2-D column pass on the
+// transposed intermediate, hgp_api.hip): y = crop(IFFT_L(S . FFT_L(pad x))) per line.
+// The two frequency halves of a line run in two different thread groups (one wavefront each
+// at H = 1024): each group loads the line, forms its half's input (x or x W_L^p), runs the
+// forward FFT, the spectrum product and the inverse FFT with wave-local exchanges only, and
+// the odd group adds the even group's result after ONE block barrier (y = ye + conj(W) yo).
+// Half the registers of a one-group-per-line kernel (no second half held), so twice the
+// waves per SIMD hide the memory and LDS latency; the spectrum of the half is prefetched
+// with the data.
+// ------------------------------------------------------------------------------------------
+template <typename T, int H> struct ConvCfg {
+  static constexpr int P = (H < PMax<T>::v) ? H : PMax<T>::v;
+  static constexpr int TT = H / P;                     // threads per half-line group
+#ifndef HGP_CONV_LINES
+  static constexpr int C0 = 4;
+#else
+  static constexpr int C0 = HGP_CONV_LINES;
+#endif
+  static constexpr int ex_elems(int c) { return 2 * c * H + (2 * c * H) / 16; }
+  static constexpr int lds_bytes_for(int c) { return ex_elems(c) * (int)sizeof(C2<T>) + H * (int)sizeof(C2<T>); }
+  static constexpr int c_lines() {
+    int c = C0 * 64 / TT;            // C0 lines per block at one wave per half-line
+    if (c < 1) c = 1;
+    while (c > 1 && (2 * c * TT > 1024 || lds_bytes_for(c) > LDS_CAP / 2)) c >>= 1;
+    return c;
+  }
+  static constexpr int C = c_lines();
+  static constexpr int THREADS = 2 * C * TT;
+  static constexpr int LDS = lds_bytes_for(C);
+  static constexpr bool WAVE = TT <= 64;
+#ifndef HGP_MINW_CONV
+  static constexpr int MINW = 4;
+#else
+  static constexpr int MINW = HGP_MINW_CONV;
+#endif
+};
+
+template <typename T, int H, bool CPLX_SPEC>
+__global__ __launch_bounds__((ConvCfg<T, H>::THREADS), (ConvCfg<T, H>::MINW)) void k_conv_ws(const PassDesc d) {
+  using Cfg = ConvCfg<T, H>;
+  constexpr int P = Cfg::P, TT = Cfg::TT, C = Cfg::C;
+  if (d.done != nullptr && *d.done) return;                          // uniform: before any barrier
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  C2<T>* lds = reinterpret_cast<C2<T>*>(smem_raw);
+  C2<T>* tab = lds + Cfg::ex_elems(C);
+  {
+    const C2<T>* __restrict__ twg = reinterpret_cast<const C2<T>*>(d.tw);
+    for (int q = threadIdx.x; q < H; q += Cfg::THREADS) tab[q] = twg[q];
+  }
+  const int g = threadIdx.x / TT;          // group: line l = g/2, half = g%2
+  const int t = threadIdx.x - g * TT;
+  const int l = g >> 1;
+  const int half = g & 1;
+  const int gbase = g * H;                 // this group's exchange image (logical, lds_phys pads)
+  const int64_t line = (int64_t)blockIdx.x * C + l;
+  int q = (int)(line / d.Rn);
+  int r = (int)(line - (int64_t)q * d.Rn);
+  const bool valid = q < d.Q;
+  if (!valid) { q = 0; r = 0; }
+  const C2<T>* in_c = reinterpret_cast<const C2<T>*>(d.in.ptr) + (int64_t)q * d.in.q_stride + (int64_t)r * d.in.r_stride;
+  C2<T>* out_c = reinterpret_cast<C2<T>*>(d.out.ptr) + (int64_t)q * d.out.q_stride + (int64_t)r * d.out.r_stride;
+  const int in_len = d.in.len;
+
+  // prefetch: this half's spectrum (real or complex) and the line (x[p], p < H; in_len <= H)
+  T sre[P];
+  C2<T> scx[P];
+  const int sp = (int)d.spec_p;
+  if constexpr (!CPLX_SPEC) {
+    const T* sb = reinterpret_cast<const T*>(d.spec) + (int64_t)r * d.spec_r;
+#pragma unroll
+    for (int k = 0; k < P; ++k) sre[k] = sb[(half * H + t + TT * k) * sp];
+  } else {
+    const C2<T>* sb = reinterpret_cast<const C2<T>*>(d.spec) + (int64_t)r * d.spec_r;
+#pragma unroll
+    for (int k = 0; k < P; ++k) scx[k] = sb[(half * H + t + TT * k) * sp];
+  }
+  C2<T> v[P];
+#pragma unroll
+  for (int k = 0; k < P; ++k) {
+    const int p = t + TT * k;
+    C2<T> a = in_c[p < in_len ? p : in_len - 1];
+    if (p >= in_len) a = mk<T>(0, 0);
+    v[k] = a;
+  }
+  __syncthreads();   // twiddle table staged
+  if (half) {
+#pragma unroll
+    for (int k = 0; k < P; ++k) v[k] = cmul<T>(v[k], tab[t + TT * k]);
+  }
+  fft_line<T, H, P, -1, 1, Cfg::WAVE>(v, lds, gbase, t, tab);
+  if constexpr (!CPLX_SPEC) {
+#pragma unroll
+    for (int k = 0; k < P; ++k) v[k] = mk<T>(v[k].x * sre[k], v[k].y * sre[k]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < P; ++k) v[k] = d.spec_kind == SPEC_CPLX ? cmul<T>(v[k], scx[k]) : cmulc<T>(v[k], scx[k]);
+  }
+  fft_line<T, H, P, +1, 1, Cfg::WAVE>(v, lds, gbase, t, tab);
+  // combine: the even group parks ye in its image, the odd group adds conj(W_L^p) yo
+  xsync<Cfg::WAVE>();
+  if (!half) {
+#pragma unroll
+    for (int k = 0; k < P; ++k) lds[lds_phys(gbase + t + TT * k)] = v[k];
+  }
+  __syncthreads();
+  if (half && valid) {
+    const int out_len = d.out.len;
+    const int ebase = gbase - H;
+    int tt = t;
+    asm volatile("" : "+v"(tt));
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+      const int p = tt + TT * k;
+      const C2<T> ye = lds[lds_phys(ebase + p)];
+      const C2<T> wo = cmulc<T>(v[k], tab[p]);
+      if (p < out_len) out_c[p] = cadd<T>(ye, wo);
+      if (p + H < out_len) out_c[p + H] = csub<T>(ye, wo);
     }
   }
 }

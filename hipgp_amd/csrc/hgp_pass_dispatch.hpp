@@ -2,6 +2,7 @@
 // hgp_pass_f32.hip / hgp_pass_f64.hip so the two compile in parallel).
 #pragma once
 #include "hgp_internal.hpp"
+#include "hgp_rows.hpp"
 
 namespace hgp {
 
@@ -28,9 +29,14 @@ static hipError_t launch_h(int mode, int lay, const PassDesc& d, int64_t nblocks
   } else if (mode == PASS_INV) {
     if (lay == LAY_STRIDED) return launch_one<T, H, PASS_INV, LAY_STRIDED>(d, nblocks, s);
     if (lay == LAY_RP) return launch_one<T, H, PASS_INV, LAY_RP>(d, nblocks, s);
-  } else {
+  } else if (mode == PASS_CONV) {
     if (lay == LAY_STRIDED) return launch_one<T, H, PASS_CONV, LAY_STRIDED>(d, nblocks, s);
+    if (lay == LAY_CONTIG) return launch_one<T, H, PASS_CONV, LAY_CONTIG>(d, nblocks, s);
     if (lay == LAY_R1) return launch_one<T, H, PASS_CONV, LAY_R1>(d, nblocks, s);
+  } else if (mode == PASS_CONVC) {
+    if (lay == LAY_STRIDED) return launch_one<T, H, PASS_CONVC, LAY_STRIDED>(d, nblocks, s);
+    if (lay == LAY_CONTIG) return launch_one<T, H, PASS_CONVC, LAY_CONTIG>(d, nblocks, s);
+    if (lay == LAY_R1) return launch_one<T, H, PASS_CONVC, LAY_R1>(d, nblocks, s);
   }
   return hipErrorInvalidValue;
 }
@@ -59,6 +65,29 @@ static PassGeom geom_h(int lay) {
     case 8192: return FN<T, 8192>(__VA_ARGS__);                                                      \
     default: break;                                                                                  \
   }
+
+template <typename T, int H>
+static hipError_t launch_rowt_h(int inv, const PassDesc& d, hipStream_t s) {
+  using Cfg = RowTCfg<T, H>;
+  const int64_t nb = (int64_t)d.Q * ((d.Rn + Cfg::C - 1) / Cfg::C);
+  if (nb <= 0) return hipSuccess;
+  static bool attr_set[2] = {false, false};
+  const void* fn = inv ? (const void*)k_row_inv_t<T, H> : (const void*)k_row_fwd_t<T, H>;
+  if (!attr_set[inv]) {
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS);
+    if (e != hipSuccess) return e;
+    attr_set[inv] = true;
+  }
+  if (inv) hipLaunchKernelGGL((k_row_inv_t<T, H>), dim3((unsigned)nb), dim3(Cfg::THREADS), Cfg::LDS, s, d);
+  else hipLaunchKernelGGL((k_row_fwd_t<T, H>), dim3((unsigned)nb), dim3(Cfg::THREADS), Cfg::LDS, s, d);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_rowt(int H, int inv, const PassDesc& d, hipStream_t s) {
+  HGP_H_SWITCH(launch_rowt_h, inv, d, s)
+  return hipErrorInvalidValue;
+}
 
 template <typename T>
 hipError_t launch_pass(int H, int mode, int lay, const PassDesc& d, int64_t nblocks, hipStream_t s) {

@@ -1,0 +1,251 @@
+// hgp_rows.hpp — row-pair passes of the 2-D operators with a COLUMN-MAJOR intermediate.
+//
+// The 2-D Toeplitz operator y = crop(IFFT2(S . FFT2(pad x))) runs as three passes:
+//   k_row_fwd_t : real rows (2j, 2j+1) of one RHS -> one complex FFT (pair packed as Re/Im),
+//                 Hermitian split into the two rows' half spectra, stored TRANSPOSED:
+//                 W[q][c][i0] (compact column c = 0..H, row i0), through an LDS tile so that
+//                 each column gets one contiguous 2C-row segment (C pairs per block).
+//   k_pass<CONTIG, CONV> (hgp_pass.hpp) : per column c, a contiguous complex line of m0
+//                 values: pad -> FFT -> x spectrum -> IFFT -> crop, wave-local exchanges.
+//   k_row_inv_t : the column-major tiles back through LDS, Hermitian rebuild of the pair,
+//                 inverse FFT, crop, real rows out (+ fused per-pair dot with a second vector).
+// Compared with a row-major intermediate this turns the heavy pass (4 FFTs per line) into a
+// barrier-free contiguous-line kernel; the transposition costs one LDS tile round trip in
+// each row pass.  Compact columns: c <= H/2 holds even frequency 2c, c > H/2 odd frequency
+// 2(c - H/2 - 1) + 1 (the order the frequency halves leave the FFT in, hgp_fft.hpp).
+#pragma once
+#include "hgp_pass.hpp"
+
+#ifndef HGP_ROWT_PAIRS
+#define HGP_ROWT_PAIRS 8          // row pairs per block (16 rows = 128-B column segments)
+#endif
+
+namespace hgp {
+
+template <typename T, int H> struct RowTCfg {
+  static constexpr int P = (H < PMax<T>::v) ? H : PMax<T>::v;
+  static constexpr int TT = H / P;
+  // exchange images: pair l owns logical elements [l*H, (l+1)*H), padded by lds_phys
+  static constexpr int ex_elems(int c) { return c * H + (c * H) / 16; }
+  static constexpr int TS(int c) { return 2 * c + 1; }           // tile row pitch (pad: banks)
+  static constexpr int tile_elems(int c) { return (H / 2 + 1) * TS(c); }
+  static constexpr int area(int c) { return ex_elems(c) > tile_elems(c) ? ex_elems(c) : tile_elems(c); }
+  static constexpr int lds_bytes_for(int c) { return (area(c) + H) * (int)sizeof(C2<T>); }
+  static constexpr int c_pairs() {
+    int c = HGP_ROWT_PAIRS * 64 / TT;              // 512 threads at the default
+    if (c < 1) c = 1;
+    if (c > 64) c = 64;                            // tiny rows: cap the tile height
+    while (c > 1 && (c * TT > 1024 || lds_bytes_for(c) > LDS_CAP)) c >>= 1;
+    return c;
+  }
+  static constexpr int C = c_pairs();
+  static constexpr int THREADS = C * TT;
+  static constexpr int AREA = area(C);
+  static constexpr int LDS = lds_bytes_for(C);
+  static constexpr int PITCH = TS(C);
+  static constexpr bool WAVE = TT <= 64;
+  static constexpr int BLOCKS_BY_LDS = LDS_CAP / LDS;
+  static constexpr int MINW_LDS = (BLOCKS_BY_LDS * ((THREADS + 63) / 64)) / 4;
+  static constexpr int MINW = MINW_LDS < 1 ? 1 : (MINW_LDS > 4 ? 4 : MINW_LDS);
+};
+
+// Real row pairs -> column-major compact half spectra.
+//   in : View{x, q_stride (elements per RHS), r_stride (row pitch), 1, len = row length}
+//   out: View{W, q_stride (complex per RHS), r_stride = column pitch S0, 1, 0}
+//   Q RHS, Rn pairs per RHS (= ceil(nrows / 2)), grid = Q * ceil(Rn / C).
+template <typename T, int H>
+__global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) void k_row_fwd_t(const PassDesc d) {
+  using Cfg = RowTCfg<T, H>;
+  constexpr int P = Cfg::P, TT = Cfg::TT, C = Cfg::C, PITCH = Cfg::PITCH;
+  if (d.done != nullptr && *d.done) return;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  C2<T>* lds = reinterpret_cast<C2<T>*>(smem_raw);
+  C2<T>* tab = lds + Cfg::AREA;
+  {
+    const C2<T>* __restrict__ twg = reinterpret_cast<const C2<T>*>(d.tw);
+    for (int q = threadIdx.x; q < H; q += Cfg::THREADS) tab[q] = twg[q];
+  }
+  const int nrb = (d.Rn + C - 1) / C;
+  const int q = blockIdx.x / nrb;
+  const int rb = blockIdx.x - q * nrb;
+  const int l = threadIdx.x / TT;
+  const int t = threadIdx.x - l * TT;
+  const int lbase = l * H;
+  const int rp = rb * C + l;                       // this group's pair
+  const bool pvalid = (l < C) && (rp < d.Rn);
+  const int row_a = pvalid ? 2 * rp : 0;
+  const bool has2 = pvalid && (2 * rp + 1 < d.nrows);
+  const T* in_a = reinterpret_cast<const T*>(d.in.ptr) + (int64_t)q * d.in.q_stride + (int64_t)row_a * d.in.r_stride;
+  const T* in_b = has2 ? in_a + d.in.r_stride : in_a;
+  const int in_len = d.in.len;
+
+  C2<T> va[P], vb[P];
+#pragma unroll
+  for (int k = 0; k < P; ++k) {
+    const int p = t + TT * k;
+    const int pc = p < in_len ? p : in_len - 1;
+    const T re = in_a[pc];
+    const T im = in_b[pc];
+    C2<T> a = mk<T>(re, has2 ? im : (T)0);
+    if (p >= in_len) a = mk<T>(0, 0);
+    va[k] = a;
+  }
+  __syncthreads();   // twiddle table staged
+#pragma unroll
+  for (int k = 0; k < P; ++k) vb[k] = cmul<T>(va[k], tab[t + TT * k]);
+
+  C2<T>* W = reinterpret_cast<C2<T>*>(d.out.ptr) + (int64_t)q * d.out.q_stride;
+  const int64_t S0 = d.out.r_stride;
+  const int row0 = 2 * rb * C;                     // first row of this block's tile
+  const int nrow_blk = d.nrows - row0 < 2 * C ? d.nrows - row0 : 2 * C;
+
+  auto do_half = [&](auto half_c, C2<T>(&v)[P]) {
+    constexpr int half = decltype(half_c)::value;
+    fft_line<T, H, P, -1, 1, Cfg::WAVE>(v, lds, lbase, t, tab);
+    // Hermitian split through this group's exchange image
+    xsync<Cfg::WAVE>();
+#pragma unroll
+    for (int k = 0; k < P; ++k) lds[lds_phys(lbase + t + TT * k)] = v[k];
+    xsync<Cfg::WAVE>();
+    C2<T> A[P], B[P];
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+      const int p = t + TT * k;
+      const int pp = (half == 0) ? ((H - p) & (H - 1)) : (H - 1 - p);
+      const C2<T> zp = lds[lds_phys(lbase + pp)];
+      const T hf = (T)0.5;
+      A[k] = mk<T>(hf * (v[k].x + zp.x), hf * (v[k].y - zp.y));    // (Z + conj Zp)/2
+      B[k] = mk<T>(hf * (v[k].y + zp.y), -hf * (v[k].x - zp.x));   // (Z - conj Zp)/2i
+    }
+    __syncthreads();   // every group done with its exchange image: the tile overlays them
+    // tile[col][row]: col = compact column - first column of the half, row = 2l + {0,1}
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+      const int p = t + TT * k;
+      const bool store = (half == 0) ? (p <= H / 2) : (p < H / 2);
+      if (store && l < C) {
+        lds[p * PITCH + 2 * l] = A[k];
+        lds[p * PITCH + 2 * l + 1] = B[k];
+      }
+    }
+    __syncthreads();
+    // column segments: rows-fast, 2C rows x sizeof(complex) contiguous per column
+    constexpr int NCOL = (half == 0) ? H / 2 + 1 : H / 2;
+    constexpr int C0 = (half == 0) ? 0 : H / 2 + 1;
+    constexpr int NE = NCOL * 2 * C;
+    for (int e = threadIdx.x; e < NE; e += Cfg::THREADS) {
+      const int col = e / (2 * C);
+      const int row = e - col * (2 * C);
+      if (row < nrow_blk) W[(int64_t)(C0 + col) * S0 + row0 + row] = lds[col * PITCH + row];
+    }
+    __syncthreads();   // tile read before the next half's FFT reuses the area
+  };
+  do_half(std::integral_constant<int, 0>{}, va);
+  do_half(std::integral_constant<int, 1>{}, vb);
+}
+
+// Column-major compact half spectra -> real row pairs (crop), optional fused dot.
+//   in : View{W, q_stride, r_stride = column pitch S0, 1, 0}
+//   out: View{y, q_stride (elements per RHS), r_stride (row pitch), 1, len = out row length}
+//   nrows = output rows per RHS, Rn = ceil(nrows / 2); dot/partial as in k_pass.
+template <typename T, int H>
+__global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) void k_row_inv_t(const PassDesc d) {
+  using Cfg = RowTCfg<T, H>;
+  constexpr int P = Cfg::P, TT = Cfg::TT, C = Cfg::C, PITCH = Cfg::PITCH;
+  if (d.done != nullptr && *d.done) return;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  C2<T>* lds = reinterpret_cast<C2<T>*>(smem_raw);
+  C2<T>* tab = lds + Cfg::AREA;
+  {
+    const C2<T>* __restrict__ twg = reinterpret_cast<const C2<T>*>(d.tw);
+    for (int q = threadIdx.x; q < H; q += Cfg::THREADS) tab[q] = twg[q];
+  }
+  const int nrb = (d.Rn + C - 1) / C;
+  const int q = blockIdx.x / nrb;
+  const int rb = blockIdx.x - q * nrb;
+  const int l = threadIdx.x / TT;
+  const int t = threadIdx.x - l * TT;
+  const int lbase = l * H;
+  const int rp = rb * C + l;
+  const bool pvalid = (l < C) && (rp < d.Rn);
+  const bool has2 = pvalid && (2 * rp + 1 < d.nrows);
+  const C2<T>* W = reinterpret_cast<const C2<T>*>(d.in.ptr) + (int64_t)q * d.in.q_stride;
+  const int64_t S0 = d.in.r_stride;
+  const int row0 = 2 * rb * C;
+  const int nrow_blk = d.nrows - row0 < 2 * C ? d.nrows - row0 : 2 * C;
+
+  C2<T> va[P], vb[P];
+  auto do_half = [&](auto half_c, C2<T>(&v)[P]) {
+    constexpr int half = decltype(half_c)::value;
+    constexpr int NCOL = (half == 0) ? H / 2 + 1 : H / 2;
+    constexpr int C0 = (half == 0) ? 0 : H / 2 + 1;
+    constexpr int NE = NCOL * 2 * C;
+    __syncthreads();   // previous users of the area are done (twiddles staged, first half)
+    for (int e = threadIdx.x; e < NE; e += Cfg::THREADS) {
+      const int col = e / (2 * C);
+      const int row = e - col * (2 * C);
+      const int rr = row < nrow_blk ? row : 0;
+      C2<T> val = W[(int64_t)(C0 + col) * S0 + row0 + rr];
+      if (row >= nrow_blk) val = mk<T>(0, 0);
+      lds[col * PITCH + row] = val;
+    }
+    __syncthreads();
+    // Hermitian rebuild Z = A + iB of the pair at frequency half `half`, position p
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+      const int p = t + TT * k;
+      bool cj;
+      int c;
+      if (half == 0) { cj = p > H / 2; c = cj ? H - p : p; }
+      else { cj = p >= H / 2; c = cj ? H - 1 - p : p; }
+      const int li = l < C ? l : 0;
+      C2<T> A = lds[c * PITCH + 2 * li];
+      C2<T> B = lds[c * PITCH + 2 * li + 1];
+      if (!has2) B = mk<T>(0, 0);
+      if (cj) { A.y = -A.y; B.y = -B.y; }
+      v[k] = mk<T>(A.x - B.y, A.y + B.x);
+    }
+    __syncthreads();   // tile consumed: the FFT exchange images overlay it
+    fft_line<T, H, P, +1, 1, Cfg::WAVE>(v, lds, lbase, t, tab);
+  };
+  do_half(std::integral_constant<int, 0>{}, va);
+  do_half(std::integral_constant<int, 1>{}, vb);
+
+  // combine: y[p] = ye + conj(W_L^p) yo, y[p+H] = ye - conj(W_L^p) yo; real rows out
+  const int out_len = d.out.len;
+  T* out_a = reinterpret_cast<T*>(d.out.ptr) + (int64_t)q * d.out.q_stride + (int64_t)(pvalid ? 2 * rp : 0) * d.out.r_stride;
+  T* out_b = out_a + d.out.r_stride;
+  const T* dot_a = nullptr;
+  const T* dot_b = nullptr;
+  if (d.partial != nullptr) {
+    dot_a = reinterpret_cast<const T*>(d.dot) + (out_a - reinterpret_cast<T*>(d.out.ptr));
+    dot_b = dot_a + d.out.r_stride;
+  }
+  T dsum = 0;
+  int tt = t;
+  asm volatile("" : "+v"(tt));
+#pragma unroll
+  for (int k = 0; k < P; ++k) {
+    const int p = tt + TT * k;
+    const C2<T> wo = cmulc<T>(vb[k], tab[p]);
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const C2<T> y = hh == 0 ? cadd<T>(va[k], wo) : csub<T>(va[k], wo);
+      const int pp = p + hh * H;
+      if (pvalid && pp < out_len) {
+        out_a[pp] = y.x;
+        if (dot_a != nullptr) dsum += y.x * dot_a[pp];
+        if (has2) {
+          out_b[pp] = y.y;
+          if (dot_a != nullptr) dsum += y.y * dot_b[pp];
+        }
+      }
+    }
+  }
+  if (d.partial != nullptr) {   // uniform over the block
+    const T s = line_sum<T, TT>(dsum, reinterpret_cast<T*>(smem_raw));
+    if (t == 0 && pvalid) reinterpret_cast<T*>(d.partial)[(int64_t)q * d.Rn + rp] = s;
+  }
+}
+
+}  // namespace hgp

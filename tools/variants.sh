@@ -1,0 +1,24 @@
+#!/bin/bash
+# Block-shape variants of libhipgp for tuning: build here (BUILD=1), time on the GPU box.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+declare -A V
+V[v1]="-DHGP_CMAX_STRIDED=16 -DHGP_MINW_STRIDED=4 -DHGP_ROW_THREADS=256 -DHGP_MINW_ROW=3"
+V[v2]="-DHGP_CMAX_STRIDED=8 -DHGP_MINW_STRIDED=3 -DHGP_ROW_THREADS=256 -DHGP_MINW_ROW=3"
+V[v3]="-DHGP_CMAX_STRIDED=4 -DHGP_MINW_STRIDED=3 -DHGP_ROW_THREADS=512 -DHGP_MINW_ROW=2"
+V[v4]="-DHGP_CMAX_STRIDED=8 -DHGP_MINW_STRIDED=4 -DHGP_ROW_THREADS=128 -DHGP_MINW_ROW=4"
+V[v5]="-DHGP_CMAX_STRIDED=8 -DHGP_MINW_STRIDED=2 -DHGP_ROW_THREADS=256 -DHGP_MINW_ROW=2"
+if [ -n "$BUILD" ]; then
+  for k in "${!V[@]}"; do make -s -C hipgp_amd/csrc VARIANT=$k VFLAGS="${V[$k]}" -j4 & done; wait
+  exit 0
+fi
+mkdir -p gpurun_out
+for k in $(echo "${!V[@]}" | tr ' ' '\n' | sort); do
+  HGP_LIB=$PWD/hipgp_amd/libhipgp_$k.so timeout -k 10 120 python bench.py --no-cpu-baseline --steps 20 --warmup 5 --pcg-reps 2 ${BENCH_ARGS:-} > gpurun_out/var_$k.json 2> gpurun_out/var_$k.err || { echo "$k failed"; tail -5 gpurun_out/var_$k.err; exit 1; }
+  python - "$k" "${V[$k]}" <<'PY'
+import json, sys
+d = json.loads(open(f"gpurun_out/var_{sys.argv[1]}.json").read().strip().splitlines()[-1])
+r = d["roofline"]
+print(sys.argv[1], sys.argv[2], "| value", round(d["value"]), "frac", round(r["frac"], 3), "pcg_ms", round(d["pcg_wall_clock_ms"], 2),
+      "passes", [(p["ms"], p["gbs"]) for p in r["passes"]])
+PY
+done
