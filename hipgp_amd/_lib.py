@@ -24,7 +24,7 @@ EXPORTS = (
     "hgp_plan_create", "hgp_plan_set_stream", "hgp_plan_set_column", "hgp_toeplitz_apply",
     "hgp_pcg_solve", "hgp_pcg_begin", "hgp_pcg_step", "hgp_get_spectrum", "hgp_rowdot",
     "hgp_plan_info", "hgp_plan_destroy", "hgp_last_error", "hgp_version",
-    "hgp_toeplitz_apply_pass", "hgp_op_pass_count",
+    "hgp_toeplitz_apply_pass", "hgp_op_pass_count", "hgp_pcg_rnorm2",
 )
 
 
@@ -61,6 +61,7 @@ def lib():
         "hgp_version": (ctypes.c_char_p, []),
         "hgp_toeplitz_apply_pass": (i32, [vp, i32, vp, vp, i64, i32]),
         "hgp_op_pass_count": (i32, [vp]),
+        "hgp_pcg_rnorm2": (i32, [vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

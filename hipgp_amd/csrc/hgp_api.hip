@@ -668,6 +668,17 @@ int hgp_pcg_solve(hgp_plan* plan, const void* b, void* x, int64_t nrhs, int maxi
   return 0;
 }
 
+int hgp_pcg_rnorm2(hgp_plan* plan, void* out) {
+  HGP_TRY(check_plan(plan));
+  if (!plan->cg_active) return fail(HGP_E_STATE, "hgp_pcg_begin has not been called");
+  if (out == nullptr) return fail(HGP_E_ARG, "null out");
+  HGP_TRY(use_device(plan));
+  const size_t es = plan->dtype == HGP_F64 ? 8 : 4;
+  const char* rnew = reinterpret_cast<const char*>(plan->scal.ptr) + 3 * plan->cg_nrhs * es;
+  HIP_TRY(hipMemcpyAsync(out, rnew, plan->cg_nrhs * es, hipMemcpyDeviceToDevice, plan->stream));
+  return 0;
+}
+
 int hgp_get_spectrum(hgp_plan* plan, int which, void* out) {
   HGP_TRY(check_plan(plan));
   if (!plan->have_spec) return fail(HGP_E_STATE, "hgp_plan_set_column has not been called");

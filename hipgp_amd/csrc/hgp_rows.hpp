@@ -133,10 +133,13 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
     constexpr int NCOL = (half == 0) ? H / 2 + 1 : H / 2;
     constexpr int C0 = (half == 0) ? 0 : H / 2 + 1;
     constexpr int NE = NCOL * 2 * C;
-    for (int e = threadIdx.x; e < NE; e += Cfg::THREADS) {
+    constexpr int ITER = (NE + Cfg::THREADS - 1) / Cfg::THREADS;
+#pragma unroll
+    for (int j = 0; j < ITER; ++j) {
+      const int e = threadIdx.x + j * Cfg::THREADS;
       const int col = e / (2 * C);
       const int row = e - col * (2 * C);
-      if (row < nrow_blk) W[(int64_t)(C0 + col) * S0 + row0 + row] = lds[col * PITCH + row];
+      if (e < NE && row < nrow_blk) W[(int64_t)(C0 + col) * S0 + row0 + row] = lds[col * PITCH + row];
     }
     __syncthreads();   // tile read before the next half's FFT reuses the area
   };
@@ -181,13 +184,25 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
     constexpr int C0 = (half == 0) ? 0 : H / 2 + 1;
     constexpr int NE = NCOL * 2 * C;
     __syncthreads();   // previous users of the area are done (twiddles staged, first half)
-    for (int e = threadIdx.x; e < NE; e += Cfg::THREADS) {
-      const int col = e / (2 * C);
-      const int row = e - col * (2 * C);
+    constexpr int ITER = (NE + Cfg::THREADS - 1) / Cfg::THREADS;
+    C2<T> buf[ITER];
+#pragma unroll
+    for (int j = 0; j < ITER; ++j) {         // all global loads in flight at once
+      const int e = threadIdx.x + j * Cfg::THREADS;
+      const int ee = e < NE ? e : NE - 1;
+      const int col = ee / (2 * C);
+      const int row = ee - col * (2 * C);
       const int rr = row < nrow_blk ? row : 0;
       C2<T> val = W[(int64_t)(C0 + col) * S0 + row0 + rr];
       if (row >= nrow_blk) val = mk<T>(0, 0);
-      lds[col * PITCH + row] = val;
+      buf[j] = val;
+    }
+#pragma unroll
+    for (int j = 0; j < ITER; ++j) {
+      const int e = threadIdx.x + j * Cfg::THREADS;
+      const int col = e / (2 * C);
+      const int row = e - col * (2 * C);
+      if (e < NE) lds[col * PITCH + row] = buf[j];
     }
     __syncthreads();
     // Hermitian rebuild Z = A + iB of the pair at frequency half `half`, position p

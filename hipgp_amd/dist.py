@@ -1,0 +1,80 @@
+"""Right-hand-side sharding of the HIP-GP hot path over GPUs (one process per GPU).
+
+SURVEY §8(e): every CG scalar is per right-hand side (`cg.py:64,66,69,74`), so a minibatch's
+observations split into contiguous shards, one per rank, and each rank runs set-up + PCG + R^T
+for its own rows with NO collective inside the solve.  Two places couple ranks:
+
+* the all-RHS break rule of `cg.py:70` — `ToeplitzPlan.pcg_allranks` applies it exactly with one
+  all-reduce(MIN) of an int flag per iteration (only when `exact_break=True`; with the usual
+  fp32 / tol 1e-8 it never fires and ranks run `maxiter` steps on their own);
+* the mean-field natural-gradient statistics (`hipgp.py:234-250`): sum_n a_n, sum_n ivar kn^2
+  and -sum_n ivar (kn.m - y) kn — one all-reduce(SUM) of a packed (2M' + 1) buffer per
+  minibatch, after which every rank holds identical theta gradients.
+
+Backend: "nccl" (= RCCL over xGMI on ROCm) on GPUs, "gloo" for the CPU tests.
+"""
+import torch
+import torch.distributed as dist
+
+
+def world():
+    """(world_size, rank) of the default group, (1, 0) when torch.distributed is not up."""
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(), dist.get_rank()
+    return 1, 0
+
+
+def rhs_shard(n, world_size, rank):
+    """Contiguous, balanced slice of n right-hand sides owned by `rank` (sizes differ by <= 1)."""
+    base, extra = divmod(n, world_size)
+    start = rank * base + min(rank, extra)
+    return slice(start, start + base + (1 if rank < extra else 0))
+
+
+def allreduce_stats(stats, group=None):
+    """Sum the mean-field batch statistics of all ranks in ONE all-reduce of a packed buffer."""
+    ws = dist.get_world_size(group) if dist.is_initialized() else 1
+    if ws == 1:
+        return stats
+    lam, dm = stats["lam_sum"], stats["dm_sum"]
+    buf = torch.cat([lam.reshape(-1), dm.reshape(-1),
+                     torch.stack([torch.as_tensor(stats["an_sum"], dtype=lam.dtype, device=lam.device),
+                                  torch.as_tensor(float(stats["n"]), dtype=lam.dtype, device=lam.device)])])
+    if dist.get_backend(group) == "gloo" and buf.is_cuda:
+        host = buf.cpu()
+        dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
+        buf = host.to(lam.device)
+    else:
+        dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
+    k = lam.numel()
+    return {"lam_sum": buf[:k], "dm_sum": buf[k:2 * k], "an_sum": buf[2 * k], "n": int(round(float(buf[2 * k + 1])))}
+
+
+def sharded_compute_kn(model, Knm_local, maxiter_cg=20, tol=1e-8, exact_break=False, group=None, Kmm=None):
+    """kn = R^T K^{-1} Knm^T for this rank's rows (`hipgp.py:117-146`).  exact_break applies
+    the all-RHS break rule across ranks (see module docstring)."""
+    if Kmm is None:
+        Kmm = model.toeplitz()
+    if exact_break:
+        d0, _ = Kmm._plan.pcg_allranks(Knm_local, maxiter_cg, tol, precond=True, group=group)
+    else:
+        d0 = Kmm.inv_matmul(Knm_local, do_precond=True, maxiter=maxiter_cg, tol=tol)
+    return Kmm._matmul_by_RT(d0)
+
+
+def sharded_elbo_and_grad(model, xbatch, ybatch, noise_std_batch=None, maxiter_cg=20, tol=1e-8,
+                          exact_break=False, group=None, compute_kn=None):
+    """`MeanFieldToeplitzGP.elbo_and_grad` with the minibatch sharded by rows over the ranks
+    of `group`; every rank passes the SAME full minibatch and gets the same ELBO and grads.
+    `compute_kn(model, Knm_local)` may be injected (tests run the host logic on CPU)."""
+    ws = dist.get_world_size(group) if dist.is_initialized() else 1
+    rk = dist.get_rank(group) if dist.is_initialized() else 0
+    sl = rhs_shard(xbatch.shape[0], ws, rk)
+    Knm, Knn_diag = model._make_grams(xbatch[sl])
+    if compute_kn is None:
+        kn = sharded_compute_kn(model, Knm, maxiter_cg=maxiter_cg, tol=tol, exact_break=exact_break, group=group)
+    else:
+        kn = compute_kn(model, Knm)
+    nsd = None if noise_std_batch is None else noise_std_batch[sl]
+    stats = allreduce_stats(model.batch_stats(kn, ybatch[sl], Knn_diag, nsd), group=group)
+    return model.apply_stats(stats, xbatch.shape[0])

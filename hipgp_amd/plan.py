@@ -122,6 +122,31 @@ class ToeplitzPlan:
                 callback(n, x)
         return x
 
+    def pcg_allranks(self, b, maxiter, tol, precond=True, group=None):
+        """PCG on this rank's right-hand sides with the reference's break rule applied over
+        ALL ranks' RHS (`cg.py:69-71`): each step runs without a local break, then one
+        all-reduce(MIN) of "every sqrt(r.r) < tol here" decides for everybody.  Returns
+        (x, iterations)."""
+        import torch.distributed as dist
+        b = self._vec(b, "b", self.M)
+        x = torch.empty_like(b)
+        self._bind_stream()
+        check(lib().hgp_pcg_begin(self._h, ctypes.c_void_p(b.data_ptr()), ctypes.c_void_p(x.data_ptr()),
+                                  b.shape[0], int(bool(precond)), _lib.LAYOUT_ROWS))
+        rn = torch.empty(b.shape[0], dtype=self.dtype, device=self.device)
+        # the flag travels on the device for RCCL ("nccl"), on the host for gloo
+        fdev = "cpu" if dist.get_backend(group) == "gloo" else self.device
+        flag = torch.empty(1, dtype=torch.int32, device=fdev)
+        it = 0
+        for it in range(1, int(maxiter) + 1):
+            check(lib().hgp_pcg_step(self._h, -1.0, None))
+            check(lib().hgp_pcg_rnorm2(self._h, ctypes.c_void_p(rn.data_ptr())))
+            flag.fill_(int(bool(torch.all(torch.sqrt(rn) < tol))))
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+            if int(flag.item()):
+                break
+        return x, it
+
     def __del__(self):
         h = getattr(self, "_h", None)
         if h is not None and _lib._lib is not None:

@@ -1,0 +1,307 @@
+"""Toeplitz-whitened SVGP ("HIP-GP") models on the MI355X operators.
+
+Mirrors the reference model API of `ziggy/hipgp.py` for the parts that sit on the hot path:
+`ToeplitzInducingGP.compute_kn` (`hipgp.py:117-146`) and the mean-field
+family's ELBO, natural gradient and prediction (`hipgp.py:160-276, 370-446, 449-524`,
+SURVEY §8(f) row 3).  `kn = R^T K^{-1} Knm^T` runs as one plan set-up + hgp_pcg_solve +
+hgp_toeplitz_apply(R^T) on the device; the batch reductions are device tensor ops.
+
+The natural-gradient statistics are split into per-RHS sums (`mf_batch_stats`) and the update
+built from them (`mf_apply_stats`), so a caller that shards the minibatch over GPUs
+(`hipgp_amd.dist`) all-reduces exactly those sums.
+
+Not built here (OUT of the hot path): integrated observations (row f2), block /
+full-rank variational families, kernel-hyper-parameter learning through the solve (row f4),
+`batch_solve`'s dense M'xM' system.
+"""
+import numpy as np
+import torch
+from torch import nn
+
+from hipgp_amd.ziggy.misc.toeplitz_tensor import ToeplitzTensor
+
+LN_2PI = float(np.log(2 * np.pi))
+
+
+def diag_kl_to_standard(m, S):
+    """KL(N(m, diag S) || N(0, I))  (`ziggy/misc/stats.py:4-8`)."""
+    return 0.5 * (torch.sum(S) + torch.sum(m * m) - torch.sum(torch.log(S)) - m.shape[0])
+
+
+def expanded_size(xgrids):
+    """M' = prod(2 m_i - 2) (m_i > 1) else m_i  (`hipgp.py:72`)."""
+    return int(np.prod([2 * len(g) - 2 if len(g) > 1 else len(g) for g in xgrids]))
+
+
+class SviGP(nn.Module):
+    """Base pieces of `ziggy/svi_gp.py:14-97` the models use: dtype coercion, the point
+    observation gram matrices (`_make_grams`, :48-76) and batched prediction (:78-97)."""
+
+    def __init__(self):
+        super().__init__()
+        self.pred_scale_factor = 1.
+
+    def torch(self, arr):
+        if isinstance(arr, np.ndarray):
+            return torch.tensor(arr, dtype=self.dtype)
+        if isinstance(arr, torch.Tensor):
+            assert arr.dtype == self.dtype, f"model dtype = {self.dtype}, data dtype = {arr.dtype}"
+            return arr
+        raise ValueError(f"Only accepts np.ndarray or torch.Tensor, got {type(arr)}")
+
+    def _make_grams(self, xbatch, integrated_obs=False, semi_integrated_estimator="analytic",
+                    semi_integrated_samps=10):
+        params = self.get_kernel_params()
+        if integrated_obs:
+            raise NotImplementedError("integrated (line-integral) observations: SURVEY §8(f) row 2")
+        return self.kernel(xbatch, self.xinduce, params), self.kernel.diag(xbatch, params)
+
+    def batch_predict(self, x, batch_size, verbose=True, **kwargs):
+        nb = int(np.ceil(len(x) / batch_size))
+        mus, sigs = [], []
+        for b in range(nb):
+            mu, sig = self.predict(x[b * batch_size:(b + 1) * batch_size], **kwargs)
+            mus.append(mu)
+            sigs.append(sig)
+            if verbose and b % 100 == 0:
+                print(" ... batch_predict %d / %d batches" % (b, nb))
+        return torch.cat(mus, dim=0), torch.cat(sigs, dim=0)
+
+
+class ToeplitzInducingGP(SviGP):
+    """`hipgp.py:15-446` (hot-path subset)."""
+
+    def __init__(self, kernel, xgrids, num_obs, sig2_init=1., ell_init=.05, noise2_init=1.,
+                 learn_kernel=True, learn_noise=True, dtype=torch.float, whitened_type='ziggy',
+                 parameterization='expectation-family', jitter_val=1e-3):
+        super().__init__()
+        assert len(xgrids) > 1, len(xgrids)
+        self.learn_kernel = learn_kernel
+        self.learn_noise = learn_noise
+        self.jitter_val = jitter_val
+        self.dtype = dtype
+        self.kernel = kernel
+        self.N = num_obs
+        self.ell = torch.tensor(ell_init, dtype=dtype)
+        self.sig2 = torch.tensor(sig2_init, dtype=dtype)
+        self.noise2 = torch.tensor(noise2_init, dtype=dtype)
+        self.log_ell = nn.Parameter(torch.log(self.ell.clone()), requires_grad=learn_kernel)
+        self.log_sig2 = nn.Parameter(torch.log(self.sig2.clone()), requires_grad=learn_kernel)
+        self.log_noise2 = nn.Parameter(torch.log(self.noise2.clone()), requires_grad=learn_noise)
+        print(f"Model initialization: sig2 = {sig2_init:.2f}, ell_init = {ell_init:.2f}, noise2 = {noise2_init:.2f}")
+        self.xgrids = xgrids
+        mesh = torch.meshgrid(*xgrids, indexing="ij")
+        self.xinduce = torch.stack([g.reshape(-1) for g in mesh], dim=-1)
+        self.M = self.xinduce.shape[0]
+        self.whitened_type = whitened_type
+        if whitened_type == 'cholesky':
+            self.Mprime = self.M
+        else:
+            assert whitened_type == 'ziggy', whitened_type
+            self.Mprime = expanded_size(xgrids)
+        self.parameterization = parameterization
+
+    @property
+    def name(self):
+        raise NotImplementedError
+
+    def cuda_params(self, cuda_num=0):
+        """Move the model and its grids to `cuda:{cuda_num}` (`hipgp.py:80-90`)."""
+        device = torch.device(f"cuda:{cuda_num}")
+        self.to(device)
+        self.xinduce = self.xinduce.to(device)
+        self.kernel = self.kernel.to(device)
+        self.xgrids = [g.to(device) for g in self.xgrids]
+        return self
+
+    def get_kernel_params(self):
+        if not self.learn_kernel:
+            return self.sig2, self.ell
+        return torch.exp(self.log_sig2), torch.exp(self.log_ell)
+
+    def update_kernel_params(self, sig2=None, ell=None):
+        assert not self.learn_kernel
+        if sig2 is not None:
+            self.sig2 = torch.tensor(sig2, dtype=self.dtype, device=self.sig2.device)
+        if ell is not None:
+            self.ell = torch.tensor(ell, dtype=self.dtype, device=self.ell.device)
+
+    def noise_terms(self, noise_std_batch):
+        """(1/sigma_n^2, log sigma_n): per observation or from log_noise2 (`hipgp.py:227-230,394-399`)."""
+        if noise_std_batch is not None:
+            return (1 / noise_std_batch ** 2), torch.log(noise_std_batch)
+        return torch.exp(-self.log_noise2), 0.5 * self.log_noise2
+
+    # ---- the hot path ----------------------------------------------------------------------
+    def toeplitz(self):
+        """A fresh ToeplitzTensor for the current kernel parameters (`hipgp.py:142-143`)."""
+        params = self.get_kernel_params()
+        return ToeplitzTensor(xgrids=self.xgrids, kernel=lambda x, y: self.kernel(x, y, params=params),
+                              batch_shape=None, jitter_val=self.jitter_val)
+
+    def compute_kn(self, Knm, maxiter_cg=10, tol=1e-8, Kmm=None):
+        """kn = R^T Kmm^{-1} Knm^T (ziggy whitening) or L^{-1} Knm^T (cholesky), (bsz, M')."""
+        if self.whitened_type == 'cholesky':
+            params = self.get_kernel_params()
+            if Kmm is None:
+                Kmm = self.kernel(self.xinduce, self.xinduce, params)
+            eye = torch.eye(Kmm.shape[0], dtype=Knm.dtype, device=Knm.device)
+            L = torch.linalg.cholesky(Kmm + self.jitter_val * eye)
+            return torch.linalg.solve_triangular(L, Knm.t(), upper=False).t()
+        if Kmm is None:
+            Kmm = self.toeplitz()
+        d0 = Kmm.inv_matmul(Knm, do_precond=True, maxiter=maxiter_cg, tol=tol)
+        return Kmm._matmul_by_RT(d0)
+
+    # ---- variational family hooks ------------------------------------------------------------
+    def standard_variational_params(self):
+        raise NotImplementedError
+
+    def compute_knSkn(self, kn, qS):
+        raise NotImplementedError
+
+    def get_kl_to_prior(self, qm, qS):
+        raise NotImplementedError
+
+    # ---- ELBO --------------------------------------------------------------------------------
+    def compute_batch_an(self, xbatch, ybatch, noise_std_batch=None, qm=None, qS=None, Knm=None,
+                         Knn_diag=None, kn=None, maxiter_cg=10, integrated_obs=False,
+                         semi_integrated_estimator=None, semi_integrated_samps=None,
+                         cache_K_matmul=None, print_debug_info=False, Kmm=None):
+        """a_n = -1/2 ln 2 pi s^2 - (mse + Knn - kn.kn + kn S kn) / 2 s^2  (`hipgp.py:370-414`)."""
+        if qm is None or qS is None:
+            qm, qS = self.standard_variational_params()
+        if Knm is None or Knn_diag is None:
+            Knm, Knn_diag = self._make_grams(xbatch, integrated_obs=integrated_obs)
+        if kn is None:
+            kn = self.compute_kn(Knm, maxiter_cg=maxiter_cg, Kmm=Kmm)
+        ivar, log_sd = self.noise_terms(noise_std_batch)
+        if noise_std_batch is not None:
+            ivar, log_sd = ivar.squeeze(), log_sd.squeeze()
+        mse = (kn.matmul(qm).squeeze() - ybatch.squeeze()) ** 2
+        variance = Knn_diag.squeeze() - torch.sum(kn * kn, dim=-1).squeeze() + self.compute_knSkn(kn, qS)
+        if print_debug_info:
+            print("mse = {:.4f}".format(torch.mean(mse)))
+            print("variance = {:.4f}".format(torch.mean(variance)))
+        return -0.5 * ivar * (mse + variance) - log_sd - 0.5 * LN_2PI
+
+    def elbo(self, xbatch, ybatch, noise_std_batch=None, maxiter_cg=10, integrated_obs=False,
+             semi_integrated_estimator="analytic", semi_integrated_samps=10, Kmm=None,
+             print_debug_info=False):
+        """mean_n a_n - KL/N  (`hipgp.py:160-192`)."""
+        Knm, Knn_diag = self._make_grams(xbatch, integrated_obs=integrated_obs)
+        kn = self.compute_kn(Knm, maxiter_cg=maxiter_cg, Kmm=Kmm)
+        qm, qS = self.standard_variational_params()
+        an = self.compute_batch_an(xbatch, ybatch, noise_std_batch, qm=qm, qS=qS, Knm=Knm,
+                                   Knn_diag=Knn_diag, kn=kn)
+        return torch.mean(an) - self.get_kl_to_prior(qm, qS) / self.N
+
+    def elbo_and_grad(self, xbatch, ybatch, noise_std_batch=None, maxiter_cg=10, integrated_obs=False,
+                      semi_integrated_estimator="analytic", semi_integrated_samps=10,
+                      print_debug_info=False, Kmm=None):
+        """ELBO estimate; sets theta1.grad / theta2.grad to minus the natural gradient
+        (`hipgp.py:194-276`)."""
+        assert self.parameterization == 'expectation-family', \
+            "need parameterization=expectation-family when performing natural gradient descent"
+        Knm, Knn_diag = self._make_grams(xbatch, integrated_obs=integrated_obs)
+        kn = self.compute_kn(Knm, maxiter_cg=maxiter_cg, Kmm=Kmm)
+        stats = self.batch_stats(kn, ybatch, Knn_diag, noise_std_batch)
+        return self.apply_stats(stats, xbatch.shape[0])
+
+    def predict(self, x, integrated_obs=False, semi_integrated_estimator="analytic",
+                semi_integrated_samps=10, maxiter_cg=50, Kmm=None):
+        """E[f(x)] and sd[f(x)] (`hipgp.py:416-446`), returned on the CPU."""
+        x = x.to(self.xgrids[0].device)
+        Knm, Knn_diag = self._make_grams(x, integrated_obs=integrated_obs)
+        kn = self.compute_kn(Knm, maxiter_cg=maxiter_cg, Kmm=Kmm)
+        qm, qS = self.standard_variational_params()
+        mu = kn.matmul(qm)
+        ktilde = (Knn_diag - torch.sum(kn * kn, dim=-1)).clamp_min(1e-5)
+        sig = torch.sqrt(ktilde + self.compute_knSkn(kn, qS))[:, None]
+        return mu.cpu().detach(), sig.cpu().detach()
+
+
+class MeanFieldToeplitzGP(ToeplitzInducingGP):
+    """Diagonal variational covariance in the expanded space (`hipgp.py:449-524`)."""
+
+    def __init__(self, kernel, xgrids, num_obs, sig2_init=1., ell_init=.05, noise2_init=1.,
+                 init_Svar=.1, learn_kernel=False, learn_noise=False, dtype=torch.float,
+                 whitened_type='ziggy', parameterization='expectation-family', jitter_val=1e-3):
+        super().__init__(kernel, xgrids, num_obs, sig2_init=sig2_init, ell_init=ell_init,
+                         noise2_init=noise2_init, learn_kernel=learn_kernel, learn_noise=learn_noise,
+                         dtype=dtype, whitened_type=whitened_type, parameterization=parameterization,
+                         jitter_val=jitter_val)
+        col = lambda: torch.zeros(self.Mprime, 1, dtype=dtype)
+        if parameterization == 'standard':
+            self.global_m = nn.Parameter(nn.init.xavier_normal_(col()), requires_grad=True)
+            self.global_S = nn.Parameter(init_Svar * torch.ones(self.Mprime, 1, dtype=dtype), requires_grad=True)
+        else:
+            self.global_theta1 = nn.Parameter(nn.init.xavier_normal_(col()), requires_grad=True)
+            self.global_theta2 = nn.Parameter((-.5 / init_Svar) * torch.ones(self.Mprime, 1, dtype=dtype),
+                                              requires_grad=True)
+
+    @property
+    def name(self):
+        return 'mean-field'
+
+    def standard_variational_params(self):
+        if self.parameterization == 'standard':
+            return self.global_m, self.global_S
+        S = -0.5 / self.global_theta2
+        return S * self.global_theta1, S
+
+    def get_kl_to_prior(self, qm=None, qS=None):
+        if qm is None or qS is None:
+            qm, qS = self.standard_variational_params()
+        return diag_kl_to_standard(qm, qS)
+
+    def get_identity_for_lam(self):
+        return 1
+
+    def get_lam(self, ivar_noise, kn, bscale=1, add_identity=True):
+        return (bscale * torch.sum(ivar_noise * kn * kn, dim=0) + (1 if add_identity else 0))[:, None]
+
+    def get_S_from_lam(self, lam):
+        return 1. / lam
+
+    def compute_knSkn(self, kn, qS):
+        return torch.sum(kn * kn * qS.t(), dim=-1).squeeze()
+
+    # ---- natural gradient as batch sums + update (sharding-friendly) ------------------------
+    def batch_stats(self, kn, ybatch, Knn_diag, noise_std_batch=None):
+        """Sums over this minibatch (or this rank's shard of it):
+           an_sum  = sum_n a_n
+           lam_sum = sum_n ivar_n kn_n^2            (M',)   `hipgp.py:241`
+           dm_sum  = -sum_n ivar_n (kn_n.m - y_n) kn_n   (M',)   `hipgp.py:234-236`"""
+        with torch.no_grad():
+            qm, qS = self.standard_variational_params()
+            ivar, log_sd = self.noise_terms(noise_std_batch)
+            y = ybatch.reshape(-1)
+            knm = kn.matmul(qm).reshape(-1)
+            kk = kn * kn
+            knkn = kk.sum(dim=-1)
+            knSkn = kk.matmul(qS).reshape(-1)
+            iv = ivar.reshape(-1) if torch.is_tensor(ivar) and ivar.dim() > 0 else ivar
+            lsd = log_sd.reshape(-1) if torch.is_tensor(log_sd) and log_sd.dim() > 0 else log_sd
+            an = -0.5 * iv * ((knm - y) ** 2 + Knn_diag.reshape(-1) - knkn + knSkn) - lsd - 0.5 * LN_2PI
+            ivcol = iv[:, None] if torch.is_tensor(iv) and iv.dim() > 0 else iv
+            lam_sum = torch.sum(ivcol * kk, dim=0)
+            bdiff = iv * (knm - y)
+            dm_sum = -(bdiff[None, :].matmul(kn)).reshape(-1)
+            an_sum = an.sum()
+        return {"an_sum": an_sum, "lam_sum": lam_sum, "dm_sum": dm_sum, "n": kn.shape[0]}
+
+    def apply_stats(self, stats, bsz):
+        """ELBO estimate and theta grads from (all-reduced) batch sums of `bsz` observations."""
+        qm, qS = self.standard_variational_params()
+        with torch.no_grad():
+            qm, qS = qm.detach(), qS.detach()
+            bscale = self.N / bsz
+            elbo = stats["an_sum"] / bsz - self.get_kl_to_prior(qm, qS) / self.N
+            dm = bscale * stats["dm_sum"][:, None] - qm
+            lam_diag = bscale * stats["lam_sum"] + 1
+            dS = -.5 * lam_diag[:, None] - self.global_theta2.data
+            deta1 = dm + dS * (-2 * qm)
+        self.global_theta1.grad = -deta1
+        self.global_theta2.grad = -dS
+        return elbo

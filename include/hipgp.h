@@ -89,6 +89,13 @@ int hgp_pcg_begin(hgp_plan* plan, const void* b, void* x, int64_t nrhs, int use_
                   int layout);
 int hgp_pcg_step(hgp_plan* plan, double tol, int* converged);
 
+/* Per-RHS r.r after the last hgp_pcg_step (device, nrhs values in the plan dtype).  With
+ * tol < 0 a step never sets the convergence flag, so a caller that shards the right-hand
+ * sides over processes can apply the reference's ALL-RHS break rule (cg.py:69-71) globally:
+ * step(tol = -1), read r.r, all-reduce "every sqrt(r.r) < tol", stop.  x is final after the
+ * step that met the test (the break precedes only the z/p update). */
+int hgp_pcg_rnorm2(hgp_plan* plan, void* out);
+
 /* The clamped spectrum D (which=HGP_SPEC_D), sqrt(D) or 1/D on the full expanded grid
  * (device, M' reals) — the real parts of ToeplitzTensor.D / D_sqrt / Di
  * (toeplitz_tensor.py:28-31). */

@@ -12,7 +12,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def _header_symbols():
     src = open(os.path.join(ROOT, "include", "hipgp.h")).read()
-    return sorted(set(re.findall(r"\b(hgp_[a-z_]+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b(hgp_[a-z0-9_]+)\s*\(", src)))
 
 
 def test_library_exports_every_header_symbol():

@@ -1,0 +1,97 @@
+"""Model-level parity on the GPU: MeanFieldToeplitzGP.elbo_and_grad / predict with kn from the
+HIP path (hgp_pcg_solve + R^T) against the reference's own outputs (G5, made by running
+/root/reference), and the RHS-sharded solve over 2 processes sharing the GPU."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from golden_cases import load, rel_err
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _model(fx, dtype=torch.float64, device=DEV):
+    import ziggy.hipgp as hg
+    import ziggy.kernels as zk
+    k = zk.Matern(nu=1.5, dtype=dtype)
+    grids = [torch.tensor(fx["grid0"], dtype=dtype), torch.tensor(fx["grid1"], dtype=dtype)]
+    mod = hg.MeanFieldToeplitzGP(k, grids, num_obs=64, sig2_init=1., ell_init=.1, noise2_init=.01,
+                                 learn_kernel=False, dtype=dtype)
+    with torch.no_grad():
+        mod.global_theta1.copy_(torch.tensor(fx["theta1"], dtype=dtype))
+        mod.global_theta2.copy_(torch.tensor(fx["theta2"], dtype=dtype))
+    return mod.cuda_params(0) if device != "cpu" else mod
+
+
+def test_compute_kn_elbo_grad_predict_G5():
+    """hipgp.py:117-146 (compute_kn), 194-276 (elbo_and_grad), 416-446 (predict), fp64."""
+    fx = load("G5", "f64")
+    mod = _model(fx)
+    x = torch.tensor(fx["xobs"], device=DEV)
+    y = torch.tensor(fx["yobs"], device=DEV)
+    Knm, _ = mod._make_grams(x)
+    kn = mod.compute_kn(Knm, maxiter_cg=20)
+    assert rel_err(kn.cpu().numpy(), fx["kn"]) < 1e-8
+    elbo = mod.elbo_and_grad(x, y, maxiter_cg=20)
+    assert abs(float(elbo) - float(fx["elbo"])) < 1e-8 * abs(float(fx["elbo"]))
+    assert rel_err(mod.global_theta1.grad.cpu().numpy(), fx["theta1_grad"]) < 1e-7
+    assert rel_err(mod.global_theta2.grad.cpu().numpy(), fx["theta2_grad"]) < 1e-7
+    mu, sig = mod.predict(x[:50], maxiter_cg=50)
+    assert rel_err(mu.numpy(), fx["pred_mu"]) < 1e-7
+    assert rel_err(sig.numpy(), fx["pred_sig"]) < 1e-7
+
+
+def test_compute_kn_fp32_G5():
+    """fp32 model (the reference default dtype, hipgp.py:23) against the reference's fp32 run:
+    no worse than 4x the reference's own fp32 error vs fp64."""
+    fx32 = load("G5", "f32")
+    fx64 = load("G5", "f64")
+    mod = _model(fx32, dtype=torch.float32)
+    Knm, _ = mod._make_grams(torch.tensor(fx32["xobs"], device=DEV))
+    kn = mod.compute_kn(Knm, maxiter_cg=20).double().cpu().numpy()
+    e_me = np.linalg.norm(kn - fx64["kn"])
+    e_ref = np.linalg.norm(fx32["kn"].astype(np.float64) - fx64["kn"])
+    assert e_me <= 4 * e_ref + 1e-6 * np.linalg.norm(fx64["kn"]), (e_me, e_ref)
+
+
+def _worker(rank, world_size, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world_size)
+    try:
+        from hipgp_amd import dist as hdist
+        torch.cuda.set_device(0)
+        fx = load("G5", "f64")
+        mod = _model(fx)
+        x = torch.tensor(fx["xobs"], device=DEV)
+        y = torch.tensor(fx["yobs"], device=DEV)
+        elbo = hdist.sharded_elbo_and_grad(mod, x, y, maxiter_cg=20, exact_break=True)
+        # the all-RHS break rule across ranks: a tolerance every RHS meets only late
+        Knm, _ = mod._make_grams(x[hdist.rhs_shard(64, world_size, rank)])
+        T = mod.toeplitz()
+        _, iters = T._plan.pcg_allranks(Knm, 200, 1e-6, precond=True)
+        torch.cuda.synchronize()
+        out[rank] = (float(elbo), mod.global_theta1.grad.cpu().numpy(), iters)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_two_ranks_one_gpu():
+    """2 processes on the GPU (gloo for the host-side reductions): identical ELBO/grads to
+    the reference, and both ranks stop PCG at the same (global) iteration."""
+    fx = load("G5", "f64")
+    mgr = mp.Manager()
+    out = mgr.dict()
+    port = 29700 + os.getpid() % 200
+    mp.spawn(_worker, args=(2, port, out), nprocs=2, join=True)
+    assert len(out) == 2
+    for r in range(2):
+        elbo, g1, _ = out[r]
+        assert abs(elbo - float(fx["elbo"])) < 1e-8 * abs(float(fx["elbo"]))
+        assert rel_err(g1, fx["theta1_grad"]) < 1e-7
+    assert out[0][2] == out[1][2] and out[0][2] < 200

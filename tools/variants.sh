@@ -2,11 +2,10 @@
 # Block-shape variants of libhipgp for tuning: build here (BUILD=1), time on the GPU box.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 declare -A V
-V[v1]="-DHGP_CMAX_STRIDED=16 -DHGP_MINW_STRIDED=4 -DHGP_ROW_THREADS=256 -DHGP_MINW_ROW=3"
-V[v2]="-DHGP_CMAX_STRIDED=8 -DHGP_MINW_STRIDED=3 -DHGP_ROW_THREADS=256 -DHGP_MINW_ROW=3"
-V[v3]="-DHGP_CMAX_STRIDED=4 -DHGP_MINW_STRIDED=3 -DHGP_ROW_THREADS=512 -DHGP_MINW_ROW=2"
-V[v4]="-DHGP_CMAX_STRIDED=8 -DHGP_MINW_STRIDED=4 -DHGP_ROW_THREADS=128 -DHGP_MINW_ROW=4"
-V[v5]="-DHGP_CMAX_STRIDED=8 -DHGP_MINW_STRIDED=2 -DHGP_ROW_THREADS=256 -DHGP_MINW_ROW=2"
+V[p8]="-DHGP_ROWT_PAIRS=8"
+V[p4]="-DHGP_ROWT_PAIRS=4"
+V[p2]="-DHGP_ROWT_PAIRS=2"
+V[p16]="-DHGP_ROWT_PAIRS=16"
 if [ -n "$BUILD" ]; then
   for k in "${!V[@]}"; do make -s -C hipgp_amd/csrc VARIANT=$k VFLAGS="${V[$k]}" -j4 & done; wait
   exit 0
