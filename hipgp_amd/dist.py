@@ -56,6 +56,7 @@ def sharded_compute_kn(model, Knm_local, maxiter_cg=20, tol=1e-8, exact_break=Fa
     if Kmm is None:
         Kmm = model.toeplitz()
     if exact_break:
+        Kmm.set_batch_shape(Knm_local.shape[:-1])   # as _solve does (toeplitz_tensor.py:61)
         d0, _ = Kmm._plan.pcg_allranks(Knm_local, maxiter_cg, tol, precond=True, group=group)
     else:
         d0 = Kmm.inv_matmul(Knm_local, do_precond=True, maxiter=maxiter_cg, tol=tol)
