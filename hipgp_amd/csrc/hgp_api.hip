@@ -341,17 +341,11 @@ int upload_twiddles(DevBuf& buf, int64_t L) {
 }
 
 // W[k][t] = w_t cos(2 pi t k / n), w_0 = w_{m-1} = 1, else 2  (length-n DFT of the even
-// extension restricted to the m unique points = DCT-I)
-int upload_dct(DevBuf& buf, int64_t m, int64_t n) {
-  std::vector<double> h((size_t)(m * m));
-  for (int64_t k = 0; k < m; ++k)
-    for (int64_t t = 0; t < m; ++t) {
-      const double w = (t == 0 || t == m - 1) ? 1.0 : 2.0;
-      const int64_t e = (t * k) % n;
-      h[(size_t)(k * m + t)] = w * std::cos(2.0 * M_PI * (double)e / (double)n);
-    }
-  HGP_TRY(buf.ensure(h.size() * sizeof(double)));
-  HIP_TRY(hipMemcpy(buf.ptr, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
+// extension restricted to the m unique points = DCT-I); built on the device (k_dct_table)
+int make_dct(DevBuf& buf, int64_t m, int64_t n, hipStream_t s) {
+  HGP_TRY(buf.ensure((size_t)(m * m) * sizeof(double)));
+  dct_table(reinterpret_cast<double*>(buf.ptr), m, n, s);
+  HIP_TRY(hipGetLastError());
   return 0;
 }
 
@@ -585,7 +579,7 @@ int hgp_plan_create(int device, int ndim, const int64_t* m, int dtype, int64_t m
     }
     if (!rc) rc = upload_twiddles<double>(P->tw64K[a], P->LK[a]);
     if (!rc) rc = upload_twiddles<double>(P->tw64R[a], P->LR[a]);
-    if (!rc) rc = upload_dct(P->Wdct[a], P->m[a], P->n[a]);
+    if (!rc) rc = make_dct(P->Wdct[a], P->m[a], P->n[a], P->stream);
   }
   if (rc) { delete P; return rc; }
   *out = P;
@@ -594,7 +588,12 @@ int hgp_plan_create(int device, int ndim, const int64_t* m, int dtype, int64_t m
 
 int hgp_plan_set_stream(hgp_plan* plan, void* hip_stream) {
   HGP_TRY(check_plan(plan));
-  plan->stream = reinterpret_cast<hipStream_t>(hip_stream);
+  hipStream_t s = reinterpret_cast<hipStream_t>(hip_stream);
+  if (s != plan->stream) {   // the plan's buffers may still be in use on the old stream
+    HGP_TRY(use_device(plan));
+    HIP_TRY(hipStreamSynchronize(plan->stream));
+  }
+  plan->stream = s;
   return 0;
 }
 

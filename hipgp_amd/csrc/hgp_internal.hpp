@@ -18,6 +18,7 @@ template <typename T>
 hipError_t launch_rowt(int H, int inv, const PassDesc& d, hipStream_t s);
 
 // setup (fp64)
+void dct_table(double* W, int64_t m, int64_t n, hipStream_t s);
 void dct_axis(const double* W, const double* in, double* out, int m, int64_t I, int64_t ncols, double scale,
               hipStream_t s);
 template <typename T> void to_f64(const void* src, double* dst, int64_t n, double add0, hipStream_t s);

@@ -82,6 +82,19 @@ void dct_axis(const double* W, const double* in, double* out, int m, int64_t I, 
   hipLaunchKernelGGL(k_dct_gemm, grid, dim3(256), 0, s, W, in, out, m, I, ncols, scale);
 }
 
+// DCT-I matrix W[k][t] = w_t cos(2 pi ((t k) mod n) / n), w = 1 at t = 0, m-1, else 2
+__global__ void k_dct_table(double* __restrict__ W, int64_t m, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m * m) return;
+  const int64_t k = i / m, t = i - k * m;
+  const double w = (t == 0 || t == m - 1) ? 1.0 : 2.0;
+  W[i] = w * cospi(2.0 * (double)((t * k) % n) / (double)n);
+}
+
+void dct_table(double* W, int64_t m, int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(k_dct_table, dim3((unsigned)((m * m + 255) / 256)), dim3(256), 0, s, W, m, n);
+}
+
 template <typename T>
 __global__ void k_to_f64(const T* __restrict__ src, double* __restrict__ dst, int64_t n, double add0) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;

@@ -46,6 +46,12 @@
 #ifndef HGP_MINW_ROW
 #define HGP_MINW_ROW 0
 #endif
+#ifndef HGP_CONTIG_THREADS
+#define HGP_CONTIG_THREADS 512   // complex contiguous lines (2-D column CONV, setup grids)
+#endif
+#ifndef HGP_MINW_CONTIG
+#define HGP_MINW_CONTIG 4
+#endif
 
 namespace hgp {
 
@@ -89,8 +95,9 @@ template <typename T, int H, int LAY> struct PassCfg {
     while (c > 1 && (c * TT > 1024 || lds_bytes_for(c) > LDS_CAP)) c >>= 1;
     return c;
   }
+  static constexpr int ROWT = (LAY == LAY_CONTIG) ? HGP_CONTIG_THREADS : HGP_ROW_THREADS;
   static constexpr int c_contig() {
-    int c = (TT >= HGP_ROW_THREADS) ? 1 : HGP_ROW_THREADS / TT;
+    int c = (TT >= ROWT) ? 1 : ROWT / TT;
     while (c > 1 && (c * TT > 1024 || lds_bytes_for(c) > LDS_CAP / 2)) c >>= 1;
     return c;
   }
@@ -106,7 +113,8 @@ template <typename T, int H, int LAY> struct PassCfg {
   static constexpr int BLOCKS_BY_LDS = LDS_CAP / LDS;
   static constexpr int MINW_LDS = (BLOCKS_BY_LDS * WAVES_PER_BLOCK) / 4;
   static constexpr int MINW_AUTO = MINW_LDS < 1 ? 1 : (MINW_LDS > 4 ? 4 : MINW_LDS);
-  static constexpr int MINW_SET = (LAY == LAY_STRIDED) ? HGP_MINW_STRIDED : HGP_MINW_ROW;
+  static constexpr int MINW_SET = (LAY == LAY_STRIDED) ? HGP_MINW_STRIDED
+                                 : (LAY == LAY_CONTIG) ? HGP_MINW_CONTIG : HGP_MINW_ROW;
   static constexpr int MINW = MINW_SET > 0 ? MINW_SET : MINW_AUTO;
 };
 
@@ -202,6 +210,15 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
     i = i0 + l;
     valid = i < d.In;               // (q, r, i0) of a launched block are always in range
     lc = valid ? l : 0;             // keep every (unconditional) load in bounds
+  } else if constexpr (LAY == LAY_CONTIG) {
+    // RHS-fastest: the C lines of a block are the same column r of C right-hand sides, so
+    // they share one spectrum line (read once per block into L1/L2, not once per RHS)
+    const int64_t line = (int64_t)blockIdx.x * C + l;
+    r = (int)(line / d.Q);
+    q = (int)(line - (int64_t)r * d.Q);
+    i = 0;
+    valid = r < d.Rn;
+    if (!valid) { q = 0; r = 0; }
   } else {
     const int64_t line = (int64_t)blockIdx.x * C + l;
     q = (int)(line / d.Rn);
@@ -289,16 +306,18 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
   // odd (x[p] - x[p+H]) W_L^p.  Peak live data is two P-arrays in every mode.
   C2<T> va[P], vb[P];
   constexpr bool CONV = MODE == PASS_CONV || MODE == PASS_CONVC;
-  // real spectrum of both halves, issued together with the data loads
-  T sre[2][P];
+  // real spectrum: the even half's values are issued together with the data loads, the odd
+  // half's right after the even product (in flight during the even IFFT + odd FFT), so at
+  // most one half's spectrum is live in registers
+  T sre[P];
+  const T* sb = nullptr;
+  int so = 0, sp = 0;
   if constexpr (MODE == PASS_CONV) {
-    const T* sb = reinterpret_cast<const T*>(d.spec) + (int64_t)i0 * d.spec_i + (int64_t)r * d.spec_r;
-    const int sp = (int)d.spec_p;
-    const int so = (LAY == LAY_STRIDED ? lc * (int)d.spec_i : 0) + t * sp;
+    sb = reinterpret_cast<const T*>(d.spec) + (int64_t)i0 * d.spec_i + (int64_t)r * d.spec_r;
+    sp = (int)d.spec_p;
+    so = (LAY == LAY_STRIDED ? lc * (int)d.spec_i : 0) + t * sp;
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int k = 0; k < P; ++k) sre[h][k] = sb[so + (h * H + TT * k) * sp];
+    for (int k = 0; k < P; ++k) sre[k] = sb[so + TT * k * sp];
   }
   if constexpr (MODE == PASS_FWD || CONV) {
     const int in_len = d.in.len;
@@ -356,7 +375,11 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
       if constexpr (MODE == PASS_CONV) {
         fft_line<T, H, P, -1, LSTRIDE, Cfg::WAVE>(v, lds, lbase, t, tab);
 #pragma unroll
-        for (int k = 0; k < P; ++k) v[k] = mk<T>(v[k].x * sre[half][k], v[k].y * sre[half][k]);
+        for (int k = 0; k < P; ++k) v[k] = mk<T>(v[k].x * sre[k], v[k].y * sre[k]);
+        if constexpr (half == 0) {
+#pragma unroll
+          for (int k = 0; k < P; ++k) sre[k] = sb[so + (H + TT * k) * sp];
+        }
       } else if constexpr (MODE == PASS_CONVC) {
         fft_line<T, H, P, -1, LSTRIDE, Cfg::WAVE>(v, lds, lbase, t, tab);
         // complex spectrum at (i, r, kperm): block-uniform base + 32-bit lane offset

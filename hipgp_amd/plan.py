@@ -17,6 +17,13 @@ def expanded_dims(dims):
     return tuple(2 * m - 2 if m > 1 else m for m in dims)
 
 
+# Idle C plans by (dims, dtype, device): the reference builds a fresh ToeplitzTensor on every
+# compute_kn call (`hipgp.py:143`); re-using an idle plan of the same grid keeps its twiddle /
+# DCT tables and HBM workspaces, so only the spectrum is recomputed (hgp_plan_set_column).
+_POOL = {}
+_POOL_MAX = 2
+
+
 class ToeplitzPlan:
     """Spectra + workspaces for the BTTB operators of one grid (`toeplitz_tensor.py:9-45`)."""
 
@@ -32,10 +39,16 @@ class ToeplitzPlan:
         self.ndims = expanded_dims(self.dims)
         self.M = int(np.prod(self.dims))
         self.Mprime = int(np.prod(self.ndims))
-        m = (ctypes.c_int64 * len(self.dims))(*self.dims)
-        h = ctypes.c_void_p()
-        check(lib().hgp_plan_create(device.index, len(self.dims), m, _lib.dtype_code(dtype), 0,
-                                    _lib.stream_ptr(device), ctypes.byref(h)))
+        self._key = (self.dims, dtype, device.index)
+        idle = _POOL.get(self._key)
+        if idle:
+            h = idle.pop()
+            check(lib().hgp_plan_set_stream(h, _lib.stream_ptr(device)))
+        else:
+            m = (ctypes.c_int64 * len(self.dims))(*self.dims)
+            h = ctypes.c_void_p()
+            check(lib().hgp_plan_create(device.index, len(self.dims), m, _lib.dtype_code(dtype), 0,
+                                        _lib.stream_ptr(device), ctypes.byref(h)))
         self._h = h
         LK = (ctypes.c_int64 * 3)()
         LR = (ctypes.c_int64 * 3)()
@@ -150,11 +163,15 @@ class ToeplitzPlan:
     def __del__(self):
         h = getattr(self, "_h", None)
         if h is not None and _lib._lib is not None:
+            self._h = None
             try:
-                lib().hgp_plan_destroy(h)
+                idle = _POOL.setdefault(self._key, [])
+                if len(idle) < _POOL_MAX:
+                    idle.append(h)          # stream-ordered re-use (see _POOL)
+                else:
+                    lib().hgp_plan_destroy(h)
             except Exception:
                 pass
-            self._h = None
 
 
 def rowdot(a, c):

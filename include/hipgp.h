@@ -44,7 +44,8 @@ enum {
 int hgp_plan_create(int device, int ndim, const int64_t* m, int dtype, int64_t max_rhs,
                     void* hip_stream, hgp_plan** out);
 
-/* Change the stream later calls are ordered on. */
+/* Change the stream later calls are ordered on (synchronises the previous stream first, so a
+ * plan can be handed between streams, e.g. from a pool of idle plans). */
 int hgp_plan_set_stream(hgp_plan* plan, void* hip_stream);
 
 /* Spectrum setup from the kernel-evaluated Toeplitz first column (device, M values):

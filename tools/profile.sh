@@ -1,14 +1,16 @@
 #!/bin/bash
 # rocprofv3 kernel-trace summary of the bench (timing pass) — run on the GPU box.
+# The stats csv is copied to profiles/<tag>_kernel_stats.csv.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=gpurun_out/prof_${1:-run}
-mkdir -p "$OUT"
+TAG=${1:-run}
+OUT=gpurun_out/prof_$TAG
+mkdir -p "$OUT" profiles
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT" -o run --output-format csv -- \
-  python3 bench.py --no-cpu-baseline --steps 10 --warmup 3 --pcg-reps 1 > "$OUT/bench.log" 2>&1
+  python3 bench.py --no-cpu-baseline --steps 20 --warmup 5 --pcg-reps 2 > "$OUT/bench.log" 2>&1
 rc=$?
 echo "[profile] rocprofv3 exit=$rc"
-find "$OUT" -name "*kernel_stats.csv" | head -3
 f=$(find "$OUT" -name "*kernel_stats.csv" | head -1)
-[ -n "$f" ] && head -30 "$f"
+[ -n "$f" ] && cp "$f" profiles/${TAG}_kernel_stats.csv && head -12 "$f" | cut -c1-200
+cp "$OUT/bench.log" profiles/${TAG}_bench_under_rocprof.log 2>/dev/null
 exit $rc
