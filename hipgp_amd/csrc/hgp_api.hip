@@ -72,13 +72,14 @@ struct hgp_plan {
   int64_t M = 1, Mp = 1, prodLK = 1, prodLR = 1;
   size_t esz = 4;
   // tables
-  DevBuf twK[3], twR[3], tw64K[3], tw64R[3], Wdct[3];
+  DevBuf twK[3], twR[3], tw64K[3], tw64R[3];
+  DevBuf bsPre[3], bsPost[3], bsFilt[3];   // Bluestein DCT-I tables per axis (fp64)
   // spectra
   DevBuf specK, specI, specR, Dm3;
   bool have_spec = false;
   DevBuf nclamp;
   // scratch
-  DevBuf ws1, ws2, set1, set2, setM1, setM2;
+  DevBuf ws1, ws2, set1, set2, setM1, setM2, setC;
   // CG state
   DevBuf r, z, p, Ap, part_op, part_u, scal, flags, bT, xT;
   int64_t cg_nrhs = 0;
@@ -89,8 +90,11 @@ struct hgp_plan {
   int64_t ws_budget = (int64_t)1 << 30;
 
   ~hgp_plan() {
-    for (int a = 0; a < 3; ++a) { twK[a].release(); twR[a].release(); tw64K[a].release(); tw64R[a].release(); Wdct[a].release(); }
-    DevBuf* bufs[] = {&specK, &specI, &specR, &Dm3, &nclamp, &ws1, &ws2, &set1, &set2, &setM1, &setM2,
+    for (int a = 0; a < 3; ++a) {
+      twK[a].release(); twR[a].release(); tw64K[a].release(); tw64R[a].release();
+      bsPre[a].release(); bsPost[a].release(); bsFilt[a].release();
+    }
+    DevBuf* bufs[] = {&specK, &specI, &specR, &Dm3, &nclamp, &ws1, &ws2, &set1, &set2, &setM1, &setM2, &setC,
                       &r, &z, &p, &Ap, &part_op, &part_u, &scal, &flags, &bT, &xT};
     for (DevBuf* b : bufs) b->release();
   }
@@ -340,11 +344,59 @@ int upload_twiddles(DevBuf& buf, int64_t L) {
   return 0;
 }
 
-// W[k][t] = w_t cos(2 pi t k / n), w_0 = w_{m-1} = 1, else 2  (length-n DFT of the even
-// extension restricted to the m unique points = DCT-I); built on the device (k_dct_table)
-int make_dct(DevBuf& buf, int64_t m, int64_t n, hipStream_t s) {
-  HGP_TRY(buf.ensure((size_t)(m * m) * sizeof(double)));
-  dct_table(reinterpret_cast<double*>(buf.ptr), m, n, s);
+// Bluestein tables of axis `ax` (hgp_kernels.hip k_chirp_*): chirps on the m-grid and the
+// chirp filter's spectrum on the operator length L_K (>= 2m - 1), scaled by 1/L_K so the
+// CONVC pass's unnormalised inverse FFT returns the linear convolution.
+int make_bluestein(hgp_plan* P, int ax) {
+  hipStream_t s = P->stream;
+  const int64_t m = P->m[ax], n = P->n[ax], L = P->LK[ax];
+  HGP_TRY(P->bsPre[ax].ensure((size_t)m * sizeof(double2)));
+  HGP_TRY(P->bsPost[ax].ensure((size_t)m * sizeof(double2)));
+  HGP_TRY(P->bsFilt[ax].ensure((size_t)L * sizeof(double2)));
+  chirp_tables(reinterpret_cast<double2*>(P->bsPre[ax].ptr), reinterpret_cast<double2*>(P->bsPost[ax].ptr), m, n, s);
+  DevBuf h;
+  HGP_TRY(h.ensure((size_t)L * sizeof(double2)));
+  chirp_filter(reinterpret_cast<double2*>(h.ptr), m, n, L, 1.0 / (double)L, s);
+  PassDesc D = base_desc();
+  D.in = View{h.ptr, L, L, 1, (int)L};
+  D.out = View{P->bsFilt[ax].ptr, L, L, 1, (int)L};
+  D.tw = P->tw64K[ax].ptr; D.Q = 1; D.Rn = 1; D.In = 1;
+  int rc = launch<double>((int)(L / 2), PASS_FWD, LAY_CONTIG, D, 1, s);
+  if (rc == 0 && hipStreamSynchronize(s) != hipSuccess) rc = fail(HGP_E_HIP, "bluestein filter FFT");
+  h.release();
+  return rc;
+}
+
+// y = scale * DCT-I_n(x) along axis ax for `nb` stacked m-grids (in, out real fp64, [nb][M]):
+// y[k] = scale * (x_0 + (-1)^k x_{m-1} + 2 sum_{0<t<m-1} x_t cos(2 pi t k / n)).
+// Chirp pre-multiply -> CONVC pass along the axis (contiguous last axis, strided otherwise)
+// -> chirp post-multiply and real part.  O(M log m) instead of a dense m x m product.
+int dct_axis(hgp_plan* P, int ax, const double* in, double* out, int nb, double scale) {
+  hipStream_t s = P->stream;
+  const int64_t m = P->m[ax], L = P->LK[ax], total = nb * P->M;
+  int64_t I = 1;
+  for (int c = ax + 1; c < P->d; ++c) I *= P->m[c];
+  const int64_t O = total / (m * I);
+  HGP_TRY(P->setC.ensure((size_t)(3 * P->M) * sizeof(double2)));
+  double2* c = reinterpret_cast<double2*>(P->setC.ptr);
+  const double2* pre = reinterpret_cast<const double2*>(P->bsPre[ax].ptr);
+  const double2* post = reinterpret_cast<const double2*>(P->bsPost[ax].ptr);
+  chirp_pre(in, pre, c, total, m, I, s);
+  PassDesc D = base_desc();
+  D.spec = P->bsFilt[ax].ptr; D.spec_kind = SPEC_CPLX; D.spec_i = 0; D.spec_r = 0; D.spec_p = 1;
+  D.tw = P->tw64K[ax].ptr; D.Q = 1;
+  if (I == 1) {
+    D.in = View{c, 0, m, 1, (int)m};
+    D.out = View{c, 0, m, 1, (int)m};
+    D.Rn = (int)O; D.In = 1;
+    HGP_TRY(launch<double>((int)(L / 2), PASS_CONVC, LAY_CONTIG, D, O, s));
+  } else {
+    D.in = View{c, 0, m * I, I, (int)m};
+    D.out = View{c, 0, m * I, I, (int)m};
+    D.Rn = (int)O; D.In = (int)I;
+    HGP_TRY(launch<double>((int)(L / 2), PASS_CONVC, LAY_STRIDED, D, 0, s));
+  }
+  chirp_post(c, post, out, total, m, I, scale, s);
   HIP_TRY(hipGetLastError());
   return 0;
 }
@@ -363,9 +415,7 @@ int set_column_t(hgp_plan* P, const void* column, double jitter, double clamp_mi
   to_f64<T>(column, a, M, jitter, s);
   // D_raw = DCT-I over every axis (length-n FFT of the circulant embedding, real part)
   for (int ax = 0; ax < d; ++ax) {
-    int64_t I = 1;
-    for (int c = ax + 1; c < d; ++c) I *= P->m[c];
-    dct_axis(reinterpret_cast<double*>(P->Wdct[ax].ptr), a, b, (int)P->m[ax], I, M / P->m[ax], 1.0, s);
+    HGP_TRY(dct_axis(P, ax, a, b, 1, 1.0));
     std::swap(a, b);
   }
   HIP_TRY(hipMemsetAsync(P->nclamp.ptr, 0, sizeof(unsigned long long), s));
@@ -375,10 +425,7 @@ int set_column_t(hgp_plan* P, const void* column, double jitter, double clamp_mi
   double* src = D3;
   double* dst = a;
   for (int ax = 0; ax < d; ++ax) {
-    int64_t I = 1;
-    for (int c = ax + 1; c < d; ++c) I *= P->m[c];
-    dct_axis(reinterpret_cast<double*>(P->Wdct[ax].ptr), src, dst, (int)P->m[ax], I, 3 * M / P->m[ax],
-             1.0 / (double)P->n[ax], s);
+    HGP_TRY(dct_axis(P, ax, src, dst, 3, 1.0 / (double)P->n[ax]));
     src = dst;
     dst = (dst == a) ? b : a;
   }
@@ -579,7 +626,7 @@ int hgp_plan_create(int device, int ndim, const int64_t* m, int dtype, int64_t m
     }
     if (!rc) rc = upload_twiddles<double>(P->tw64K[a], P->LK[a]);
     if (!rc) rc = upload_twiddles<double>(P->tw64R[a], P->LR[a]);
-    if (!rc) rc = make_dct(P->Wdct[a], P->m[a], P->n[a], P->stream);
+    if (!rc) rc = make_bluestein(P, a);
   }
   if (rc) { delete P; return rc; }
   *out = P;

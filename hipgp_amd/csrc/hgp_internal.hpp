@@ -18,9 +18,12 @@ template <typename T>
 hipError_t launch_rowt(int H, int inv, const PassDesc& d, hipStream_t s);
 
 // setup (fp64)
-void dct_table(double* W, int64_t m, int64_t n, hipStream_t s);
-void dct_axis(const double* W, const double* in, double* out, int m, int64_t I, int64_t ncols, double scale,
-              hipStream_t s);
+// Bluestein partial DFT pieces of the DCT-I (hgp_kernels.hip)
+void chirp_tables(double2* pre, double2* post, int64_t m, int64_t n, hipStream_t s);
+void chirp_filter(double2* h, int64_t m, int64_t n, int64_t L, double scale, hipStream_t s);
+void chirp_pre(const double* x, const double2* pre, double2* c, int64_t total, int64_t m, int64_t I, hipStream_t s);
+void chirp_post(const double2* c, const double2* post, double* y, int64_t total, int64_t m, int64_t I, double scale,
+                hipStream_t s);
 template <typename T> void to_f64(const void* src, double* dst, int64_t n, double add0, hipStream_t s);
 void clamp_spectrum(const double* Draw, double* out3, int64_t M, double clamp_min, unsigned long long* nclamp,
                     hipStream_t s);

@@ -7,92 +7,72 @@ namespace hgp {
 // spectrum setup (fp64)
 // ------------------------------------------------------------------------------------------
 
-// out(k, j) = scale * sum_t W[k*m + t] * in(t, j);   (t,j) -> o*(m*I) + t*I + i, j = o*I + i.
-// LDS-tiled DGEMM: 64x64 output tile, 16-deep k-steps, 256 threads, 4x4 outputs each.
-__global__ __launch_bounds__(256) void k_dct_gemm(const double* __restrict__ W, const double* __restrict__ in,
-                                                  double* __restrict__ out, int m, int64_t I, int64_t ncols,
-                                                  double scale) {
-  __shared__ double As[16][65];
-  __shared__ double Bs[16][65];
-  const int tid = threadIdx.x;
-  const int tx = tid & 15, ty = tid >> 4;
-  const int64_t j0 = (int64_t)blockIdx.x * 64;
-  const int k0 = blockIdx.y * 64;
-  double acc[4][4];
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = 0.0;
-  for (int t0 = 0; t0 < m; t0 += 16) {
-    // A tile: As[tt][kk] = W[(k0+kk)*m + t0+tt]
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int e = tid + 256 * c;       // 0..1023
-      const int tt = e & 15, kk = e >> 4;
-      const int k = k0 + kk, tcol = t0 + tt;
-      As[tt][kk] = (k < m && tcol < m) ? W[(int64_t)k * m + tcol] : 0.0;
-    }
-    // B tile: Bs[tt][jj] = in(t0+tt, j0+jj)
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int e = tid + 256 * c;
-      int tt, jj;
-      if (I == 1) { tt = e & 15; jj = e >> 4; } else { jj = e & 63; tt = e >> 6; }
-      const int64_t j = j0 + jj;
-      const int tcol = t0 + tt;
-      double val = 0.0;
-      if (j < ncols && tcol < m) {
-        const int64_t o = j / I, i = j - o * I;
-        val = in[o * (int64_t)m * I + (int64_t)tcol * I + i];
-      }
-      Bs[tt][jj] = val;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int tt = 0; tt < 16; ++tt) {
-      double av[4], bv[4];
-#pragma unroll
-      for (int a = 0; a < 4; ++a) av[a] = As[tt][ty + 16 * a];
-#pragma unroll
-      for (int b = 0; b < 4; ++b) bv[b] = Bs[tt][tx + 16 * b];
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) acc[a][b] = fma(av[a], bv[b], acc[a][b]);
-    }
-    __syncthreads();
-  }
-#pragma unroll
-  for (int a = 0; a < 4; ++a) {
-    const int k = k0 + ty + 16 * a;
-    if (k >= m) continue;
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const int64_t j = j0 + tx + 16 * b;
-      if (j >= ncols) continue;
-      const int64_t o = j / I, i = j - o * I;
-      out[o * (int64_t)m * I + (int64_t)k * I + i] = acc[a][b] * scale;
-    }
-  }
-}
-
-void dct_axis(const double* W, const double* in, double* out, int m, int64_t I, int64_t ncols, double scale,
-              hipStream_t s) {
-  dim3 grid((unsigned)((ncols + 63) / 64), (unsigned)((m + 63) / 64));
-  hipLaunchKernelGGL(k_dct_gemm, grid, dim3(256), 0, s, W, in, out, m, I, ncols, scale);
-}
-
-// DCT-I matrix W[k][t] = w_t cos(2 pi ((t k) mod n) / n), w = 1 at t = 0, m-1, else 2
-__global__ void k_dct_table(double* __restrict__ W, int64_t m, int64_t n) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= m * m) return;
-  const int64_t k = i / m, t = i - k * m;
+// Partial DFT of the length-n even extension by Bluestein's chirp-z identity
+//   X[k] = sum_{t<m} a_t W^{tk} = W^{k^2/2} sum_t (a_t W^{t^2/2}) W^{-(k-t)^2/2},  W = e^{-2 pi i/n},
+// so the DCT-I D[k] = Re sum_t w_t c_t W^{tk} (w = 1 at t = 0, m-1, else 2) is a chirp
+// pre-multiply, a linear convolution with the chirp filter (taps k-t in (-m, m): any FFT length
+// L >= 2m-1, the operator length L_K, hgp_pass CONVC) and a chirp post-multiply.  fp64.
+// pre[t] = w_t e^{-i pi t^2/n}, post[k] = e^{-i pi k^2/n}; angles reduced exactly (t^2 mod 2n).
+__global__ void k_chirp_tables(double2* __restrict__ pre, double2* __restrict__ post, int64_t m, int64_t n) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= m) return;
+  const double ang = (double)((t * t) % (2 * n)) / (double)n;    // in units of pi
+  double sv, cv;
+  sincospi(ang, &sv, &cv);
   const double w = (t == 0 || t == m - 1) ? 1.0 : 2.0;
-  W[i] = w * cospi(2.0 * (double)((t * k) % n) / (double)n);
+  pre[t] = make_double2(w * cv, -w * sv);
+  post[t] = make_double2(cv, -sv);
 }
 
-void dct_table(double* W, int64_t m, int64_t n, hipStream_t s) {
-  hipLaunchKernelGGL(k_dct_table, dim3((unsigned)((m * m + 255) / 256)), dim3(256), 0, s, W, m, n);
+// filter h[u] = scale * e^{+i pi u^2/n} on the L-grid: u in [0, m) and L - u for u in [1, m)
+__global__ void k_chirp_filter(double2* __restrict__ h, int64_t m, int64_t n, int64_t L, double scale) {
+  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= L) return;
+  int64_t v = -1;
+  if (u < m) v = u;
+  else if (u > L - m) v = L - u;
+  double2 r = make_double2(0.0, 0.0);
+  if (v >= 0) {
+    double sv, cv;
+    sincospi((double)((v * v) % (2 * n)) / (double)n, &sv, &cv);
+    r = make_double2(scale * cv, scale * sv);
+  }
+  h[u] = r;
+}
+
+// c[j] = x[j] * pre[t(j)], t = (j / I) mod m  (real in, complex out)
+__global__ void k_chirp_pre(const double* __restrict__ x, const double2* __restrict__ pre, double2* __restrict__ c,
+                            int64_t total, int64_t m, int64_t I) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= total) return;
+  const double2 w = pre[(j / I) % m];
+  const double v = x[j];
+  c[j] = make_double2(v * w.x, v * w.y);
+}
+
+// y[j] = scale * Re(c[j] * post[k(j)])
+__global__ void k_chirp_post(const double2* __restrict__ c, const double2* __restrict__ post, double* __restrict__ y,
+                             int64_t total, int64_t m, int64_t I, double scale) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= total) return;
+  const double2 w = post[(j / I) % m];
+  const double2 v = c[j];
+  y[j] = scale * (v.x * w.x - v.y * w.y);
+}
+
+void chirp_tables(double2* pre, double2* post, int64_t m, int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(k_chirp_tables, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, pre, post, m, n);
+}
+void chirp_filter(double2* h, int64_t m, int64_t n, int64_t L, double scale, hipStream_t s) {
+  hipLaunchKernelGGL(k_chirp_filter, dim3((unsigned)((L + 255) / 256)), dim3(256), 0, s, h, m, n, L, scale);
+}
+void chirp_pre(const double* x, const double2* pre, double2* c, int64_t total, int64_t m, int64_t I, hipStream_t s) {
+  hipLaunchKernelGGL(k_chirp_pre, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, x, pre, c, total, m, I);
+}
+void chirp_post(const double2* c, const double2* post, double* y, int64_t total, int64_t m, int64_t I, double scale,
+                hipStream_t s) {
+  hipLaunchKernelGGL(k_chirp_post, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, c, post, y, total, m, I,
+                     scale);
 }
 
 template <typename T>
