@@ -703,7 +703,19 @@ int hgp_pcg_step(hgp_plan* plan, double tol, int* converged) {
 int hgp_pcg_solve(hgp_plan* plan, const void* b, void* x, int64_t nrhs, int maxiter, double tol, int use_precond,
                   int layout, int* iters_done) {
   HGP_TRY(hgp_pcg_begin(plan, b, x, nrhs, use_precond, layout));
-  for (int it = 0; it < maxiter; ++it) HGP_TRY(DISPATCH(plan, pcg_step_t, plan, tol));
+  // The break test runs on the device (every kernel after it is a no-op), so short solves
+  // never synchronise.  Long ones (maxiter > 32, e.g. gram_solve's 2000) peek at the flag
+  // every 16 iterations so that an early break also stops the host from queueing no-ops.
+  const int chk = maxiter > 32 ? 16 : 0;
+  for (int it = 0; it < maxiter; ++it) {
+    HGP_TRY(DISPATCH(plan, pcg_step_t, plan, tol));
+    if (chk && (it + 1) % chk == 0 && it + 1 < maxiter) {
+      int h = 0;
+      HIP_TRY(hipMemcpyAsync(&h, plan->flags.ptr, sizeof(int), hipMemcpyDeviceToHost, plan->stream));
+      HIP_TRY(hipStreamSynchronize(plan->stream));
+      if (h) break;
+    }
+  }
   HGP_TRY(DISPATCH(plan, pcg_finish_x, plan));
   if (iters_done) {
     int h[2] = {0, 0};

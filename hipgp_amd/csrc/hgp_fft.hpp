@@ -134,11 +134,36 @@ __device__ __forceinline__ void xsync() {
   }
 }
 
-// W_L^q (forward sign), q in [0, L = 2H), from the LDS half table tab[q] = W_L^q, q < H:
-// W_L^{q+H} = -W_L^q.  Twiddles never come from global memory inside the FFT.
+// Twiddles W_L^q (forward sign), q in [0, L = 2H), live in LDS, staged once per block:
+//  * half table (H * sizeof(complex) <= 32 KB): tab[q] = W_L^q for q < H, W_L^{q+H} = -W_L^q;
+//  * two-level table beyond that (fp64 at H >= 4096, fp32 at H >= 8192, where a half table
+//    would not fit next to the exchange image): tab = [A | B], A[j] = W_L^j (j < S),
+//    B[i] = W_L^{iS} (i < H/S), W_L^q = A[q mod S] B[q div S] (one extra product, ~1 ulp).
+template <typename T, int H> struct TwTab {
+  static constexpr bool TWO = H * (int)sizeof(C2<T>) > 32 * 1024;
+  static constexpr int LG = [] { int l = 0; while ((1 << l) < H) ++l; return l; }();
+  static constexpr int S = TWO ? (1 << ((LG + 1) / 2)) : H;
+  static constexpr int ENTRIES = TWO ? S + H / S : H;
+  static constexpr int BYTES = ENTRIES * (int)sizeof(C2<T>);
+};
+
+// copy the table layout above from the global W_L^q array (all threads of the block)
+template <typename T, int H>
+__device__ __forceinline__ void stage_tw(C2<T>* tab, const C2<T>* __restrict__ twg, int tid, int nthreads) {
+  using TW = TwTab<T, H>;
+  for (int q = tid; q < TW::ENTRIES; q += nthreads) {
+    if constexpr (TW::TWO) tab[q] = q < TW::S ? twg[q] : twg[(q - TW::S) * TW::S];
+    else tab[q] = twg[q];
+  }
+}
+
 template <typename T, int H>
 __device__ __forceinline__ C2<T> tw_at(const C2<T>* __restrict__ tab, int q) {
-  C2<T> w = tab[q & (H - 1)];
+  using TW = TwTab<T, H>;
+  C2<T> w;
+  const int qq = q & (H - 1);
+  if constexpr (TW::TWO) w = cmul<T>(tab[qq & (TW::S - 1)], tab[TW::S + (qq >> (TW::LG + 1) / 2)]);
+  else w = tab[qq];
   if (q & H) { w.x = -w.x; w.y = -w.y; }
   return w;
 }

@@ -88,7 +88,7 @@ template <typename T, int H, int LAY> struct PassCfg {
   static constexpr int TT = H / P;
   // LDS: exchange image of C lines (H complex each, 1 pad slot per 16) + twiddle half table
   static constexpr int ex_elems(int c) { return c * H + ((c * H) >> 4); }
-  static constexpr int TW_BYTES = H * (int)sizeof(C2<T>);
+  static constexpr int TW_BYTES = TwTab<T, H>::BYTES;
   static constexpr int lds_bytes_for(int c) { return ex_elems(c) * (int)sizeof(C2<T>) + TW_BYTES; }
   static constexpr int c_strided() {
     int c = TT >= 16 ? HGP_CMAX_STRIDED : 64;
@@ -182,7 +182,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
   C2<T>* tab = lds + Cfg::EX_ELEMS;
   {
     const C2<T>* __restrict__ twg = reinterpret_cast<const C2<T>*>(d.tw);
-    for (int q = threadIdx.x; q < H; q += Cfg::THREADS) tab[q] = twg[q];
+    stage_tw<T, H>(tab, twg, threadIdx.x, Cfg::THREADS);
   }
 
   const int tid = threadIdx.x;
@@ -333,7 +333,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
         if (fold) c = load_hi(p);
       }
       va[k] = cadd<T>(a, c);
-      vb[k] = cmul<T>(csub<T>(a, c), tab[p]);
+      vb[k] = cmul<T>(csub<T>(a, c), tw_at<T, H>(tab, p));
     }
   }
 
@@ -419,7 +419,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
 #pragma unroll
     for (int k = 0; k < P; ++k) {
       const int p = t + TT * k;
-      const C2<T> wo = cmulc<T>(vb[k], tab[p]);
+      const C2<T> wo = cmulc<T>(vb[k], tw_at<T, H>(tab, p));
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
         const C2<T> y = hh == 0 ? cadd<T>(va[k], wo) : csub<T>(va[k], wo);
@@ -469,7 +469,7 @@ template <typename T, int H> struct ConvCfg {
   static constexpr int C0 = HGP_CONV_LINES;
 #endif
   static constexpr int ex_elems(int c) { return 2 * c * H + (2 * c * H) / 16; }
-  static constexpr int lds_bytes_for(int c) { return ex_elems(c) * (int)sizeof(C2<T>) + H * (int)sizeof(C2<T>); }
+  static constexpr int lds_bytes_for(int c) { return ex_elems(c) * (int)sizeof(C2<T>) + TwTab<T, H>::BYTES; }
   static constexpr int c_lines() {
     int c = C0 * 64 / TT;            // C0 lines per block at one wave per half-line
     if (c < 1) c = 1;
@@ -497,7 +497,7 @@ __global__ __launch_bounds__((ConvCfg<T, H>::THREADS), (ConvCfg<T, H>::MINW)) vo
   C2<T>* tab = lds + Cfg::ex_elems(C);
   {
     const C2<T>* __restrict__ twg = reinterpret_cast<const C2<T>*>(d.tw);
-    for (int q = threadIdx.x; q < H; q += Cfg::THREADS) tab[q] = twg[q];
+    stage_tw<T, H>(tab, twg, threadIdx.x, Cfg::THREADS);
   }
   const int g = threadIdx.x / TT;          // group: line l = g/2, half = g%2
   const int t = threadIdx.x - g * TT;
@@ -537,7 +537,7 @@ __global__ __launch_bounds__((ConvCfg<T, H>::THREADS), (ConvCfg<T, H>::MINW)) vo
   __syncthreads();   // twiddle table staged
   if (half) {
 #pragma unroll
-    for (int k = 0; k < P; ++k) v[k] = cmul<T>(v[k], tab[t + TT * k]);
+    for (int k = 0; k < P; ++k) v[k] = cmul<T>(v[k], tw_at<T, H>(tab, t + TT * k));
   }
   fft_line<T, H, P, -1, 1, Cfg::WAVE>(v, lds, gbase, t, tab);
   if constexpr (!CPLX_SPEC) {
@@ -564,7 +564,7 @@ __global__ __launch_bounds__((ConvCfg<T, H>::THREADS), (ConvCfg<T, H>::MINW)) vo
     for (int k = 0; k < P; ++k) {
       const int p = tt + TT * k;
       const C2<T> ye = lds[lds_phys(ebase + p)];
-      const C2<T> wo = cmulc<T>(v[k], tab[p]);
+      const C2<T> wo = cmulc<T>(v[k], tw_at<T, H>(tab, p));
       if (p < out_len) out_c[p] = cadd<T>(ye, wo);
       if (p + H < out_len) out_c[p + H] = csub<T>(ye, wo);
     }

@@ -30,7 +30,7 @@ template <typename T, int H> struct RowTCfg {
   static constexpr int TS(int c) { return 2 * c + 1; }           // tile row pitch (pad: banks)
   static constexpr int tile_elems(int c) { return (H / 2 + 1) * TS(c); }
   static constexpr int area(int c) { return ex_elems(c) > tile_elems(c) ? ex_elems(c) : tile_elems(c); }
-  static constexpr int lds_bytes_for(int c) { return (area(c) + H) * (int)sizeof(C2<T>); }
+  static constexpr int lds_bytes_for(int c) { return area(c) * (int)sizeof(C2<T>) + TwTab<T, H>::BYTES; }
   static constexpr int c_pairs() {
     int c = HGP_ROWT_PAIRS * 64 / TT;              // 512 threads at the default
     if (c < 1) c = 1;
@@ -63,7 +63,7 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
   C2<T>* tab = lds + Cfg::AREA;
   {
     const C2<T>* __restrict__ twg = reinterpret_cast<const C2<T>*>(d.tw);
-    for (int q = threadIdx.x; q < H; q += Cfg::THREADS) tab[q] = twg[q];
+    stage_tw<T, H>(tab, twg, threadIdx.x, Cfg::THREADS);
   }
   const int nrb = (d.Rn + C - 1) / C;
   const int q = blockIdx.x / nrb;
@@ -92,7 +92,7 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
   }
   __syncthreads();   // twiddle table staged
 #pragma unroll
-  for (int k = 0; k < P; ++k) vb[k] = cmul<T>(va[k], tab[t + TT * k]);
+  for (int k = 0; k < P; ++k) vb[k] = cmul<T>(va[k], tw_at<T, H>(tab, t + TT * k));
 
   C2<T>* W = reinterpret_cast<C2<T>*>(d.out.ptr) + (int64_t)q * d.out.q_stride;
   const int64_t S0 = d.out.r_stride;
@@ -161,7 +161,7 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
   C2<T>* tab = lds + Cfg::AREA;
   {
     const C2<T>* __restrict__ twg = reinterpret_cast<const C2<T>*>(d.tw);
-    for (int q = threadIdx.x; q < H; q += Cfg::THREADS) tab[q] = twg[q];
+    stage_tw<T, H>(tab, twg, threadIdx.x, Cfg::THREADS);
   }
   const int nrb = (d.Rn + C - 1) / C;
   const int q = blockIdx.x / nrb;
@@ -242,7 +242,7 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
 #pragma unroll
   for (int k = 0; k < P; ++k) {
     const int p = tt + TT * k;
-    const C2<T> wo = cmulc<T>(vb[k], tab[p]);
+    const C2<T> wo = cmulc<T>(vb[k], tw_at<T, H>(tab, p));
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
       const C2<T> y = hh == 0 ? cadd<T>(va[k], wo) : csub<T>(va[k], wo);

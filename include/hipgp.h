@@ -69,7 +69,8 @@ int hgp_toeplitz_apply(hgp_plan* plan, int op, const void* x, void* y, int64_t n
  * (b,x:(nrhs,M)) and conj_grad (cg.py:5-41) for layout COLS (b,x:(M,nrhs)): A = K,
  * preconditioner C^-1 if use_precond, x0 = 0, per-RHS alpha/beta, stop when ALL
  * sqrt(r.r) < tol after the x/r update.  The early-exit test runs on the device (a flag read
- * by every later kernel), so the host is not synchronised per iteration.
+ * by every later kernel), so the host is not synchronised per iteration (solves with
+ * maxiter > 32 read the flag every 16 iterations to stop queueing no-op iterations).
  * iters_done (host, may be NULL): number of iterations executed (synchronises).
  * Replaces ToeplitzTensor._solve (toeplitz_tensor.py:54-68) / InvMatmul.forward. */
 int hgp_pcg_solve(hgp_plan* plan, const void* b, void* x, int64_t nrhs, int maxiter,

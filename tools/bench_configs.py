@@ -1,0 +1,114 @@
+"""Coverage benchmark over the five BASELINE.json configs (GPU box; not the driver's bench line).
+
+For each config: batched K matvec throughput and compute_kn wall-clock (set-up + PCG + R^T,
+`hipgp.py:117-146`) on synthetic data of the config's shape.  The reference CPU timings quoted
+next to them are BASELINE.md §2 (reference ziggy itself, survey container, 8 threads); the
+same-box CPU baseline of the headline config is bench.py's cpu_baseline.
+
+    python tools/bench_configs.py [--only C2,C5] > gpurun_out/configs.json
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+# name: (dims, kernel, params, jitter, B, maxiter, tol, reference CPU)
+CONFIGS = {
+    "C1": ((256,), ("matern", 2.5), (1.0, 0.1), 0.0, 1000, 2000, 1e-10,
+           {"gram_solve_s": 0.065, "note": "1000 RHS, PCG to tol 1e-10 + R^T"}),
+    "C2": ((1024, 1024), ("sqexp", None), (1.0, 0.01), 1e-3, 32, 20, 1e-8,
+           {"kmatvec_rhs_per_s": 16.0, "compute_kn_s": 83.8, "note": "B=32"}),
+    "C3": ((2048, 2048), ("matern", 1.5), (1.0, 0.1), 1e-3, 200, 20, 1e-8,
+           {"kmatvec_rhs_per_s": 3.64, "compute_kn_s_per_rhs": 12.4, "note": "extrapolated per RHS"}),
+    "C4": ((4096, 4096), ("matern", 1.5), (0.1, 0.1), 1e-3, 25, 20, 1e-8,
+           {"kmatvec_rhs_per_s": 1.06, "compute_kn_s_per_rhs": 38.7, "note": "B=25 = one GPU's share of 200 over 8"}),
+    "C5": ((256, 256, 128), ("matern", 2.5), (0.1, 0.1), 1e-3, 25, 20, 1e-8,
+           {"kmatvec_rhs_per_s": 1.07, "compute_kn_s_per_rhs": 41.8, "note": "B=25 = one GPU's share of 200 over 8"}),
+}
+BOX = {1: [(0.0, 4.0)], 2: [(-1.0, 1.0)] * 2, 3: [(-0.25, 0.25), (-0.25, 0.25), (-0.05, 0.05)]}
+
+
+def kernel(kind, nu, dtype):
+    import ziggy.kernels as zk
+    return zk.SqExp(dtype=dtype) if kind == "sqexp" else zk.Matern(nu=nu, dtype=dtype)
+
+
+def timed(fn, reps=3):
+    fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts))
+
+
+def run(name, dev):
+    from hipgp_amd import _lib
+    from ziggy.misc.toeplitz_tensor import ToeplitzTensor
+    from ziggy.misc import toeplitz_expanded as te
+    dims, (kind, nu), params, jitter, B, maxiter, tol, ref = CONFIGS[name]
+    d = len(dims)
+    k = kernel(kind, nu, torch.float32)
+    kf = lambda x, y: k.forward(x, y, params=params)
+    grids = [torch.linspace(lo, hi, m, device=dev) for (lo, hi), m in zip(BOX[d], dims)]
+    g = torch.Generator(device="cpu").manual_seed(42)
+    lo = torch.tensor([b[0] for b in BOX[d]])
+    hi = torch.tensor([b[1] for b in BOX[d]])
+    xobs = (lo + (hi - lo) * torch.rand(B, d, generator=g)).to(dev)
+    mesh = torch.meshgrid(*grids, indexing="ij")
+    xs = torch.stack([x.reshape(-1) for x in mesh], dim=-1)
+    Knm = torch.cat([kf(xobs[i:i + 64], xs) for i in range(0, B, 64)], dim=0).contiguous()
+    out = {"config": name, "dims": dims, "M": int(np.prod(dims)), "B": B, "maxiter": maxiter, "tol": tol}
+    if d == 1:
+        t = timed(lambda: te.gram_solve(grids, kf, Knm, maxiter=maxiter, do_precond=True, tol=tol, mult_RT=True))
+        out.update({"gram_solve_s": t, "reference_cpu": ref, "speedup_vs_reference_cpu": ref["gram_solve_s"] / t})
+        return out
+    T = ToeplitzTensor(grids, kf, batch_shape=(B,), jitter_val=jitter)
+    y = torch.empty_like(Knm)
+    t_op = timed(lambda: T._plan.apply(_lib.OP_K, Knm, out=y), reps=5)
+    out["kmatvec_batched_ms"] = t_op * 1e3
+    out["kmatvec_rhs_per_s"] = B / t_op
+
+    def compute_kn():
+        Tk = ToeplitzTensor(grids, kf, batch_shape=None, jitter_val=jitter)
+        return Tk._matmul_by_RT(Tk.inv_matmul(Knm, do_precond=True, maxiter=maxiter, tol=tol))
+
+    t_kn = timed(compute_kn, reps=2)
+    out["compute_kn_s"] = t_kn
+    out["compute_kn_s_per_rhs"] = t_kn / B
+    out["reference_cpu"] = ref
+    out["speedup_kmatvec_vs_reference_cpu"] = out["kmatvec_rhs_per_s"] / ref["kmatvec_rhs_per_s"]
+    if "compute_kn_s_per_rhs" in ref:
+        out["speedup_compute_kn_vs_reference_cpu"] = ref["compute_kn_s_per_rhs"] / out["compute_kn_s_per_rhs"]
+    else:
+        out["speedup_compute_kn_vs_reference_cpu"] = ref["compute_kn_s"] / t_kn
+    out["peak_mem_gb"] = torch.cuda.max_memory_allocated(dev) / 1e9
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="C1,C2,C3,C4,C5")
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    res = []
+    for name in a.only.split(","):
+        r = run(name, dev)
+        res.append(r)
+        print(json.dumps(r), flush=True)
+        torch.cuda.empty_cache()
+    return res
+
+
+if __name__ == "__main__":
+    main()
