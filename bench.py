@@ -41,6 +41,9 @@ def parse():
     ap.add_argument("--pcg-reps", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="rehearsal on a 1-GPU box: every rank uses cuda:0 (with --backend gloo)")
     ap.add_argument("--kop-only", action="store_true",
                     help="only the timed K matvec steps (for rocprofv3 --pmc passes)")
     return ap.parse_args()
@@ -125,11 +128,15 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
+    dev_index = 0 if (args.same_device or not dist) else local
     if dist:
         import torch.distributed as tdist
-        torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    device = torch.device("cuda", local if dist else 0)
+        torch.cuda.set_device(dev_index)
+        if args.backend == "nccl":
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        else:
+            tdist.init_process_group(args.backend)
+    device = torch.device("cuda", dev_index)
     torch.cuda.set_device(device)
 
     from hipgp_amd import _lib
@@ -161,7 +168,7 @@ def main():
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     if dist:
-        tt = torch.tensor([dt], device=device, dtype=torch.float64)
+        tt = torch.tensor([dt], device=device if args.backend == "nccl" else "cpu", dtype=torch.float64)
         tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
         dt = float(tt.item())
     ms_per_step = dt / args.steps * 1e3
@@ -220,7 +227,7 @@ def main():
     solve_s = time.perf_counter() - t1
     pcg_ms = float(np.median(pcg_times) * 1e3)
     if dist:
-        tt = torch.tensor([pcg_ms], device=device, dtype=torch.float64)
+        tt = torch.tensor([pcg_ms], device=device if args.backend == "nccl" else "cpu", dtype=torch.float64)
         tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
         pcg_ms = float(tt.item())
 

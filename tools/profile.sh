@@ -1,16 +1,16 @@
 #!/bin/bash
 # rocprofv3 kernel-trace summary of the bench (timing pass) — run on the GPU box.
-# The stats csv is copied to profiles/<tag>_kernel_stats.csv.
+# Output under gpurun_out/prof_<tag>/ (copy the stats csv into profiles/ afterwards).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 TAG=${1:-run}
 OUT=gpurun_out/prof_$TAG
-mkdir -p "$OUT" profiles
+mkdir -p "$OUT"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT" -o run --output-format csv -- \
   python3 bench.py --no-cpu-baseline --steps 20 --warmup 5 --pcg-reps 2 > "$OUT/bench.log" 2>&1
 rc=$?
 echo "[profile] rocprofv3 exit=$rc"
 f=$(find "$OUT" -name "*kernel_stats.csv" | head -1)
-[ -n "$f" ] && cp "$f" profiles/${TAG}_kernel_stats.csv && head -12 "$f" | cut -c1-200
-cp "$OUT/bench.log" profiles/${TAG}_bench_under_rocprof.log 2>/dev/null
+[ -n "$f" ] && head -12 "$f" | cut -c1-200
+
 exit $rc

@@ -2,10 +2,10 @@
 # Block-shape variants of libhipgp for tuning: build here (BUILD=1), time on the GPU box.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 declare -A V
-V[p8]="-DHGP_ROWT_PAIRS=8"
-V[p4]="-DHGP_ROWT_PAIRS=4"
-V[p2]="-DHGP_ROWT_PAIRS=2"
-V[p16]="-DHGP_ROWT_PAIRS=16"
+V[a]=""
+V[b]="-DHGP_CONTIG_THREADS=256"
+V[c]="-DHGP_CONTIG_THREADS=256 -DHGP_ROWT_PAIRS=4"
+V[d]="-DHGP_ROWT_PAIRS=4"
 if [ -n "$BUILD" ]; then
   for k in "${!V[@]}"; do make -s -C hipgp_amd/csrc VARIANT=$k VFLAGS="${V[$k]}" -j4 & done; wait
   exit 0
