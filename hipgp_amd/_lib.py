@@ -24,8 +24,9 @@ EXPORTS = (
     "hgp_plan_create", "hgp_plan_set_stream", "hgp_plan_set_column", "hgp_toeplitz_apply",
     "hgp_pcg_solve", "hgp_pcg_begin", "hgp_pcg_step", "hgp_get_spectrum", "hgp_rowdot",
     "hgp_plan_info", "hgp_plan_destroy", "hgp_last_error", "hgp_version",
-    "hgp_toeplitz_apply_pass", "hgp_op_pass_count", "hgp_pcg_rnorm2",
+    "hgp_toeplitz_apply_pass", "hgp_op_pass_count", "hgp_pcg_rnorm2", "hgp_kuf_grid",
 )
+KERN_SQEXP, KERN_MATERN12, KERN_MATERN32, KERN_MATERN52 = 0, 1, 2, 3
 
 
 class HipgpError(RuntimeError):
@@ -62,6 +63,7 @@ def lib():
         "hgp_toeplitz_apply_pass": (i32, [vp, i32, vp, vp, i64, i32]),
         "hgp_op_pass_count": (i32, [vp]),
         "hgp_pcg_rnorm2": (i32, [vp, vp]),
+        "hgp_kuf_grid": (i32, [i32, i32, i32, pi64, ctypes.POINTER(vp), vp, i64, dbl, dbl, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

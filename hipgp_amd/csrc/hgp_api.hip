@@ -768,6 +768,20 @@ int hgp_rowdot(int dtype, const void* a, const void* c, void* out, int64_t nrhs,
   return 0;
 }
 
+int hgp_kuf_grid(int dtype, int kind, int ndim, const int64_t* m, const void* const* grids, const void* x,
+                 int64_t nobs, double sig2, double ell, void* out, void* hip_stream) {
+  if (ndim < 1 || ndim > 3 || m == nullptr || grids == nullptr) return fail(HGP_E_ARG, "ndim must be 1..3, m/grids non-null");
+  if (kind < HGP_KERN_SQEXP || kind > HGP_KERN_MATERN52) return fail(HGP_E_ARG, "bad kernel kind");
+  if (dtype != HGP_F32 && dtype != HGP_F64) return fail(HGP_E_ARG, "dtype must be HGP_F32 or HGP_F64");
+  if (nobs == 0) return 0;
+  if (nobs < 0 || x == nullptr || out == nullptr) return fail(HGP_E_ARG, "bad x/out/nobs");
+  for (int a = 0; a < ndim; ++a)
+    if (m[a] < 1 || grids[a] == nullptr) return fail(HGP_E_ARG, "grid sizes must be >= 1 with non-null grids");
+  hipError_t e = kuf_grid(dtype, kind, ndim, m, grids, x, nobs, sig2, ell, out, reinterpret_cast<hipStream_t>(hip_stream));
+  if (e != hipSuccess) return fail(HGP_E_HIP, std::string("hgp_kuf_grid: ") + hipGetErrorString(e));
+  return 0;
+}
+
 int hgp_plan_info(const hgp_plan* plan, int64_t* M, int64_t* Mprime, int64_t* L_K, int64_t* L_R) {
   HGP_TRY(check_plan(plan));
   if (M) *M = plan->M;

@@ -35,6 +35,10 @@ template <typename T> void extract_cplx(const double2* F, void* o, int64_t n, in
                                         hipStream_t s, int64_t L0t = 0);
 template <typename T> void expand_spec(const double* src, void* out, const GridDims& g, hipStream_t s);
 
+// dense grid cross covariance (hgp_kuf.hip)
+hipError_t kuf_grid(int dtype, int kind, int ndim, const int64_t* m, const void* const* grids, const void* x,
+                    int64_t nobs, double sig2, double ell, void* out, hipStream_t s);
+
 // CG
 int update_np(int64_t M);
 template <typename T> void cg_init(const void* b, void* x, void* r, int64_t n, hipStream_t s);

@@ -3,11 +3,12 @@
 Mirrors the reference model API of `ziggy/hipgp.py` for the parts that sit on the hot path:
 `ToeplitzInducingGP.compute_kn` (`hipgp.py:117-146`) and the mean-field
 family's ELBO, natural gradient and prediction (`hipgp.py:160-276, 370-446, 449-524`,
-SURVEY §8(f) row 3).  `kn = R^T K^{-1} Knm^T` runs as one plan set-up + hgp_pcg_solve +
+SURVEY §8(f) row 3).  `Knm` comes from the fused grid kernel hgp_kuf_grid (SURVEY §8(f)
+row 1, `hipgp_amd/kuf.py`).  `kn = R^T K^{-1} Knm^T` runs as one plan set-up + hgp_pcg_solve +
 hgp_toeplitz_apply(R^T) on the device; the batch reductions are device tensor ops.
 
-The natural-gradient statistics are split into per-RHS sums (`mf_batch_stats`) and the update
-built from them (`mf_apply_stats`), so a caller that shards the minibatch over GPUs
+The natural-gradient statistics are split into per-RHS sums (`batch_stats`) and the update
+built from them (`apply_stats`), so a caller that shards the minibatch over GPUs
 (`hipgp_amd.dist`) all-reduces exactly those sums.
 
 Not built here (OUT of the hot path): integrated observations (row f2), block /
@@ -54,7 +55,13 @@ class SviGP(nn.Module):
         params = self.get_kernel_params()
         if integrated_obs:
             raise NotImplementedError("integrated (line-integral) observations: SURVEY §8(f) row 2")
-        return self.kernel(xbatch, self.xinduce, params), self.kernel.diag(xbatch, params)
+        Knm = None
+        if getattr(self, "xgrids", None) is not None:
+            from hipgp_amd.kuf import kuf_grid
+            Knm = kuf_grid(self.kernel, self.xgrids, xbatch, params)    # fused HIP kernel
+        if Knm is None:
+            Knm = self.kernel(xbatch, self.xinduce, params)
+        return Knm, self.kernel.diag(xbatch, params)
 
     def batch_predict(self, x, batch_size, verbose=True, **kwargs):
         nb = int(np.ceil(len(x) / batch_size))

@@ -32,6 +32,7 @@ enum { HGP_F32 = 0, HGP_F64 = 1 };
 enum { HGP_OP_K = 0, HGP_OP_CINV = 1, HGP_OP_RT = 2, HGP_OP_R = 3 };
 enum { HGP_SPEC_D = 0, HGP_SPEC_DSQRT = 1, HGP_SPEC_DI = 2 };
 enum { HGP_LAYOUT_ROWS = 0, HGP_LAYOUT_COLS = 1 };
+enum { HGP_KERN_SQEXP = 0, HGP_KERN_MATERN12 = 1, HGP_KERN_MATERN32 = 2, HGP_KERN_MATERN52 = 3 };
 enum {
   HGP_OK = 0, HGP_E_ARG = -1, HGP_E_HIP = -2, HGP_E_STATE = -3, HGP_E_UNSUPPORTED = -4,
   HGP_E_OOM = -5
@@ -107,6 +108,17 @@ int hgp_get_spectrum(hgp_plan* plan, int which, void* out);
  * conj_grad2 path with caller-supplied A_mul callables (cg.py:64,66,69,74). */
 int hgp_rowdot(int dtype, const void* a, const void* c, void* out, int64_t nrhs, int64_t M,
                void* hip_stream);
+
+/* Point-observation cross covariance on a gridded mesh, the PCG right-hand sides:
+ *   out[n, j] = k(x_n, u_j),  x: (nobs, ndim) device, u_j the C-order mesh of grids[0..ndim-1]
+ *   (device arrays of m[a] points), out: (nobs, M) device, dtype HGP_F32 / HGP_F64.
+ * kind: HGP_KERN_SQEXP  sig2 exp(-|(x-u)/ell|^2 / 2)            (kernels.py:73-79)
+ *       HGP_KERN_MATERN{12,32,52}  Matern nu = 1/2, 3/2, 5/2    (kernels.py:145-158)
+ * Same per-element arithmetic as the reference, without its (nobs, M, ndim) broadcast
+ * (replaces svi_gp.py:72 `self.kernel(xbatch, self.xinduce, kern_params)`). */
+int hgp_kuf_grid(int dtype, int kind, int ndim, const int64_t* m, const void* const* grids,
+                 const void* x, int64_t nobs, double sig2, double ell, void* out,
+                 void* hip_stream);
 
 /* Sizes of a plan: M, M' and the padded FFT lengths per axis (K-type and R-type ops). */
 int hgp_plan_info(const hgp_plan* plan, int64_t* M, int64_t* Mprime, int64_t* L_K,

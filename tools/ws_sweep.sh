@@ -3,7 +3,7 @@
 # intermediates resident in the 256 MiB Infinity Cache between passes.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-for mb in ${WS_LIST:-1024 256 128 64 32}; do
+for mb in ${WS_LIST:-1024 200 136 100 68}; do
   HGP_WS_MB=$mb timeout -k 10 120 python bench.py --no-cpu-baseline --steps 20 --warmup 5 --pcg-reps 2 ${BENCH_ARGS:-} > gpurun_out/ws_$mb.json 2> gpurun_out/ws_$mb.err || exit $?
   python - "$mb" <<'PY'
 import json, sys
