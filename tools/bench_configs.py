@@ -67,8 +67,15 @@ def run(name, dev):
     xobs = (lo + (hi - lo) * torch.rand(B, d, generator=g)).to(dev)
     mesh = torch.meshgrid(*grids, indexing="ij")
     xs = torch.stack([x.reshape(-1) for x in mesh], dim=-1)
-    Knm = torch.cat([kf(xobs[i:i + 64], xs) for i in range(0, B, 64)], dim=0).contiguous()
+    from hipgp_amd.kuf import kuf_grid
     out = {"config": name, "dims": dims, "M": int(np.prod(dims)), "B": B, "maxiter": maxiter, "tol": tol}
+    Knm = kuf_grid(k, grids, xobs, params)
+    out["kuf_fused_ms"] = timed(lambda: kuf_grid(k, grids, xobs, params), reps=5) * 1e3
+    try:    # the reference's broadcast evaluation (kernels.py:78,149), for comparison
+        out["kuf_broadcast_ms"] = timed(lambda: kf(xobs, xs), reps=3) * 1e3
+    except torch.cuda.OutOfMemoryError:
+        out["kuf_broadcast_ms"] = None
+    torch.cuda.empty_cache()
     if d == 1:
         t = timed(lambda: te.gram_solve(grids, kf, Knm, maxiter=maxiter, do_precond=True, tol=tol, mult_RT=True))
         out.update({"gram_solve_s": t, "reference_cpu": ref, "speedup_vs_reference_cpu": ref["gram_solve_s"] / t})
