@@ -4,6 +4,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -160,12 +161,30 @@ int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
 // compact half-spectrum row length of the last (real) axis: >= H+1, 64-byte aligned rows
 int64_t compact_stride(int64_t L) { return round_up(L / 2 + 1, 8); }
 
+// Fused PCG epilogue of the 2-D row-inverse pass (hgp_rows.hpp EPI_XR / EPI_P): the operator
+// output y updates the CG vectors (x, r, p: row layout, nrhs x M) instead of being stored.
+struct RowEpi {
+  int mode;
+  void* r;
+  void* x;
+  void* p;
+  const void* coef;   // per-RHS alpha (EPI_XR) or beta (EPI_P)
+  void* part;         // EPI_XR: r.r partials [q][row block]
+};
+
+// Called between the 2-D column pass and the row-inverse pass of each RHS chunk (q0, qn):
+// computes the chunk's alpha / beta from the column pass's spectral dots.
+using MidFn = std::function<void(int64_t, int)>;
+
 // y = op(x) on RHS [0, nrhs); optional fused dot with `dotv` into partial[b][rn_last].
 // Every RHS is processed on its own (no two RHS share an FFT).  only_pass >= 0 runs a single
-// pass of the sequence (profiling).
+// pass of the sequence (profiling).  2-D only: `spart` receives the column pass's spectral
+// dots <x, op x> per (RHS, compact column) [q][L_1/2 + 1]; `epi` replaces the output store by
+// the fused PCG update, `mid` runs between the column pass and the row-inverse pass.
 template <typename T>
 int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void* dotv, void* partial,
-           const int* done, int only_pass = -1) {
+           const int* done, int only_pass = -1, void* spart = nullptr, const RowEpi* epi = nullptr,
+           const MidFn* mid = nullptr) {
   const OpGeom g = op_geom(P, op);
   const int d = P->d;
   const int conv_mode = g.spec_kind == SPEC_REAL ? PASS_CONV : PASS_CONVC;
@@ -218,10 +237,10 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
     } else if (d == 2) {
       C2<T>* w1 = reinterpret_cast<C2<T>*>(P->ws1.ptr);
       const int64_t H1 = g.L[1] / 2;
-      auto run_rowt = [&](int inv, PassDesc& D) -> int {
+      auto run_rowt = [&](int inv, PassDesc& D, int epi_mode) -> int {
         const int me = pass_no++;
         if (only_pass >= 0 && only_pass != me) return 0;
-        hipError_t e = launch_rowt<T>((int)H1, inv, D, P->stream);
+        hipError_t e = launch_rowt<T>((int)H1, inv, epi_mode, D, P->stream);
         if (e != hipSuccess) return fail(HGP_E_HIP, std::string("row pass launch: ") + hipGetErrorString(e));
         return 0;
       };
@@ -230,21 +249,36 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
       A.in = View{(void*)xi, g.in_M, g.in[1], 1, (int)g.in[1]};
       A.out = View{w1, B1, S0, 1, 0};
       A.tw = g.tw[1].ptr; A.Q = qn; A.Rn = (int)((g.in[0] + 1) / 2); A.nrows = (int)g.in[0]; A.done = done;
-      HGP_TRY(run_rowt(0, A));
+      HGP_TRY(run_rowt(0, A, EPI_OUT));
       // B: CONV along axis 0 = contiguous lines (q, c1), in place; spectrum [c1][k0]
       PassDesc Bd = base_desc();
       Bd.in = View{w1, B1, S0, 1, (int)g.in[0]};
       Bd.out = View{w1, B1, S0, 1, (int)g.out[0]};
       Bd.spec = g.spec; Bd.spec_kind = g.spec_kind; Bd.spec_i = 0; Bd.spec_p = 1; Bd.spec_r = g.L[0];
       Bd.tw = g.tw[0].ptr; Bd.Q = qn; Bd.Rn = (int)(H1 + 1); Bd.In = 1; Bd.done = done;
+      if (spart != nullptr) {
+        Bd.spart = reinterpret_cast<T*>(spart) + q0 * (H1 + 1);
+        Bd.spart_mid = (int)(H1 / 2);
+      }
       HGP_TRY(run((int)(g.L[0] / 2), conv_mode, LAY_CONTIG, Bd, (int64_t)qn * Bd.Rn));
-      // C: INV along axis 1: column-major tiles -> row pairs, crop, fused dot
+      if (mid != nullptr) (*mid)(q0, qn);
+      // C: INV along axis 1: column-major tiles -> row pairs, crop, fused dot or PCG update
       PassDesc Cd = base_desc();
       Cd.in = View{w1, B1, S0, 1, 0};
       Cd.out = View{yo, g.out_M, g.out[1], 1, (int)g.out[1]};
       Cd.dot = dvc; Cd.partial = pc;
       Cd.tw = g.tw[1].ptr; Cd.Q = qn; Cd.Rn = (int)((g.out[0] + 1) / 2); Cd.nrows = (int)g.out[0]; Cd.done = done;
-      HGP_TRY(run_rowt(1, Cd));
+      int epi_mode = EPI_OUT;
+      if (epi != nullptr) {
+        epi_mode = epi->mode;
+        const int nrb = (Cd.Rn + rowt_pairs<T>((int)H1) - 1) / rowt_pairs<T>((int)H1);
+        Cd.cg_r = reinterpret_cast<T*>(epi->r) + q0 * g.out_M;
+        Cd.cg_x = reinterpret_cast<T*>(epi->x) + q0 * g.out_M;
+        Cd.cg_p = reinterpret_cast<T*>(epi->p) + q0 * g.out_M;
+        Cd.cg_coef = reinterpret_cast<const T*>(epi->coef) + q0;
+        Cd.cg_part = epi->part ? reinterpret_cast<T*>(epi->part) + q0 * nrb : nullptr;
+      }
+      HGP_TRY(run_rowt(1, Cd, epi_mode));
     } else {
       C2<T>* w1 = reinterpret_cast<C2<T>*>(P->ws1.ptr);
       C2<T>* w2 = reinterpret_cast<C2<T>*>(P->ws2.ptr);
@@ -476,6 +510,16 @@ int rn_last(const hgp_plan* P) {
   return (int)((P->m[0] * P->m[1] + 1) / 2);
 }
 
+// 2-D fused PCG (pcg_step_t): the dots p.Ap and z.r come from the column pass as spectral
+// sums over the (RHS, compact column) lines, L_1/2 + 1 partials per RHS; r.r from the fused
+// x/r update, one partial per row block of the row-inverse pass.
+int spec_np(const hgp_plan* P) { return (int)(P->LK[1] / 2 + 1); }
+template <typename T>
+int xr_np(const hgp_plan* P) {
+  const int pairs = rowt_pairs<T>((int)(P->LK[1] / 2));
+  return (int)(((P->m[0] + 1) / 2 + pairs - 1) / pairs);
+}
+
 template <typename T>
 int pcg_begin_t(hgp_plan* P, const void* b, void* x, int64_t nrhs, int use_precond, int layout) {
   hipStream_t s = P->stream;
@@ -485,7 +529,9 @@ int pcg_begin_t(hgp_plan* P, const void* b, void* x, int64_t nrhs, int use_preco
   HGP_TRY(P->z.ensure(vb));
   HGP_TRY(P->p.ensure(vb));
   HGP_TRY(P->Ap.ensure(vb));
-  const int npo = rn_last(P), npu = update_np(M);
+  const bool fused = P->d == 2;
+  const int npo = fused ? std::max(rn_last(P), spec_np(P)) : rn_last(P);
+  const int npu = fused ? std::max(update_np(M), xr_np<T>(P)) : update_np(M);
   HGP_TRY(P->part_op.ensure((size_t)(nrhs * npo) * sizeof(T)));
   HGP_TRY(P->part_u.ensure((size_t)(nrhs * npu) * sizeof(T)));
   HGP_TRY(P->scal.ensure((size_t)(4 * nrhs) * sizeof(T)));
@@ -504,7 +550,11 @@ int pcg_begin_t(hgp_plan* P, const void* b, void* x, int64_t nrhs, int use_preco
   T* sc = reinterpret_cast<T*>(P->scal.ptr);
   T* rs = sc;
   cg_init<T>(brow, xrow, P->r.ptr, nrhs * M, s);
-  if (use_precond) {
+  if (use_precond && fused) {
+    // p = z = C^-1 r straight into p; rs = z.r as the column pass's spectral dot
+    HGP_TRY(run_op<T>(P, HGP_OP_CINV, P->r.ptr, P->p.ptr, nrhs, nullptr, nullptr, nullptr, -1, P->part_op.ptr));
+    reduce_rows<T>(P->part_op.ptr, spec_np(P), (int)nrhs, rs, s);
+  } else if (use_precond) {
     HGP_TRY(run_op<T>(P, HGP_OP_CINV, P->r.ptr, P->z.ptr, nrhs, P->r.ptr, P->part_op.ptr, nullptr));
     reduce_rows<T>(P->part_op.ptr, npo, (int)nrhs, rs, s);
     vcopy<T>(P->z.ptr, P->p.ptr, nrhs * M, nullptr, s);
@@ -536,6 +586,32 @@ int pcg_step_t(hgp_plan* P, double tol) {
   T* alpha = sc + nrhs;
   T* beta = sc + 2 * nrhs;
   T* rnew = sc + 3 * nrhs;
+  if (P->d == 2) {
+    // Fused 2-D iteration.  K p: the column pass leaves the spectral p.Ap partials, alpha is
+    // formed per RHS chunk before the row-inverse pass, whose epilogue does x += alpha p,
+    // r -= alpha Ap (+ r.r partials) with Ap never stored.  Then the break test; then C^-1 r,
+    // whose epilogue does p = z + beta p (z never stored).  Order and semantics of cg.py:63-78.
+    const int nps = spec_np(P), npx = xr_np<T>(P);
+    T* part_s = reinterpret_cast<T*>(P->part_op.ptr);
+    const MidFn mid_alpha = [&](int64_t q0, int qn) {
+      cg_alpha<T>(part_s + q0 * nps, nps, qn, rs + q0, alpha + q0, done, s);
+    };
+    const RowEpi exr{EPI_XR, P->r.ptr, P->cg_x, P->p.ptr, alpha, P->part_u.ptr};
+    HGP_TRY(run_op<T>(P, HGP_OP_K, P->p.ptr, P->Ap.ptr, nrhs, nullptr, nullptr, done, -1, part_s, &exr, &mid_alpha));
+    cg_check<T>(P->part_u.ptr, npx, (int)nrhs, tol, rnew, done, iters, s);
+    if (P->cg_precond) {
+      const MidFn mid_beta = [&](int64_t q0, int qn) {
+        cg_beta<T>(part_s + q0 * nps, nps, qn, rs + q0, beta + q0, done, s);
+      };
+      const RowEpi ep{EPI_P, P->r.ptr, P->cg_x, P->p.ptr, beta, nullptr};
+      HGP_TRY(run_op<T>(P, HGP_OP_CINV, P->r.ptr, P->Ap.ptr, nrhs, nullptr, nullptr, done, -1, part_s, &ep, &mid_beta));
+    } else {
+      cg_beta<T>(P->part_u.ptr, npx, (int)nrhs, rs, beta, done, s);
+      cg_update_p<T>(P->p.ptr, P->r.ptr, beta, nrhs, M, done, s);
+    }
+    HIP_TRY(hipGetLastError());
+    return 0;
+  }
   // Ap = K p ; fused p.Ap
   HGP_TRY(run_op<T>(P, HGP_OP_K, P->p.ptr, P->Ap.ptr, nrhs, P->p.ptr, P->part_op.ptr, done));
   cg_alpha<T>(P->part_op.ptr, npo, (int)nrhs, rs, alpha, done, s);

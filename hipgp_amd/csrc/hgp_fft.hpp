@@ -255,4 +255,101 @@ __device__ __forceinline__ void fft_line(C2<T> (&v)[P], C2<T>* lds, int base, in
   fft_stage<T, H, P, DIR, STRIDE, WAVE, 0>(v, lds, base, tt, tab);
 }
 
+// ---- two independent transforms of one thread group, software-pipelined over ONE exchange
+// image.  Stage S of transform a exchanges through LDS while the butterflies of transform b
+// run (and vice versa), so the LDS write -> read latency of one transform is covered by the
+// other's arithmetic instead of stalling the wave.  Same arithmetic, per transform, as
+// fft_line (bitwise identical results).
+
+// stage-S butterflies of the P values in v -> a, in exchange-write order a[b*R + r]
+template <typename T, int H, int P, int DIR, int S>
+__device__ __forceinline__ void fft_bfly(const C2<T> (&v)[P], C2<T> (&a)[P], int t,
+                                         const C2<T>* __restrict__ tab) {
+  using St = Stages<H, P>;
+  constexpr int R = St::radix(S), NS = St::ns(S), TT = H / P, NB = P / R;
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) a[b * R + r] = v[b + r * NB];
+    if constexpr (NS > 1) {
+      const int j = t + b * TT;
+      const int kk = j & (NS - 1);
+      C2<T> wp[R];
+      wp[1] = tw_at<T, H>(tab, (2 * (H / (NS * R))) * kk);
+#pragma unroll
+      for (int r = 2; r < R; ++r) {
+        const int hi = (r & (r - 1)) == 0 ? r / 2 : (1 << (31 - __builtin_clz(r)));
+        const int lo = r - hi;
+        wp[r] = cmul<T>(wp[hi], wp[lo]);
+      }
+#pragma unroll
+      for (int r = 1; r < R; ++r)
+        a[b * R + r] = (DIR < 0) ? cmul<T>(a[b * R + r], wp[r]) : cmulc<T>(a[b * R + r], wp[r]);
+    }
+    dft<T, R, DIR>(&a[b * R]);
+  }
+}
+
+// exchange after stage S: write a (stage-S outputs), read this thread's stage-(S+1) inputs
+template <typename T, int H, int P, int STRIDE, bool WAVE, int S>
+__device__ __forceinline__ void fft_xchg(const C2<T> (&a)[P], C2<T> (&v)[P], C2<T>* lds, int base, int t) {
+  using St = Stages<H, P>;
+  constexpr int R = St::radix(S), NS = St::ns(S), TT = H / P, NB = P / R;
+  const int idxD = (t / NS) * NS * R + (t & (NS - 1));
+  const int wb = base + idxD * STRIDE;
+  const int pwb = lds_phys(wb);
+  constexpr bool WB16 = (STRIDE == 1) && (NS == 1) && (R == 16);
+  xsync<WAVE>();   // earlier readers of the image are done
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int r = 0; r < R; ++r) lds[lds_at(pwb, wb, (b * TT * R + r * NS) * STRIDE, WB16)] = a[b * R + r];
+  xsync<WAVE>();
+  const int rb = base + t * STRIDE;
+  const int prb = lds_phys(rb);
+#pragma unroll
+  for (int k = 0; k < P; ++k) v[k] = lds[lds_at(prb, rb, TT * k * STRIDE, false)];
+}
+
+// last stage's outputs back to natural register order
+template <typename T, int H, int P, int S>
+__device__ __forceinline__ void fft_final(const C2<T> (&a)[P], C2<T> (&v)[P]) {
+  using St = Stages<H, P>;
+  constexpr int R = St::radix(S), NB = P / R;
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[b + r * NB] = a[b * R + r];
+}
+
+template <typename T, int H, int P, int DIR, int STRIDE, bool WAVE, int S>
+__device__ __forceinline__ void fft_stage2(C2<T> (&va)[P], C2<T> (&vb)[P], C2<T> (&a)[P], C2<T>* lds, int base, int t,
+                                           const C2<T>* __restrict__ tab) {
+  // entry: a = stage-S butterflies of va (already computed); vb holds stage-S inputs
+  constexpr int NST = Stages<H, P>::count();
+  if constexpr (S + 1 < NST) {
+    fft_xchg<T, H, P, STRIDE, WAVE, S>(a, va, lds, base, t);       // va: stage S+1 inputs in flight
+    fft_bfly<T, H, P, DIR, S>(vb, a, t, tab);                       // ... while vb's butterflies run
+    fft_xchg<T, H, P, STRIDE, WAVE, S>(a, vb, lds, base, t);
+    fft_bfly<T, H, P, DIR, S + 1>(va, a, t, tab);                   // ... while vb's reads land
+    fft_stage2<T, H, P, DIR, STRIDE, WAVE, S + 1>(va, vb, a, lds, base, t, tab);
+  } else {
+    fft_final<T, H, P, S>(a, va);
+    fft_bfly<T, H, P, DIR, S>(vb, a, t, tab);
+    fft_final<T, H, P, S>(a, vb);
+  }
+}
+
+// Two H-point FFTs (same direction) of the lines whose values this thread holds in va and vb,
+// through one exchange image at `base` (fft_line semantics for each).
+template <typename T, int H, int P, int DIR, int STRIDE, bool WAVE = false>
+__device__ __forceinline__ void fft_line2(C2<T> (&va)[P], C2<T> (&vb)[P], C2<T>* lds, int base, int t,
+                                          const C2<T>* __restrict__ tab) {
+  int tt = t;
+  asm volatile("" : "+v"(tt));
+  C2<T> a[P];
+  fft_bfly<T, H, P, DIR, 0>(va, a, tt, tab);
+  fft_stage2<T, H, P, DIR, STRIDE, WAVE, 0>(va, vb, a, lds, base, tt, tab);
+}
+
 }  // namespace hgp

@@ -15,7 +15,9 @@ hipError_t launch_pass(int H, int mode, int lay, const PassDesc& d, int64_t nblo
 template <typename T> PassGeom pass_geom(int H, int lay);
 // 2-D row-pair passes with the column-major intermediate (hgp_rows.hpp); inv = 0 FWD, 1 INV
 template <typename T>
-hipError_t launch_rowt(int H, int inv, const PassDesc& d, hipStream_t s);
+hipError_t launch_rowt(int H, int inv, int epi, const PassDesc& d, hipStream_t s);
+// row pairs per block of the 2-D row passes (partials of the fused PCG epilogue are per block)
+template <typename T> int rowt_pairs(int H);
 
 // setup (fp64)
 // Bluestein partial DFT pieces of the DCT-I (hgp_kernels.hip)
@@ -38,6 +40,9 @@ template <typename T> void expand_spec(const double* src, void* out, const GridD
 // dense grid cross covariance (hgp_kuf.hip)
 hipError_t kuf_grid(int dtype, int kind, int ndim, const int64_t* m, const void* const* grids, const void* x,
                     int64_t nobs, double sig2, double ell, void* out, hipStream_t s);
+hipError_t kuf_semi_grid(int dtype, int kind, int method, int ndim, const int64_t* m, const void* const* grids,
+                         const void* x, int64_t nobs, double sig2, double ell, const void* nodes,
+                         const void* weights, int npts, void* out, hipStream_t s);
 
 // CG
 int update_np(int64_t M);

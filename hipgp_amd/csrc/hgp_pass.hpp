@@ -58,6 +58,7 @@ namespace hgp {
 enum { PASS_FWD = 0, PASS_INV = 1, PASS_CONV = 2, PASS_CONVC = 3 };   // CONV: real spectrum, CONVC: complex
 enum { LAY_STRIDED = 0, LAY_CONTIG = 1, LAY_RP = 2, LAY_R1 = 3 };
 enum { SPEC_REAL = 0, SPEC_CPLX = 1, SPEC_CPLX_CONJ = 2 };
+enum { EPI_OUT = 0, EPI_XR = 1, EPI_P = 2 };   // 2-D row-inverse epilogue (hgp_rows.hpp)
 
 struct View {
   void* ptr;
@@ -79,6 +80,18 @@ struct PassDesc {
   int Rn, In;                 // lines per RHS: r in [0,Rn) (outer), i in [0,In) (inner, strided)
   int nrows;                  // LAY_RP: real rows per RHS (the pair (2r, 2r+1) needs 2r+1 < nrows)
   const int* done;            // optional device flag: skip the pass when *done != 0
+  // CONV passes (non-strided): spectral dot of the transformed line with itself weighted by
+  // the real spectrum, sum_k S_k |X_k|^2 = <x, op x> by Parseval (the crop is exact: x is zero
+  // outside it), stored as spart[q * Rn + r] x the compact-column weight (1 for columns 0 and
+  // spart_mid, else 2 = the column and its Hermitian mirror; spart_mid < 0: weight 1).
+  void* spart;
+  int spart_mid;
+  // fused PCG epilogue of the 2-D row-inverse pass (hgp_rows.hpp, EPI_XR / EPI_P)
+  void* cg_r;
+  void* cg_x;
+  void* cg_p;
+  const void* cg_coef;        // per-RHS alpha (EPI_XR) or beta (EPI_P)
+  void* cg_part;              // EPI_XR: per-block partial sums of r.r  [q][row block]
 };
 
 constexpr int LDS_CAP = 160 * 1024;
@@ -212,8 +225,9 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
     lc = valid ? l : 0;             // keep every (unconditional) load in bounds
   } else if constexpr (LAY == LAY_CONTIG) {
     // RHS-fastest: the C lines of a block are the same column r of C right-hand sides, so
-    // they share one spectrum line (read once per block into L1/L2, not once per RHS)
-    const int64_t line = (int64_t)blockIdx.x * C + l;
+    // they share one spectrum line; the XCD remap keeps the blocks of one column (all its
+    // RHS) on one XCD, so the line is fetched into that L2 once
+    const int64_t line = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * C + l;
     r = (int)(line / d.Q);
     q = (int)(line - (int64_t)r * d.Q);
     i = 0;
@@ -310,14 +324,13 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
   // half's right after the even product (in flight during the even IFFT + odd FFT), so at
   // most one half's spectrum is live in registers
   T sre[P];
+  T sdot = 0;
   const T* sb = nullptr;
   int so = 0, sp = 0;
   if constexpr (MODE == PASS_CONV) {
     sb = reinterpret_cast<const T*>(d.spec) + (int64_t)i0 * d.spec_i + (int64_t)r * d.spec_r;
     sp = (int)d.spec_p;
     so = (LAY == LAY_STRIDED ? lc * (int)d.spec_i : 0) + t * sp;
-#pragma unroll
-    for (int k = 0; k < P; ++k) sre[k] = sb[so + TT * k * sp];
   }
   if constexpr (MODE == PASS_FWD || CONV) {
     const int in_len = d.in.len;
@@ -338,9 +351,10 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
   }
 
   if constexpr (MODE == PASS_FWD) {
+    // both halves' transforms interleaved over one exchange image (hgp_fft.hpp fft_line2)
+    fft_line2<T, H, P, -1, LSTRIDE, Cfg::WAVE>(va, vb, lds, lbase, t, tab);
     auto fwd_half = [&](auto half_c, C2<T>(&v)[P]) {
       constexpr int half = decltype(half_c)::value;
-      fft_line<T, H, P, -1, LSTRIDE, Cfg::WAVE>(v, lds, lbase, t, tab);
       if constexpr (HERM_OUT) {
         // split Z = X_a + i X_b by Hermitian symmetry: partner of position p is
         // (H - p) mod H in the even half and H - 1 - p in the odd half.
@@ -369,39 +383,56 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
     fwd_half(std::integral_constant<int, 0>{}, va);
     fwd_half(std::integral_constant<int, 1>{}, vb);
   } else {
-    // va ends as the even half's inverse (ye), vb as the odd half's (yo)
-    auto inv_half = [&](auto half_c, C2<T>(&v)[P]) {
-      constexpr int half = decltype(half_c)::value;
-      if constexpr (MODE == PASS_CONV) {
-        fft_line<T, H, P, -1, LSTRIDE, Cfg::WAVE>(v, lds, lbase, t, tab);
+    // va ends as the even half's inverse (ye), vb as the odd half's (yo); the two halves'
+    // transforms run interleaved over one exchange image (hgp_fft.hpp fft_line2)
+    if constexpr (MODE == PASS_CONV) {
+      fft_line2<T, H, P, -1, LSTRIDE, Cfg::WAVE>(va, vb, lds, lbase, t, tab);
+      // the line's real spectrum, loaded after the forward transforms (no registers held across
+      // them); L2-resident: every line of a block shares it (RHS-fastest map, XCD-grouped)
+      T sre1[P];
 #pragma unroll
-        for (int k = 0; k < P; ++k) v[k] = mk<T>(v[k].x * sre[k], v[k].y * sre[k]);
-        if constexpr (half == 0) {
-#pragma unroll
-          for (int k = 0; k < P; ++k) sre[k] = sb[so + (H + TT * k) * sp];
-        }
-      } else if constexpr (MODE == PASS_CONVC) {
-        fft_line<T, H, P, -1, LSTRIDE, Cfg::WAVE>(v, lds, lbase, t, tab);
-        // complex spectrum at (i, r, kperm): block-uniform base + 32-bit lane offset
-        const C2<T>* sbase = reinterpret_cast<const C2<T>*>(d.spec) + (int64_t)i0 * d.spec_i + (int64_t)r * d.spec_r;
-        const int sp = (int)d.spec_p;
-        const int so = (LAY == LAY_STRIDED ? lc * (int)d.spec_i : 0) + (half * H + t) * sp;
+      for (int k = 0; k < P; ++k) {
+        sre[k] = sb[so + TT * k * sp];
+        sre1[k] = sb[so + (H + TT * k) * sp];
+      }
+      if (d.spart != nullptr) {   // uniform: spectral dot sum_k S_k |X_k|^2 of this line
 #pragma unroll
         for (int k = 0; k < P; ++k) {
-          const C2<T> sv = sbase[so + TT * k * sp];
-          v[k] = d.spec_kind == SPEC_CPLX ? cmul<T>(v[k], sv) : cmulc<T>(v[k], sv);
-        }
-      } else {
-#pragma unroll
-        for (int k = 0; k < P; ++k) {
-          if constexpr (HERM_IN) v[k] = load_herm(half, t + TT * k);
-          else v[k] = load_in(half * H + t + TT * k);
+          sdot += sre[k] * (va[k].x * va[k].x + va[k].y * va[k].y);
+          sdot += sre1[k] * (vb[k].x * vb[k].x + vb[k].y * vb[k].y);
         }
       }
-      fft_line<T, H, P, +1, LSTRIDE, Cfg::WAVE>(v, lds, lbase, t, tab);
-    };
-    inv_half(std::integral_constant<int, 0>{}, va);
-    inv_half(std::integral_constant<int, 1>{}, vb);
+#pragma unroll
+      for (int k = 0; k < P; ++k) {
+        va[k] = mk<T>(va[k].x * sre[k], va[k].y * sre[k]);
+        vb[k] = mk<T>(vb[k].x * sre1[k], vb[k].y * sre1[k]);
+      }
+    } else if constexpr (MODE == PASS_CONVC) {
+      fft_line2<T, H, P, -1, LSTRIDE, Cfg::WAVE>(va, vb, lds, lbase, t, tab);
+      // complex spectrum at (i, r, kperm): block-uniform base + 32-bit lane offset
+      const C2<T>* sbase = reinterpret_cast<const C2<T>*>(d.spec) + (int64_t)i0 * d.spec_i + (int64_t)r * d.spec_r;
+      const int sp = (int)d.spec_p;
+      const int so0 = (LAY == LAY_STRIDED ? lc * (int)d.spec_i : 0) + t * sp;
+#pragma unroll
+      for (int k = 0; k < P; ++k) {
+        const C2<T> s0 = sbase[so0 + TT * k * sp];
+        const C2<T> s1 = sbase[so0 + (H + TT * k) * sp];
+        va[k] = d.spec_kind == SPEC_CPLX ? cmul<T>(va[k], s0) : cmulc<T>(va[k], s0);
+        vb[k] = d.spec_kind == SPEC_CPLX ? cmul<T>(vb[k], s1) : cmulc<T>(vb[k], s1);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < P; ++k) {
+        if constexpr (HERM_IN) {
+          va[k] = load_herm(0, t + TT * k);
+          vb[k] = load_herm(1, t + TT * k);
+        } else {
+          va[k] = load_in(t + TT * k);
+          vb[k] = load_in(H + t + TT * k);
+        }
+      }
+    }
+    fft_line2<T, H, P, +1, LSTRIDE, Cfg::WAVE>(va, vb, lds, lbase, t, tab);
     // combine in registers: y[p] = ye + conj(W_L^p) yo, y[p+H] = ye - conj(W_L^p) yo; crop.
     const int out_len = d.out.len;
     const T* dot_re = nullptr; const T* dot_im = nullptr;
@@ -444,6 +475,15 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
       if (d.partial != nullptr) {   // uniform over the block
         const T s = line_sum<T, TT>(dsum, reinterpret_cast<T*>(smem_raw));
         if (t == 0 && valid) reinterpret_cast<T*>(d.partial)[(int64_t)q * d.Rn + r] = s;
+      }
+    }
+    if constexpr (MODE == PASS_CONV && LAY != LAY_STRIDED) {
+      if (d.spart != nullptr) {     // uniform over the block
+        const T s = line_sum<T, TT>(sdot, reinterpret_cast<T*>(smem_raw));
+        if (t == 0 && valid) {
+          const T w = (d.spart_mid < 0 || r == 0 || r == d.spart_mid) ? (T)1 : (T)2;
+          reinterpret_cast<T*>(d.spart)[(int64_t)q * d.Rn + r] = w * s;
+        }
       }
     }
   }

@@ -66,27 +66,53 @@ static PassGeom geom_h(int lay) {
     default: break;                                                                                  \
   }
 
-template <typename T, int H>
-static hipError_t launch_rowt_h(int inv, const PassDesc& d, hipStream_t s) {
+template <typename T, int H, int EPI>
+static hipError_t launch_rowt_inv(const PassDesc& d, int64_t nb, hipStream_t s) {
   using Cfg = RowTCfg<T, H>;
-  const int64_t nb = (int64_t)d.Q * ((d.Rn + Cfg::C - 1) / Cfg::C);
-  if (nb <= 0) return hipSuccess;
-  static bool attr_set[2] = {false, false};
-  const void* fn = inv ? (const void*)k_row_inv_t<T, H> : (const void*)k_row_fwd_t<T, H>;
-  if (!attr_set[inv]) {
-    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS);
+  static bool attr_set = false;   // opt in to > 64 KB dynamic LDS once per instance
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)k_row_inv_t<T, H, EPI>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS);
     if (e != hipSuccess) return e;
-    attr_set[inv] = true;
+    attr_set = true;
   }
-  if (inv) hipLaunchKernelGGL((k_row_inv_t<T, H>), dim3((unsigned)nb), dim3(Cfg::THREADS), Cfg::LDS, s, d);
-  else hipLaunchKernelGGL((k_row_fwd_t<T, H>), dim3((unsigned)nb), dim3(Cfg::THREADS), Cfg::LDS, s, d);
+  hipLaunchKernelGGL((k_row_inv_t<T, H, EPI>), dim3((unsigned)nb), dim3(Cfg::THREADS), Cfg::LDS, s, d);
   return hipGetLastError();
 }
 
+template <typename T, int H>
+static hipError_t launch_rowt_h(int inv, int epi, const PassDesc& d, hipStream_t s) {
+  using Cfg = RowTCfg<T, H>;
+  const int64_t nb = (int64_t)d.Q * ((d.Rn + Cfg::C - 1) / Cfg::C);
+  if (nb <= 0) return hipSuccess;
+  if (inv) {
+    if (epi == EPI_XR) return launch_rowt_inv<T, H, EPI_XR>(d, nb, s);
+    if (epi == EPI_P) return launch_rowt_inv<T, H, EPI_P>(d, nb, s);
+    return launch_rowt_inv<T, H, EPI_OUT>(d, nb, s);
+  }
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)k_row_fwd_t<T, H>, hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((k_row_fwd_t<T, H>), dim3((unsigned)nb), dim3(Cfg::THREADS), Cfg::LDS, s, d);
+  return hipGetLastError();
+}
+
+template <typename T, int H>
+static int rowt_pairs_h() { return RowTCfg<T, H>::C; }
+
 template <typename T>
-hipError_t launch_rowt(int H, int inv, const PassDesc& d, hipStream_t s) {
-  HGP_H_SWITCH(launch_rowt_h, inv, d, s)
+hipError_t launch_rowt(int H, int inv, int epi, const PassDesc& d, hipStream_t s) {
+  HGP_H_SWITCH(launch_rowt_h, inv, epi, d, s)
   return hipErrorInvalidValue;
+}
+
+template <typename T>
+int rowt_pairs(int H) {
+  HGP_H_SWITCH(rowt_pairs_h)
+  return 0;
 }
 
 template <typename T>

@@ -99,9 +99,10 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
   const int row0 = 2 * rb * C;                     // first row of this block's tile
   const int nrow_blk = d.nrows - row0 < 2 * C ? d.nrows - row0 : 2 * C;
 
+  // both frequency halves' transforms, interleaved over the group's exchange image
+  fft_line2<T, H, P, -1, 1, Cfg::WAVE>(va, vb, lds, lbase, t, tab);
   auto do_half = [&](auto half_c, C2<T>(&v)[P]) {
     constexpr int half = decltype(half_c)::value;
-    fft_line<T, H, P, -1, 1, Cfg::WAVE>(v, lds, lbase, t, tab);
     // Hermitian split through this group's exchange image
     xsync<Cfg::WAVE>();
 #pragma unroll
@@ -151,7 +152,51 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
 //   in : View{W, q_stride, r_stride = column pitch S0, 1, 0}
 //   out: View{y, q_stride (elements per RHS), r_stride (row pitch), 1, len = out row length}
 //   nrows = output rows per RHS, Rn = ceil(nrows / 2); dot/partial as in k_pass.
-template <typename T, int H>
+// Fused PCG update of one block's output rows y (staged in LDS, `ys` [row][col], pitch
+// out_len), streamed with the row layout of the (nrhs, M) vectors:
+//   EPI_XR (y = A p):     x += a p;  r -= a y;  returns this thread's share of r.r  (cg.py:67-69)
+//   EPI_P  (y = C^-1 r):  p = y + b p                                                 (cg.py:75)
+// Four elements per thread are loaded before any is stored (the vectors never alias).
+template <typename T, int EPI, int THREADS>
+__device__ __forceinline__ T cg_epilogue(const T* __restrict__ ys, int nrow, int out_len, T* __restrict__ xg,
+                                         T* __restrict__ rg, T* __restrict__ pg, int64_t rpitch, T coef) {
+  const int nel = nrow * out_len;
+  T s = 0;
+  for (int e0 = threadIdx.x; e0 < nel; e0 += 4 * THREADS) {
+    int64_t g[4];
+    T yv[4], pv[4], xv[4], rv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = e0 + u * THREADS;
+      const int ee = e < nel ? e : nel - 1;
+      const int row = ee / out_len;
+      const int c = ee - row * out_len;
+      g[u] = (int64_t)row * rpitch + c;
+      yv[u] = ys[ee];
+      pv[u] = pg[g[u]];
+      if constexpr (EPI == EPI_XR) {
+        xv[u] = xg[g[u]];
+        rv[u] = rg[g[u]];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (e0 + u * THREADS < nel) {
+        if constexpr (EPI == EPI_XR) {
+          xg[g[u]] = xv[u] + coef * pv[u];
+          const T rn = rv[u] - coef * yv[u];
+          rg[g[u]] = rn;
+          s += rn * rn;
+        } else {
+          pg[g[u]] = yv[u] + coef * pv[u];
+        }
+      }
+    }
+  }
+  return s;
+}
+
+template <typename T, int H, int EPI = EPI_OUT>
 __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) void k_row_inv_t(const PassDesc d) {
   using Cfg = RowTCfg<T, H>;
   constexpr int P = Cfg::P, TT = Cfg::TT, C = Cfg::C, PITCH = Cfg::PITCH;
@@ -220,14 +265,56 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
       if (cj) { A.y = -A.y; B.y = -B.y; }
       v[k] = mk<T>(A.x - B.y, A.y + B.x);
     }
-    __syncthreads();   // tile consumed: the FFT exchange images overlay it
-    fft_line<T, H, P, +1, 1, Cfg::WAVE>(v, lds, lbase, t, tab);
   };
   do_half(std::integral_constant<int, 0>{}, va);
-  do_half(std::integral_constant<int, 1>{}, vb);
+  do_half(std::integral_constant<int, 1>{}, vb);   // (starts with a barrier: even tile consumed)
+  __syncthreads();   // tile consumed: the FFT exchange images overlay it
+  fft_line2<T, H, P, +1, 1, Cfg::WAVE>(va, vb, lds, lbase, t, tab);
 
   // combine: y[p] = ye + conj(W_L^p) yo, y[p+H] = ye - conj(W_L^p) yo; real rows out
   const int out_len = d.out.len;
+  if constexpr (EPI != EPI_OUT) {
+    // PCG epilogue: stage the block's 2C output rows in LDS, then update the CG vectors in
+    // one coalesced sweep (y itself never goes to HBM)
+    T* ys = reinterpret_cast<T*>(smem_raw);
+    __syncthreads();   // every group is done with its exchange image
+    int tt = t;
+    asm volatile("" : "+v"(tt));
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+      const int p = tt + TT * k;
+      const C2<T> wo = cmulc<T>(vb[k], tw_at<T, H>(tab, p));
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const C2<T> y = hh == 0 ? cadd<T>(va[k], wo) : csub<T>(va[k], wo);
+        const int pp = p + hh * H;
+        if (pvalid && pp < out_len) {
+          ys[(2 * l) * out_len + pp] = y.x;
+          if (has2) ys[(2 * l + 1) * out_len + pp] = y.y;
+        }
+      }
+    }
+    __syncthreads();
+    const int64_t g0 = (int64_t)q * d.out.q_stride + (int64_t)row0 * d.out.r_stride;
+    const T coef = reinterpret_cast<const T*>(d.cg_coef)[q];
+    T* pg = reinterpret_cast<T*>(d.cg_p) + g0;
+    T* xg = EPI == EPI_XR ? reinterpret_cast<T*>(d.cg_x) + g0 : pg;
+    T* rg = EPI == EPI_XR ? reinterpret_cast<T*>(d.cg_r) + g0 : pg;
+    T s = cg_epilogue<T, EPI, Cfg::THREADS>(ys, nrow_blk, out_len, xg, rg, pg, d.out.r_stride, coef);
+    if constexpr (EPI == EPI_XR) {   // deterministic block sum of r.r -> partial [q][rb]
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+      T* red = reinterpret_cast<T*>(tab);   // twiddles are no longer read
+      if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        T tot = 0;
+        for (int w = 0; w < Cfg::THREADS / 64; ++w) tot += red[w];
+        reinterpret_cast<T*>(d.cg_part)[(int64_t)q * nrb + rb] = tot;
+      }
+    }
+    return;
+  }
   T* out_a = reinterpret_cast<T*>(d.out.ptr) + (int64_t)q * d.out.q_stride + (int64_t)(pvalid ? 2 * rp : 0) * d.out.r_stride;
   T* out_b = out_a + d.out.r_stride;
   const T* dot_a = nullptr;
