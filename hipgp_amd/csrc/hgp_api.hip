@@ -89,6 +89,11 @@ struct hgp_plan {
   void* cg_x = nullptr;
   bool cg_active = false;
   int64_t ws_budget = (int64_t)1 << 30;
+  // 2-D operators run their RHS chunks on `nstreams` streams (the plan's own + side streams),
+  // so one chunk's compute-heavy column pass overlaps another's memory-heavy row passes
+  int nstreams = 2;
+  hipStream_t side[3] = {nullptr, nullptr, nullptr};
+  hipEvent_t ev_fork = nullptr, ev_join[3] = {nullptr, nullptr, nullptr};
 
   ~hgp_plan() {
     for (int a = 0; a < 3; ++a) {
@@ -98,6 +103,11 @@ struct hgp_plan {
     DevBuf* bufs[] = {&specK, &specI, &specR, &Dm3, &nclamp, &ws1, &ws2, &set1, &set2, &setM1, &setM2, &setC,
                       &r, &z, &p, &Ap, &part_op, &part_u, &scal, &flags, &bT, &xT};
     for (DevBuf* b : bufs) b->release();
+    for (int i = 0; i < 3; ++i) {
+      if (side[i]) (void)hipStreamDestroy(side[i]);
+      if (ev_join[i]) (void)hipEventDestroy(ev_join[i]);
+    }
+    if (ev_fork) (void)hipEventDestroy(ev_fork);
   }
 };
 
@@ -161,6 +171,16 @@ int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
 // compact half-spectrum row length of the last (real) axis: >= H+1, 64-byte aligned rows
 int64_t compact_stride(int64_t L) { return round_up(L / 2 + 1, 8); }
 
+// Side streams + fork/join events of a plan (created on first use, on the plan's device).
+int ensure_side_streams(hgp_plan* P, int n) {
+  for (int i = 0; i < n - 1 && i < 3; ++i) {
+    if (P->side[i] == nullptr) HIP_TRY(hipStreamCreateWithFlags(&P->side[i], hipStreamNonBlocking));
+    if (P->ev_join[i] == nullptr) HIP_TRY(hipEventCreateWithFlags(&P->ev_join[i], hipEventDisableTiming));
+  }
+  if (P->ev_fork == nullptr) HIP_TRY(hipEventCreateWithFlags(&P->ev_fork, hipEventDisableTiming));
+  return 0;
+}
+
 // Fused PCG epilogue of the 2-D row-inverse pass (hgp_rows.hpp EPI_XR / EPI_P): the operator
 // output y updates the CG vectors (x, r, p: row layout, nrhs x M) instead of being stored.
 struct RowEpi {
@@ -174,7 +194,7 @@ struct RowEpi {
 
 // Called between the 2-D column pass and the row-inverse pass of each RHS chunk (q0, qn):
 // computes the chunk's alpha / beta from the column pass's spectral dots.
-using MidFn = std::function<void(int64_t, int)>;
+using MidFn = std::function<void(int64_t, int, hipStream_t)>;
 
 // y = op(x) on RHS [0, nrhs); optional fused dot with `dotv` into partial[b][rn_last].
 // Every RHS is processed on its own (no two RHS share an FFT).  only_pass >= 0 runs a single
@@ -199,12 +219,24 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
     B1 = std::max(g.in[0] * g.in[1], g.out[0] * g.out[1]) * Sl;
     B2 = std::max(g.in[0], g.out[0]) * g.L[1] * Sl;
   }
+  // RHS chunks: 2-D ops spread them over NS streams, chunk j on stream (and workspace slot)
+  // j % NS; each chunk's RHS are processed entirely on its stream (no cross-stream data).
+  const int NS = (d == 2 && only_pass < 0) ? (int)std::min<int64_t>(std::max(1, P->nstreams), nrhs) : 1;
   int64_t Qc = nrhs;
   if (B1 + B2 > 0) {
     const int64_t per = (B1 + B2) * (int64_t)cs;
-    Qc = std::max<int64_t>(1, std::min<int64_t>(nrhs, P->ws_budget / per));
-    HGP_TRY(P->ws1.ensure((size_t)(B1 * Qc) * cs));
+    Qc = std::max<int64_t>(1, std::min<int64_t>((nrhs + NS - 1) / NS, P->ws_budget / (per * NS)));
+    HGP_TRY(P->ws1.ensure((size_t)(B1 * Qc * NS) * cs));
     if (B2) HGP_TRY(P->ws2.ensure((size_t)(B2 * Qc) * cs));
+  }
+  hipStream_t streams[4] = {P->stream, nullptr, nullptr, nullptr};
+  if (NS > 1) {
+    HGP_TRY(ensure_side_streams(P, NS));
+    HIP_TRY(hipEventRecord(P->ev_fork, P->stream));
+    for (int i = 1; i < NS; ++i) {
+      streams[i] = P->side[i - 1];
+      HIP_TRY(hipStreamWaitEvent(streams[i], P->ev_fork, 0));
+    }
   }
   const T* xin = reinterpret_cast<const T*>(x);
   T* yout = reinterpret_cast<T*>(y);
@@ -213,12 +245,15 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
   const int64_t rows_out = (d == 1) ? 1 : (d == 2 ? g.out[0] : g.out[0] * g.out[1]);
   const int64_t rn_last = (d == 1) ? 1 : (rows_out + 1) / 2;
 
-  for (int64_t q0 = 0; q0 < nrhs; q0 += Qc) {
+  int64_t chunk = 0;
+  for (int64_t q0 = 0; q0 < nrhs; q0 += Qc, ++chunk) {
+    const int slot = (int)(chunk % NS);
+    hipStream_t st = streams[slot];
     int pass_no = 0;
     auto run = [&](int H, int mode, int lay, PassDesc& D, int64_t lines) -> int {
       const int me = pass_no++;
       if (only_pass >= 0 && only_pass != me) return 0;
-      return launch<T>(H, mode, lay, D, lines, P->stream);
+      return launch<T>(H, mode, lay, D, lines, st);
     };
     const int qn = (int)std::min(Qc, nrhs - q0);
     const T* xi = xin + q0 * g.in_M;
@@ -235,12 +270,12 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
       D.tw = g.tw[0].ptr; D.Q = qn; D.Rn = 1; D.In = 1; D.done = done;
       HGP_TRY(run((int)(g.L[0] / 2), conv_mode, LAY_R1, D, qn));
     } else if (d == 2) {
-      C2<T>* w1 = reinterpret_cast<C2<T>*>(P->ws1.ptr);
+      C2<T>* w1 = reinterpret_cast<C2<T>*>(P->ws1.ptr) + (int64_t)slot * Qc * B1;
       const int64_t H1 = g.L[1] / 2;
       auto run_rowt = [&](int inv, PassDesc& D, int epi_mode) -> int {
         const int me = pass_no++;
         if (only_pass >= 0 && only_pass != me) return 0;
-        hipError_t e = launch_rowt<T>((int)H1, inv, epi_mode, D, P->stream);
+        hipError_t e = launch_rowt<T>((int)H1, inv, epi_mode, D, st);
         if (e != hipSuccess) return fail(HGP_E_HIP, std::string("row pass launch: ") + hipGetErrorString(e));
         return 0;
       };
@@ -261,7 +296,7 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
         Bd.spart_mid = (int)(H1 / 2);
       }
       HGP_TRY(run((int)(g.L[0] / 2), conv_mode, LAY_CONTIG, Bd, (int64_t)qn * Bd.Rn));
-      if (mid != nullptr) (*mid)(q0, qn);
+      if (mid != nullptr) (*mid)(q0, qn, st);
       // C: INV along axis 1: column-major tiles -> row pairs, crop, fused dot or PCG update
       PassDesc Cd = base_desc();
       Cd.in = View{w1, B1, S0, 1, 0};
@@ -317,6 +352,10 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
       P5.tw = g.tw[2].ptr; P5.Q = qn; P5.Rn = (int)((rows_out + 1) / 2); P5.nrows = (int)rows_out; P5.done = done;
       HGP_TRY(run((int)H2, PASS_INV, LAY_RP, P5, (int64_t)qn * P5.Rn));
     }
+  }
+  for (int i = 1; i < NS; ++i) {   // join: later work on the plan's stream sees every chunk
+    HIP_TRY(hipEventRecord(P->ev_join[i - 1], streams[i]));
+    HIP_TRY(hipStreamWaitEvent(P->stream, P->ev_join[i - 1], 0));
   }
   return 0;
 }
@@ -593,15 +632,15 @@ int pcg_step_t(hgp_plan* P, double tol) {
     // whose epilogue does p = z + beta p (z never stored).  Order and semantics of cg.py:63-78.
     const int nps = spec_np(P), npx = xr_np<T>(P);
     T* part_s = reinterpret_cast<T*>(P->part_op.ptr);
-    const MidFn mid_alpha = [&](int64_t q0, int qn) {
-      cg_alpha<T>(part_s + q0 * nps, nps, qn, rs + q0, alpha + q0, done, s);
+    const MidFn mid_alpha = [&](int64_t q0, int qn, hipStream_t cs) {
+      cg_alpha<T>(part_s + q0 * nps, nps, qn, rs + q0, alpha + q0, done, cs);
     };
     const RowEpi exr{EPI_XR, P->r.ptr, P->cg_x, P->p.ptr, alpha, P->part_u.ptr};
     HGP_TRY(run_op<T>(P, HGP_OP_K, P->p.ptr, P->Ap.ptr, nrhs, nullptr, nullptr, done, -1, part_s, &exr, &mid_alpha));
     cg_check<T>(P->part_u.ptr, npx, (int)nrhs, tol, rnew, done, iters, s);
     if (P->cg_precond) {
-      const MidFn mid_beta = [&](int64_t q0, int qn) {
-        cg_beta<T>(part_s + q0 * nps, nps, qn, rs + q0, beta + q0, done, s);
+      const MidFn mid_beta = [&](int64_t q0, int qn, hipStream_t cs) {
+        cg_beta<T>(part_s + q0 * nps, nps, qn, rs + q0, beta + q0, done, cs);
       };
       const RowEpi ep{EPI_P, P->r.ptr, P->cg_x, P->p.ptr, beta, nullptr};
       HGP_TRY(run_op<T>(P, HGP_OP_CINV, P->r.ptr, P->Ap.ptr, nrhs, nullptr, nullptr, done, -1, part_s, &ep, &mid_beta));
@@ -691,6 +730,8 @@ int hgp_plan_create(int device, int ndim, const int64_t* m, int dtype, int64_t m
   }
   const char* wb = std::getenv("HGP_WS_MB");
   if (wb) P->ws_budget = (int64_t)std::atoll(wb) << 20;
+  const char* ns = std::getenv("HGP_STREAMS");
+  if (ns) P->nstreams = std::max(1, std::min(4, std::atoi(ns)));
   int rc = 0;
   for (int a = 0; a < d && rc == 0; ++a) {
     if (dtype == HGP_F64) {

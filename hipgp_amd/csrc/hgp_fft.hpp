@@ -20,6 +20,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace hgp {
 
 template <typename T> struct cx;
@@ -290,11 +292,67 @@ __device__ __forceinline__ void fft_bfly(const C2<T> (&v)[P], C2<T> (&a)[P], int
   }
 }
 
+// The exchange before the last stage of the one-wave 1024-point fp32 transform (radices
+// 16, 16, 4; TT = 64 threads) needs no LDS.  Thread t = (row rho = t>>4, column c = t&15)
+// reads positions t + 64k; stage 1 (NS = 16, one radix-16 butterfly per thread) wrote output
+// r' of thread t' to 256 (t'>>4) + 16 r' + (t'&15).  So destination (lane (rho, c), register
+// k = 4 al + be) <- source (lane (al, c), register 4 be + rho): the lane-row bits (lane bits
+// 4, 5) trade places with the register's low bits, and the register's two 2-bit fields swap.
+// v_permlane16_swap exchanges lane bit 4 with the pairing of two registers (odd rows of the
+// first <-> even rows of the second), v_permlane32_swap lane bit 5 (upper half <-> lower
+// half); the field swap is a renaming.  32 cross-lane moves instead of 16 LDS writes + 16
+// reads and their round-trip latency.
+template <typename T, int H, int P, int S>
+struct PermlaneXchg {
+  using St = Stages<H, P>;
+#ifdef HGP_PERMLANE_XCHG
+  static constexpr bool enabled = true;
+#else
+  static constexpr bool enabled = false;   // measured slower than the LDS exchange
+#endif
+  static constexpr bool value = enabled && std::is_same<T, float>::value && H == 1024 && P == 16 && St::count() == 3 &&
+                                S == 1 && St::radix(1) == 16 && St::ns(1) == 16 && St::radix(2) == 4;
+};
+
+__device__ __forceinline__ void pl16_swap(float& a, float& b) {
+  auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  a = __uint_as_float(r[0]);
+  b = __uint_as_float(r[1]);
+}
+__device__ __forceinline__ void pl32_swap(float& a, float& b) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  a = __uint_as_float(r[0]);
+  b = __uint_as_float(r[1]);
+}
+
+template <int P>
+__device__ __forceinline__ void fft_xchg_permlane(C2<float> (&a)[P], C2<float> (&v)[P]) {
+#pragma unroll
+  for (int r = 0; r < 16; r += 2) {          // lane bit 4 <-> register bit 0
+    pl16_swap(a[r].x, a[r + 1].x);
+    pl16_swap(a[r].y, a[r + 1].y);
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {             // lane bit 5 <-> register bit 1
+    if (r & 2) continue;
+    pl32_swap(a[r].x, a[r + 2].x);
+    pl32_swap(a[r].y, a[r + 2].y);
+  }
+#pragma unroll
+  for (int al = 0; al < 4; ++al)
+#pragma unroll
+    for (int be = 0; be < 4; ++be) v[4 * al + be] = a[4 * be + al];
+}
+
 // exchange after stage S: write a (stage-S outputs), read this thread's stage-(S+1) inputs
 template <typename T, int H, int P, int STRIDE, bool WAVE, int S>
-__device__ __forceinline__ void fft_xchg(const C2<T> (&a)[P], C2<T> (&v)[P], C2<T>* lds, int base, int t) {
+__device__ __forceinline__ void fft_xchg(C2<T> (&a)[P], C2<T> (&v)[P], C2<T>* lds, int base, int t) {
   using St = Stages<H, P>;
   constexpr int R = St::radix(S), NS = St::ns(S), TT = H / P, NB = P / R;
+  if constexpr (PermlaneXchg<T, H, P, S>::value && STRIDE == 1 && WAVE) {
+    fft_xchg_permlane<P>(a, v);
+    return;
+  }
   const int idxD = (t / NS) * NS * R + (t & (NS - 1));
   const int wb = base + idxD * STRIDE;
   const int pwb = lds_phys(wb);
@@ -307,8 +365,19 @@ __device__ __forceinline__ void fft_xchg(const C2<T> (&a)[P], C2<T> (&v)[P], C2<
   xsync<WAVE>();
   const int rb = base + t * STRIDE;
   const int prb = lds_phys(rb);
+#ifdef HGP_LDS_NOREAD2
+  // one ds_read_b64 per value (2 LDS cycles) instead of the ds_read2_b64 pairs (8 cycles) the
+  // load/store optimiser forms from a shared base: every read gets its own address register
+#pragma unroll
+  for (int k = 0; k < P; ++k) {
+    int a = lds_at(prb, rb, TT * k * STRIDE, false);
+    asm volatile("" : "+v"(a));
+    v[k] = lds[a];
+  }
+#else
 #pragma unroll
   for (int k = 0; k < P; ++k) v[k] = lds[lds_at(prb, rb, TT * k * STRIDE, false)];
+#endif
 }
 
 // last stage's outputs back to natural register order

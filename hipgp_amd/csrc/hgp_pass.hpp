@@ -390,11 +390,16 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
       // the line's real spectrum, loaded after the forward transforms (no registers held across
       // them); L2-resident: every line of a block shares it (RHS-fastest map, XCD-grouped)
       T sre1[P];
+#ifdef HGP_EXP_NOSPEC   // timing experiment only (wrong results): no spectrum loads
+#pragma unroll
+      for (int k = 0; k < P; ++k) { sre[k] = (T)1; sre1[k] = (T)1; }
+#else
 #pragma unroll
       for (int k = 0; k < P; ++k) {
         sre[k] = sb[so + TT * k * sp];
         sre1[k] = sb[so + (H + TT * k) * sp];
       }
+#endif
       if (d.spart != nullptr) {   // uniform: spectral dot sum_k S_k |X_k|^2 of this line
 #pragma unroll
         for (int k = 0; k < P; ++k) {

@@ -223,14 +223,16 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
   const int nrow_blk = d.nrows - row0 < 2 * C ? d.nrows - row0 : 2 * C;
 
   C2<T> va[P], vb[P];
-  auto do_half = [&](auto half_c, C2<T>(&v)[P]) {
+  // Tiles of the two frequency halves (compact columns [0, H/2] and [H/2+1, H]) go through the
+  // same LDS area one after the other; the odd half's global loads are issued before the even
+  // half is rebuilt from LDS, so its memory latency overlaps that work.
+  constexpr int ITER = ((H / 2 + 1) * 2 * C + Cfg::THREADS - 1) / Cfg::THREADS;
+  C2<T> buf[ITER];
+  auto load_tile = [&](auto half_c) {
     constexpr int half = decltype(half_c)::value;
     constexpr int NCOL = (half == 0) ? H / 2 + 1 : H / 2;
     constexpr int C0 = (half == 0) ? 0 : H / 2 + 1;
     constexpr int NE = NCOL * 2 * C;
-    __syncthreads();   // previous users of the area are done (twiddles staged, first half)
-    constexpr int ITER = (NE + Cfg::THREADS - 1) / Cfg::THREADS;
-    C2<T> buf[ITER];
 #pragma unroll
     for (int j = 0; j < ITER; ++j) {         // all global loads in flight at once
       const int e = threadIdx.x + j * Cfg::THREADS;
@@ -242,6 +244,11 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
       if (row >= nrow_blk) val = mk<T>(0, 0);
       buf[j] = val;
     }
+  };
+  auto park_tile = [&](auto half_c) {
+    constexpr int half = decltype(half_c)::value;
+    constexpr int NCOL = (half == 0) ? H / 2 + 1 : H / 2;
+    constexpr int NE = NCOL * 2 * C;
 #pragma unroll
     for (int j = 0; j < ITER; ++j) {
       const int e = threadIdx.x + j * Cfg::THREADS;
@@ -249,8 +256,10 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
       const int row = e - col * (2 * C);
       if (e < NE) lds[col * PITCH + row] = buf[j];
     }
-    __syncthreads();
-    // Hermitian rebuild Z = A + iB of the pair at frequency half `half`, position p
+  };
+  // Hermitian rebuild Z = A + iB of the pair at frequency half `half`, position p
+  auto rebuild = [&](auto half_c, C2<T>(&v)[P]) {
+    constexpr int half = decltype(half_c)::value;
 #pragma unroll
     for (int k = 0; k < P; ++k) {
       const int p = t + TT * k;
@@ -266,8 +275,18 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
       v[k] = mk<T>(A.x - B.y, A.y + B.x);
     }
   };
-  do_half(std::integral_constant<int, 0>{}, va);
-  do_half(std::integral_constant<int, 1>{}, vb);   // (starts with a barrier: even tile consumed)
+  using H0 = std::integral_constant<int, 0>;
+  using H1 = std::integral_constant<int, 1>;
+  load_tile(H0{});
+  __syncthreads();   // twiddles staged (the tile area is free)
+  park_tile(H0{});
+  __syncthreads();
+  load_tile(H1{});   // in flight during the even rebuild
+  rebuild(H0{}, va);
+  __syncthreads();   // even tile consumed
+  park_tile(H1{});
+  __syncthreads();
+  rebuild(H1{}, vb);
   __syncthreads();   // tile consumed: the FFT exchange images overlay it
   fft_line2<T, H, P, +1, 1, Cfg::WAVE>(va, vb, lds, lbase, t, tab);
 

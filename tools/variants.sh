@@ -1,23 +1,27 @@
 #!/bin/bash
-# Block-shape variants of libhipgp for tuning: build here (BUILD=1), time on the GPU box.
+# Compile-time variants of libhipgp for tuning: build here (BUILD=1), time on the GPU box.
+#   VARS="a: n:-DHGP_LDS_NOREAD2"  (name:flags, space separated; flags use ',' for spaces)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-declare -A V
-V[a]=""
-V[b]="-DHGP_CONTIG_THREADS=256"
-V[c]="-DHGP_CONTIG_THREADS=256 -DHGP_ROWT_PAIRS=4"
-V[d]="-DHGP_ROWT_PAIRS=4"
+VARS=${VARS:-"a: n:-DHGP_LDS_NOREAD2"}
 if [ -n "$BUILD" ]; then
-  for k in "${!V[@]}"; do make -s -C hipgp_amd/csrc VARIANT=$k VFLAGS="${V[$k]}" -j4 & done; wait
+  for v in $VARS; do
+    k=${v%%:*}; f=${v#*:}; f=${f//,/ }
+    make -s -C hipgp_amd/csrc VARIANT=$k VFLAGS="$f" -j8 > /tmp/variant_$k.log 2>&1 &
+  done
+  wait
+  ls -la hipgp_amd/libhipgp_*.so
   exit 0
 fi
 mkdir -p gpurun_out
-for k in $(echo "${!V[@]}" | tr ' ' '\n' | sort); do
-  HGP_LIB=$PWD/hipgp_amd/libhipgp_$k.so timeout -k 10 120 python bench.py --no-cpu-baseline --steps 20 --warmup 5 --pcg-reps 2 ${BENCH_ARGS:-} > gpurun_out/var_$k.json 2> gpurun_out/var_$k.err || { echo "$k failed"; tail -5 gpurun_out/var_$k.err; exit 1; }
-  python - "$k" "${V[$k]}" <<'PY'
+for v in $VARS; do
+  k=${v%%:*}
+  HGP_LIB=$PWD/hipgp_amd/libhipgp_$k.so timeout -k 10 120 python bench.py --no-cpu-baseline --steps 20 --warmup 5 --pcg-reps 3 ${BENCH_ARGS:-} > gpurun_out/var_$k.json 2> gpurun_out/var_$k.err || { echo "$k failed"; tail -5 gpurun_out/var_$k.err; exit 1; }
+  python3 - "$v" <<'PY'
 import json, sys
-d = json.loads(open(f"gpurun_out/var_{sys.argv[1]}.json").read().strip().splitlines()[-1])
+k = sys.argv[1].split(":")[0]
+d = json.loads(open(f"gpurun_out/var_{k}.json").read().strip().splitlines()[-1])
 r = d["roofline"]
-print(sys.argv[1], sys.argv[2], "| value", round(d["value"]), "frac", round(r["frac"], 3), "pcg_ms", round(d["pcg_wall_clock_ms"], 2),
-      "passes", [(p["ms"], p["gbs"]) for p in r["passes"]])
+print(sys.argv[1], "| value", round(d["value"]), "frac", round(r["frac"], 3), "pcg_ms", round(d["pcg_wall_clock_ms"], 2),
+      "passes", [(p["ms"], p["gbs"]) for p in r["passes"]], flush=True)
 PY
 done
