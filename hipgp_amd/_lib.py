@@ -25,8 +25,9 @@ EXPORTS = (
     "hgp_pcg_solve", "hgp_pcg_begin", "hgp_pcg_step", "hgp_get_spectrum", "hgp_rowdot",
     "hgp_plan_info", "hgp_plan_destroy", "hgp_last_error", "hgp_version",
     "hgp_toeplitz_apply_pass", "hgp_op_pass_count", "hgp_pcg_rnorm2", "hgp_kuf_grid",
+    "hgp_kuf_semi_mc", "hgp_kuf_semi_sqexp", "hgp_knn_doubly_diag",
 )
-KERN_SQEXP, KERN_MATERN12, KERN_MATERN32, KERN_MATERN52 = 0, 1, 2, 3
+KERN_SQEXP, KERN_MATERN12, KERN_MATERN32, KERN_MATERN52, KERN_GNEITING = 0, 1, 2, 3, 4
 
 
 class HipgpError(RuntimeError):
@@ -64,6 +65,9 @@ def lib():
         "hgp_op_pass_count": (i32, [vp]),
         "hgp_pcg_rnorm2": (i32, [vp, vp]),
         "hgp_kuf_grid": (i32, [i32, i32, i32, pi64, ctypes.POINTER(vp), vp, i64, dbl, dbl, vp, vp]),
+        "hgp_kuf_semi_mc": (i32, [i32, i32, dbl, i32, pi64, ctypes.POINTER(vp), vp, i64, dbl, dbl, i32, vp, vp, vp]),
+        "hgp_kuf_semi_sqexp": (i32, [i32, i32, pi64, ctypes.POINTER(vp), vp, i64, dbl, dbl, vp, vp]),
+        "hgp_knn_doubly_diag": (i32, [i32, i32, vp, i64, dbl, dbl, vp, i32, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

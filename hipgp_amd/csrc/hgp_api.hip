@@ -899,6 +899,52 @@ int hgp_kuf_grid(int dtype, int kind, int ndim, const int64_t* m, const void* co
   return 0;
 }
 
+static int check_grid_args(int dtype, int ndim, const int64_t* m, const void* const* grids, const void* x,
+                           int64_t nobs, const void* out) {
+  if (ndim < 1 || ndim > 3 || m == nullptr || grids == nullptr) return fail(HGP_E_ARG, "ndim must be 1..3, m/grids non-null");
+  if (dtype != HGP_F32 && dtype != HGP_F64) return fail(HGP_E_ARG, "dtype must be HGP_F32 or HGP_F64");
+  if (nobs < 0 || (nobs > 0 && (x == nullptr || out == nullptr))) return fail(HGP_E_ARG, "bad x/out/nobs");
+  for (int a = 0; a < ndim; ++a)
+    if (m[a] < 1 || grids[a] == nullptr) return fail(HGP_E_ARG, "grid sizes must be >= 1 with non-null grids");
+  return 0;
+}
+
+int hgp_kuf_semi_mc(int dtype, int kind, double kparam, int ndim, const int64_t* m, const void* const* grids,
+                    const void* x, int64_t nobs, double sig2, double ell, int npts, const void* u, void* out,
+                    void* hip_stream) {
+  HGP_TRY(check_grid_args(dtype, ndim, m, grids, x, nobs, out));
+  if (kind < HGP_KERN_SQEXP || kind > HGP_KERN_GNEITING) return fail(HGP_E_ARG, "bad kernel kind");
+  if (npts < 1 || npts > 1024) return fail(HGP_E_ARG, "npts must be in [1, 1024]");
+  if (u == nullptr) return fail(HGP_E_ARG, "u (the device offset draw) is null");
+  if (nobs == 0) return 0;
+  hipError_t e = kuf_semi(dtype, kind, kparam, ndim, m, grids, x, nobs, sig2, ell, npts, u, out,
+                          reinterpret_cast<hipStream_t>(hip_stream));
+  if (e != hipSuccess) return fail(HGP_E_HIP, std::string("hgp_kuf_semi_mc: ") + hipGetErrorString(e));
+  return 0;
+}
+
+int hgp_kuf_semi_sqexp(int dtype, int ndim, const int64_t* m, const void* const* grids, const void* x, int64_t nobs,
+                       double sig2, double ell, void* out, void* hip_stream) {
+  HGP_TRY(check_grid_args(dtype, ndim, m, grids, x, nobs, out));
+  if (nobs == 0) return 0;
+  hipError_t e = kuf_semi(dtype, HGP_KERN_SQEXP, 1.0, ndim, m, grids, x, nobs, sig2, ell, 0, nullptr, out,
+                          reinterpret_cast<hipStream_t>(hip_stream));
+  if (e != hipSuccess) return fail(HGP_E_HIP, std::string("hgp_kuf_semi_sqexp: ") + hipGetErrorString(e));
+  return 0;
+}
+
+int hgp_knn_doubly_diag(int dtype, int ndim, const void* x, int64_t nobs, double sig2, double ell, const void* table,
+                        int N, void* out, void* hip_stream) {
+  if (ndim < 1 || ndim > 3) return fail(HGP_E_ARG, "ndim must be 1..3");
+  if (dtype != HGP_F32 && dtype != HGP_F64) return fail(HGP_E_ARG, "dtype must be HGP_F32 or HGP_F64");
+  if (N < 2 || table == nullptr) return fail(HGP_E_ARG, "table needs N >= 2 entries");
+  if (nobs < 0 || (nobs > 0 && (x == nullptr || out == nullptr))) return fail(HGP_E_ARG, "bad x/out/nobs");
+  if (nobs == 0) return 0;
+  hipError_t e = doubly_diag(dtype, ndim, x, nobs, sig2, ell, table, N, out, reinterpret_cast<hipStream_t>(hip_stream));
+  if (e != hipSuccess) return fail(HGP_E_HIP, std::string("hgp_knn_doubly_diag: ") + hipGetErrorString(e));
+  return 0;
+}
+
 int hgp_plan_info(const hgp_plan* plan, int64_t* M, int64_t* Mprime, int64_t* L_K, int64_t* L_R) {
   HGP_TRY(check_plan(plan));
   if (M) *M = plan->M;

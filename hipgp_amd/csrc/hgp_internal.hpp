@@ -40,6 +40,11 @@ template <typename T> void expand_spec(const double* src, void* out, const GridD
 // dense grid cross covariance (hgp_kuf.hip)
 hipError_t kuf_grid(int dtype, int kind, int ndim, const int64_t* m, const void* const* grids, const void* x,
                     int64_t nobs, double sig2, double ell, void* out, hipStream_t s);
+hipError_t kuf_semi(int dtype, int kind, double kp, int ndim, const int64_t* m, const void* const* grids,
+                    const void* x, int64_t nobs, double sig2, double ell, int npts, const void* u, void* out,
+                    hipStream_t s);
+hipError_t doubly_diag(int dtype, int ndim, const void* x, int64_t nobs, double sig2, double ell, const void* tab,
+                       int N, void* out, hipStream_t s);
 hipError_t kuf_semi_grid(int dtype, int kind, int method, int ndim, const int64_t* m, const void* const* grids,
                          const void* x, int64_t nobs, double sig2, double ell, const void* nodes,
                          const void* weights, int npts, void* out, hipStream_t s);

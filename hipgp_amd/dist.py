@@ -64,14 +64,19 @@ def sharded_compute_kn(model, Knm_local, maxiter_cg=20, tol=1e-8, exact_break=Fa
 
 
 def sharded_elbo_and_grad(model, xbatch, ybatch, noise_std_batch=None, maxiter_cg=20, tol=1e-8,
-                          exact_break=False, group=None, compute_kn=None):
+                          exact_break=False, group=None, compute_kn=None, integrated_obs=False,
+                          semi_integrated_estimator="analytic", semi_integrated_samps=10):
     """`MeanFieldToeplitzGP.elbo_and_grad` with the minibatch sharded by rows over the ranks
     of `group`; every rank passes the SAME full minibatch and gets the same ELBO and grads.
-    `compute_kn(model, Knm_local)` may be injected (tests run the host logic on CPU)."""
+    `compute_kn(model, Knm_local)` may be injected (tests run the host logic on CPU).
+    Line-integral observations ("mc-biased") draw the reference's one torch.rand(1) offset per
+    rank: ranks seeded alike draw the same offset, as the single-process reference does."""
     ws = dist.get_world_size(group) if dist.is_initialized() else 1
     rk = dist.get_rank(group) if dist.is_initialized() else 0
     sl = rhs_shard(xbatch.shape[0], ws, rk)
-    Knm, Knn_diag = model._make_grams(xbatch[sl])
+    Knm, Knn_diag = model._make_grams(xbatch[sl], integrated_obs=integrated_obs,
+                                      semi_integrated_estimator=semi_integrated_estimator,
+                                      semi_integrated_samps=semi_integrated_samps)
     if compute_kn is None:
         kn = sharded_compute_kn(model, Knm, maxiter_cg=maxiter_cg, tol=tol, exact_break=exact_break, group=group)
     else:

@@ -54,7 +54,7 @@ class SviGP(nn.Module):
                     semi_integrated_samps=10):
         params = self.get_kernel_params()
         if integrated_obs:
-            raise NotImplementedError("integrated (line-integral) observations: SURVEY §8(f) row 2")
+            return self._make_integrated_grams(xbatch, params, semi_integrated_estimator, semi_integrated_samps)
         Knm = None
         if getattr(self, "xgrids", None) is not None:
             from hipgp_amd.kuf import kuf_grid
@@ -62,6 +62,26 @@ class SviGP(nn.Module):
         if Knm is None:
             Knm = self.kernel(xbatch, self.xinduce, params)
         return Knm, self.kernel.diag(xbatch, params)
+
+    def _make_integrated_grams(self, xbatch, params, estimator, samps):
+        """Line-integral observations, `svi_gp.py:55-69`: Knm by the analytic SqExp integral or
+        the biased MC estimator (fused HIP kernels on the grid, `hipgp_amd.kuf`), Knn_diag by the
+        doubly-integrated table (`hgp_knn_doubly_diag`)."""
+        from hipgp_amd import kuf
+        grids = getattr(self, "xgrids", None)
+        if estimator == "analytic":
+            Knm = kuf.kuf_semi_sqexp(self.kernel, grids, xbatch, params) if grids is not None else None
+            if Knm is None:
+                Knm = self.kernel.k_semi(self.xinduce, xbatch, params).transpose(0, 1)
+        elif estimator == "mc-biased":
+            Knm = kuf.kuf_semi_mc(self.kernel, grids, xbatch, params, samps) if grids is not None else None
+            if Knm is None:
+                Knm = self.kernel.k_semi_mc(self.xinduce, xbatch, params, npts=samps).transpose(0, 1)
+        elif estimator == "numerical":
+            Knm = self.kernel.k_semi_num(self.xinduce, xbatch, params).transpose(0, 1)
+        else:
+            raise NotImplementedError
+        return Knm, self.kernel.k_doubly_diag(xbatch, params)
 
     def batch_predict(self, x, batch_size, verbose=True, **kwargs):
         nb = int(np.ceil(len(x) / batch_size))
@@ -179,7 +199,9 @@ class ToeplitzInducingGP(SviGP):
         if qm is None or qS is None:
             qm, qS = self.standard_variational_params()
         if Knm is None or Knn_diag is None:
-            Knm, Knn_diag = self._make_grams(xbatch, integrated_obs=integrated_obs)
+            Knm, Knn_diag = self._make_grams(xbatch, integrated_obs=integrated_obs,
+                                             semi_integrated_estimator=semi_integrated_estimator or "analytic",
+                                             semi_integrated_samps=semi_integrated_samps or 10)
         if kn is None:
             kn = self.compute_kn(Knm, maxiter_cg=maxiter_cg, Kmm=Kmm)
         ivar, log_sd = self.noise_terms(noise_std_batch)
@@ -196,7 +218,9 @@ class ToeplitzInducingGP(SviGP):
              semi_integrated_estimator="analytic", semi_integrated_samps=10, Kmm=None,
              print_debug_info=False):
         """mean_n a_n - KL/N  (`hipgp.py:160-192`)."""
-        Knm, Knn_diag = self._make_grams(xbatch, integrated_obs=integrated_obs)
+        Knm, Knn_diag = self._make_grams(xbatch, integrated_obs=integrated_obs,
+                                         semi_integrated_estimator=semi_integrated_estimator,
+                                         semi_integrated_samps=semi_integrated_samps)
         kn = self.compute_kn(Knm, maxiter_cg=maxiter_cg, Kmm=Kmm)
         qm, qS = self.standard_variational_params()
         an = self.compute_batch_an(xbatch, ybatch, noise_std_batch, qm=qm, qS=qS, Knm=Knm,
@@ -210,7 +234,9 @@ class ToeplitzInducingGP(SviGP):
         (`hipgp.py:194-276`)."""
         assert self.parameterization == 'expectation-family', \
             "need parameterization=expectation-family when performing natural gradient descent"
-        Knm, Knn_diag = self._make_grams(xbatch, integrated_obs=integrated_obs)
+        Knm, Knn_diag = self._make_grams(xbatch, integrated_obs=integrated_obs,
+                                         semi_integrated_estimator=semi_integrated_estimator,
+                                         semi_integrated_samps=semi_integrated_samps)
         kn = self.compute_kn(Knm, maxiter_cg=maxiter_cg, Kmm=Kmm)
         stats = self.batch_stats(kn, ybatch, Knn_diag, noise_std_batch)
         return self.apply_stats(stats, xbatch.shape[0])
@@ -219,7 +245,9 @@ class ToeplitzInducingGP(SviGP):
                 semi_integrated_samps=10, maxiter_cg=50, Kmm=None):
         """E[f(x)] and sd[f(x)] (`hipgp.py:416-446`), returned on the CPU."""
         x = x.to(self.xgrids[0].device)
-        Knm, Knn_diag = self._make_grams(x, integrated_obs=integrated_obs)
+        Knm, Knn_diag = self._make_grams(x, integrated_obs=integrated_obs,
+                                         semi_integrated_estimator=semi_integrated_estimator,
+                                         semi_integrated_samps=semi_integrated_samps)
         kn = self.compute_kn(Knm, maxiter_cg=maxiter_cg, Kmm=Kmm)
         qm, qS = self.standard_variational_params()
         mu = kn.matmul(qm)

@@ -32,7 +32,8 @@ enum { HGP_F32 = 0, HGP_F64 = 1 };
 enum { HGP_OP_K = 0, HGP_OP_CINV = 1, HGP_OP_RT = 2, HGP_OP_R = 3 };
 enum { HGP_SPEC_D = 0, HGP_SPEC_DSQRT = 1, HGP_SPEC_DI = 2 };
 enum { HGP_LAYOUT_ROWS = 0, HGP_LAYOUT_COLS = 1 };
-enum { HGP_KERN_SQEXP = 0, HGP_KERN_MATERN12 = 1, HGP_KERN_MATERN32 = 2, HGP_KERN_MATERN52 = 3 };
+enum { HGP_KERN_SQEXP = 0, HGP_KERN_MATERN12 = 1, HGP_KERN_MATERN32 = 2, HGP_KERN_MATERN52 = 3,
+       HGP_KERN_GNEITING = 4 };
 enum {
   HGP_OK = 0, HGP_E_ARG = -1, HGP_E_HIP = -2, HGP_E_STATE = -3, HGP_E_UNSUPPORTED = -4,
   HGP_E_OOM = -5
@@ -119,6 +120,31 @@ int hgp_rowdot(int dtype, const void* a, const void* c, void* out, int64_t nrhs,
 int hgp_kuf_grid(int dtype, int kind, int ndim, const int64_t* m, const void* const* grids,
                  const void* x, int64_t nobs, double sig2, double ell, void* out,
                  void* hip_stream);
+
+/* Line-integral ("semi-integrated") cross covariance on a gridded mesh, SURVEY §8(f) row 2
+ * (the inter-domain observations of config 5: observation n is the segment 0 -> x_n):
+ *   out[n, j] = |x_n| * mean_{a < npts} k(u_j, alpha_a x_n),  alpha_a = a/npts + u[0]/npts
+ * = Kernel.k_semi_mc (kernels.py:19-39) as svi_gp._make_grams uses it (svi_gp.py:61-64,
+ * transposed).  u: device scalar holding the reference's single torch.rand(1) draw, so the
+ * caller consumes the RNG exactly as the reference does.  kind: any HGP_KERN_*; kparam is
+ * Gneiting's alpha (ignored otherwise).  1 <= npts <= 1024.  Layout as hgp_kuf_grid. */
+int hgp_kuf_semi_mc(int dtype, int kind, double kparam, int ndim, const int64_t* m,
+                    const void* const* grids, const void* x, int64_t nobs, double sig2,
+                    double ell, int npts, const void* u, void* out, void* hip_stream);
+
+/* Analytic SqExp line integral, SqExp.k_semi -> semi_integrated_sqe (kernels.py:80-85,
+ * 223-237), replacing svi_gp.py:58-59:  out[n, j] = |x_n| int_0^1 k(u_j, a x_n) da
+ * (NaN for |x_n| = 0, as the reference).  Layout as hgp_kuf_grid. */
+int hgp_kuf_semi_sqexp(int dtype, int ndim, const int64_t* m, const void* const* grids,
+                       const void* x, int64_t nobs, double sig2, double ell, void* out,
+                       void* hip_stream);
+
+/* Doubly-integrated diagonal Knn_diag by table interpolation,
+ * KernelDoublyDiagInterpolator.forward (kernels.py:200-220): table = device array of 3*N
+ * values in dtype (distance grid, knn, slopes: the reference's float32 table), x: (nobs,
+ * ndim), out: (nobs,). */
+int hgp_knn_doubly_diag(int dtype, int ndim, const void* x, int64_t nobs, double sig2, double ell,
+                        const void* table, int N, void* out, void* hip_stream);
 
 /* Sizes of a plan: M, M' and the padded FFT lengths per axis (K-type and R-type ops). */
 int hgp_plan_info(const hgp_plan* plan, int64_t* M, int64_t* Mprime, int64_t* L_K,

@@ -47,7 +47,82 @@ def kernel_eval(kind, x, y, params, nu=None):
         else:
             raise ValueError(nu)
         return (sig2 * k).astype(x.dtype)
+    if kind == "gneiting":          # `kernels.py:108-117` (alpha = nu argument)
+        alpha = 1. if nu is None else nu
+        t = np.sqrt(np.sum(((x[:, None, :] - y[None, :, :]) / ell) ** 2, axis=-1))
+        c = (1 - t) * np.cos(np.pi * t) + (1 / np.pi) * np.sin(np.pi * t)
+        c = (1 + t ** alpha) ** (-3) * c
+        c[t > 1.] = 0.
+        return (sig2 * c).astype(x.dtype)
     raise ValueError(kind)
+
+
+# --------------------------------------------------------------------------------------
+# line-integral (semi-integrated) cross covariance, SURVEY §8(f) row 2
+# --------------------------------------------------------------------------------------
+def k_semi_mc(kind, xinduce, xint, params, npts, u, nu=None):
+    """`Kernel.k_semi_mc` `kernels.py:19-39`, transposed as `svi_gp._make_grams` uses it
+    (`svi_gp.py:61-64`): Knm[n, m] = |x_n| * mean_j k(u_m, alpha_j x_n),
+    alpha_j = j/npts + u/npts with u the single torch.rand(1) draw (passed explicitly)."""
+    dt = xint.dtype
+    alphas = np.arange(npts, dtype=dt) / dt.type(npts) + dt.type(u) * dt.type(1. / npts)
+    xg = (xint[:, None, :] * alphas[None, :, None]).reshape(-1, xint.shape[1])
+    K = kernel_eval(kind, xinduce, xg, params, nu=nu).reshape(xinduce.shape[0], xint.shape[0], npts)
+    dists = np.sqrt(np.sum(xint ** 2, axis=-1))
+    return (np.mean(K, axis=-1) * dists[None, :]).T.astype(dt)
+
+
+def _normal_cdf(x, loc, scale):      # `ziggy/misc/stats.py:74-76`
+    from scipy.special import erf
+    return .5 * (1. + erf((x - loc) / (scale * np.sqrt(2))))
+
+
+def k_semi_sqexp(xinduce, xint, params):
+    """`SqExp.k_semi` `kernels.py:80-85` -> `semi_integrated_sqe` `kernels.py:223-237`
+    (integral of k(u, a x) over a in [0, 1] times |x|), returned as (nobs, M)."""
+    sig2, ell = params
+    dt = xint.dtype
+    D = xint.shape[1]
+    Sinv = (1. / (ell ** 2)) * np.eye(D, dtype=dt)
+    xdists = np.sqrt(np.sum(xint * xint, axis=-1))
+    xi_S = xint @ Sinv
+    a = np.sum(xi_S * xint, axis=-1)
+    b = xi_S @ xinduce.T
+    c = np.sum((xinduce @ Sinv) * xinduce, axis=-1)
+    scale = np.sqrt(1 / a[:, None])
+    loc = b / a[:, None]
+    coef = sig2 * np.exp((b ** 2) / (2 * a[:, None]) - c[None, :] / 2) * np.sqrt(2 * np.pi) * scale
+    return (coef * (_normal_cdf(1, loc, scale) - _normal_cdf(0, loc, scale)) * xdists[:, None]).astype(dt)
+
+
+def doubly_diag_table(kind, N=50, dmax=5., nu=None):
+    """`KernelDoublyDiagInterpolator.__init__` `kernels.py:172-198`: knn(d) = |x|^2 *
+    int_0^1 int_0^1 k(a x, a' x) da da' at x = (d, 0), kernel params (1, 1), by the same
+    scipy dblquad tolerances as `doubly_integrated_diag` `kernels.py:266-289`; stored as
+    float32 (`torch.Tensor(...)`) before the cast to the model dtype, as the reference."""
+    from scipy import integrate
+    dgrid = np.linspace(0, dmax, N)
+    knn = np.zeros(N)
+    for n, d in enumerate(dgrid):
+        xn = np.array([d, 0.])
+        f = lambda a, ap: float(kernel_eval(kind, (a * xn)[None, :], (ap * xn)[None, :], (1., 1.), nu=nu)[0, 0])
+        res = integrate.dblquad(f, a=0, b=1, gfun=lambda a: 0, hfun=lambda b: 1, epsrel=1.49e-5, epsabs=1.49e-1)
+        knn[n] = res[0] * d * d
+    slopes = (knn[1:] - knn[:-1]) / (dgrid[1:] - dgrid[:-1])
+    slopes = np.concatenate([slopes, [slopes[-1]]])
+    f32 = lambda v: np.asarray(v, dtype=np.float32)
+    return f32(dgrid), f32(knn), f32(slopes)
+
+
+def doubly_diag(x, params, table):
+    """`KernelDoublyDiagInterpolator.forward` `kernels.py:200-220` (linear interpolation in
+    |x/ell|; an index of -1 (|x| = 0) wraps to the last entry, as torch indexing does)."""
+    sig2, ell = params
+    grid, knn, slopes = (np.asarray(t, dtype=x.dtype) for t in table)
+    d = np.sqrt(np.sum((x / ell) ** 2, axis=-1))
+    lo = np.sum(d[:, None] > grid[None, :], axis=-1) - 1
+    iv = knn[lo] + slopes[lo] * (d - grid[lo])
+    return (ell * ell * sig2 * iv).astype(x.dtype)
 
 
 def grid_points(grids):

@@ -38,8 +38,16 @@ def grids_of(fx):
 
 
 def rel_err(a, b):
+    """max |a - b| / max |b| over the entries; NaNs must sit at the same places (the
+    reference's own NaNs, e.g. the analytic line integral of a zero-length segment)."""
     a = np.asarray(a, dtype=np.float64)
     b = np.asarray(b, dtype=np.float64)
+    na, nb = np.isnan(a), np.isnan(b)
+    if not np.array_equal(na, nb):
+        return float("inf")
+    a, b = a[~na], b[~nb]
+    if b.size == 0:
+        return 0.0
     return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300))
 
 
@@ -69,3 +77,10 @@ def op_ok(y, y_ref32, y_f64, factor=4.0):
     e_me = float(np.max(np.abs(y - y_f64)))
     e_ref = float(np.max(np.abs(np.asarray(y_ref32, np.float64) - y_f64)))
     return e_me <= factor * e_ref + 1e-7 * float(np.max(np.abs(y_f64)))
+
+
+# Line-integral Kuf fixtures (tests/golden/make_golden_semi.py): name -> params
+SEMI_CASES = {"G8": (1., .1), "G9": (.7, .3)}
+# kernel key in the fixture -> (oracle kind, nu / Gneiting alpha)
+SEMI_KERNELS = {"sqexp": ("sqexp", None), "matern0.5": ("matern", .5), "matern1.5": ("matern", 1.5),
+                "matern2.5": ("matern", 2.5), "gneiting1.0": ("gneiting", 1.)}

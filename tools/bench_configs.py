@@ -76,6 +76,15 @@ def run(name, dev):
     except torch.cuda.OutOfMemoryError:
         out["kuf_broadcast_ms"] = None
     torch.cuda.empty_cache()
+    if d == 3:   # config 5's line-integral observations, npts 10 (svi_gp.py:212)
+        from hipgp_amd.kuf import kuf_semi_mc, kuf_semi_sqexp
+        xi = xobs * 1.0
+        t_mc = timed(lambda: kuf_semi_mc(k, grids, xi, params, 10), reps=3)
+        out["kuf_semi_mc10_ms"] = t_mc * 1e3
+        out["kuf_semi_mc10_evals_per_s"] = B * out["M"] * 10 / t_mc
+        ks = kernel("sqexp", None, torch.float32)
+        out["kuf_semi_sqexp_ms"] = timed(lambda: kuf_semi_sqexp(ks, grids, xi, params), reps=3) * 1e3
+        out["kuf_semi_write_gbs"] = B * out["M"] * 4 / (out["kuf_semi_sqexp_ms"] * 1e-3) / 1e9
     if d == 1:
         t = timed(lambda: te.gram_solve(grids, kf, Knm, maxiter=maxiter, do_precond=True, tol=tol, mult_RT=True))
         out.update({"gram_solve_s": t, "reference_cpu": ref, "speedup_vs_reference_cpu": ref["gram_solve_s"] / t})
