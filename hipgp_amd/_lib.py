@@ -25,7 +25,7 @@ EXPORTS = (
     "hgp_pcg_solve", "hgp_pcg_begin", "hgp_pcg_step", "hgp_get_spectrum", "hgp_rowdot",
     "hgp_plan_info", "hgp_plan_destroy", "hgp_last_error", "hgp_version",
     "hgp_toeplitz_apply_pass", "hgp_op_pass_count", "hgp_pcg_rnorm2", "hgp_kuf_grid",
-    "hgp_kuf_semi_mc", "hgp_kuf_semi_sqexp", "hgp_knn_doubly_diag",
+    "hgp_kuf_semi_mc", "hgp_kuf_semi_sqexp", "hgp_knn_doubly_diag", "hgp_meanfield_stats",
 )
 KERN_SQEXP, KERN_MATERN12, KERN_MATERN32, KERN_MATERN52, KERN_GNEITING = 0, 1, 2, 3, 4
 
@@ -68,6 +68,7 @@ def lib():
         "hgp_kuf_semi_mc": (i32, [i32, i32, dbl, i32, pi64, ctypes.POINTER(vp), vp, i64, dbl, dbl, i32, vp, vp, vp]),
         "hgp_kuf_semi_sqexp": (i32, [i32, i32, pi64, ctypes.POINTER(vp), vp, i64, dbl, dbl, vp, vp]),
         "hgp_knn_doubly_diag": (i32, [i32, i32, vp, i64, dbl, dbl, vp, i32, vp, vp]),
+        "hgp_meanfield_stats": (i32, [i32, vp, i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

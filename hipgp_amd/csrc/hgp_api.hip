@@ -945,6 +945,21 @@ int hgp_knn_doubly_diag(int dtype, int ndim, const void* x, int64_t nobs, double
   return 0;
 }
 
+int hgp_meanfield_stats(int dtype, const void* kn, int64_t nrhs, int64_t Mp, const void* qm, const void* qS,
+                        const void* y, const void* ivar, const void* Knn_diag, const void* log_sd, void* an, void* lam,
+                        void* dm, void* hip_stream) {
+  if (dtype != HGP_F32 && dtype != HGP_F64) return fail(HGP_E_ARG, "dtype must be HGP_F32 or HGP_F64");
+  if (nrhs < 0 || Mp <= 0) return fail(HGP_E_ARG, "nrhs >= 0 and Mp > 0 required");
+  if (nrhs > 65535) return fail(HGP_E_ARG, "nrhs must be <= 65535 (grid y dimension)");
+  if (kn == nullptr || qm == nullptr || qS == nullptr || lam == nullptr || dm == nullptr ||
+      (nrhs > 0 && (y == nullptr || ivar == nullptr || Knn_diag == nullptr || log_sd == nullptr || an == nullptr)))
+    return fail(HGP_E_ARG, "null pointer");
+  hipError_t e = meanfield_stats(dtype, kn, nrhs, Mp, qm, qS, y, ivar, Knn_diag, log_sd, an, lam, dm,
+                                 reinterpret_cast<hipStream_t>(hip_stream));
+  if (e != hipSuccess) return fail(HGP_E_HIP, std::string("hgp_meanfield_stats: ") + hipGetErrorString(e));
+  return 0;
+}
+
 int hgp_plan_info(const hgp_plan* plan, int64_t* M, int64_t* Mprime, int64_t* L_K, int64_t* L_R) {
   HGP_TRY(check_plan(plan));
   if (M) *M = plan->M;

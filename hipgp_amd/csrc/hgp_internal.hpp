@@ -45,6 +45,9 @@ hipError_t kuf_semi(int dtype, int kind, double kp, int ndim, const int64_t* m, 
                     hipStream_t s);
 hipError_t doubly_diag(int dtype, int ndim, const void* x, int64_t nobs, double sig2, double ell, const void* tab,
                        int N, void* out, hipStream_t s);
+hipError_t meanfield_stats(int dtype, const void* kn, int64_t nrhs, int64_t Mp, const void* qm, const void* qS,
+                           const void* y, const void* iv, const void* knn, const void* lsd, void* an, void* lam,
+                           void* dm, hipStream_t s);
 hipError_t kuf_semi_grid(int dtype, int kind, int method, int ndim, const int64_t* m, const void* const* grids,
                          const void* x, int64_t nobs, double sig2, double ell, const void* nodes,
                          const void* weights, int npts, void* out, hipStream_t s);

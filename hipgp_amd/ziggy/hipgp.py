@@ -311,6 +311,9 @@ class MeanFieldToeplitzGP(ToeplitzInducingGP):
         with torch.no_grad():
             qm, qS = self.standard_variational_params()
             ivar, log_sd = self.noise_terms(noise_std_batch)
+            if kn.is_cuda:      # the device path: two streaming passes of hgp_meanfield_stats
+                return self._batch_stats_device(kn, ybatch, Knn_diag, qm, qS, ivar, log_sd)
+            # CPU tensors only reach here in the gloo host-logic tests (tests/test_model_cpu.py)
             y = ybatch.reshape(-1)
             knm = kn.matmul(qm).reshape(-1)
             kk = kn * kn
@@ -325,6 +328,24 @@ class MeanFieldToeplitzGP(ToeplitzInducingGP):
             dm_sum = -(bdiff[None, :].matmul(kn)).reshape(-1)
             an_sum = an.sum()
         return {"an_sum": an_sum, "lam_sum": lam_sum, "dm_sum": dm_sum, "n": kn.shape[0]}
+
+    def _batch_stats_device(self, kn, ybatch, Knn_diag, qm, qS, ivar, log_sd):
+        import ctypes
+        from hipgp_amd import _lib
+        B, Mp = kn.shape
+        dev, dt = kn.device, kn.dtype
+        col = lambda v: torch.as_tensor(v, dtype=dt, device=dev).reshape(-1).expand(B).contiguous()
+        knc = kn.detach().contiguous()
+        qmv = qm.detach().reshape(-1).to(dt).contiguous()
+        qSv = qS.detach().reshape(-1).to(dt).contiguous()
+        y, iv, kd, lsd = col(ybatch), col(ivar), col(Knn_diag), col(log_sd)
+        an = torch.empty(B, dtype=dt, device=dev)
+        lam = torch.empty(Mp, dtype=dt, device=dev)
+        dm = torch.empty(Mp, dtype=dt, device=dev)
+        p = lambda t: ctypes.c_void_p(t.data_ptr())
+        _lib.check(_lib.lib().hgp_meanfield_stats(_lib.dtype_code(dt), p(knc), B, Mp, p(qmv), p(qSv), p(y), p(iv),
+                                                  p(kd), p(lsd), p(an), p(lam), p(dm), _lib.stream_ptr(dev)))
+        return {"an_sum": an.sum(), "lam_sum": lam, "dm_sum": dm, "n": B}
 
     def apply_stats(self, stats, bsz):
         """ELBO estimate and theta grads from (all-reduced) batch sums of `bsz` observations."""

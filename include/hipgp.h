@@ -146,6 +146,18 @@ int hgp_kuf_semi_sqexp(int dtype, int ndim, const int64_t* m, const void* const*
 int hgp_knn_doubly_diag(int dtype, int ndim, const void* x, int64_t nobs, double sig2, double ell,
                         const void* table, int N, void* out, void* hip_stream);
 
+/* Mean-field natural-gradient statistics of a minibatch (the batch sums
+ * of MeanFieldToeplitzGP.elbo_and_grad, hipgp.py:234-250, and a_n of compute_batch_an,
+ * hipgp.py:370-414), from kn = R^T K^-1 Knm^T (nrhs, Mp) and the variational mean qm / diagonal
+ * covariance qS (Mp,), with per-observation y, ivar = 1/noise^2, Knn_diag, log_sd (nrhs,):
+ *   an[n]  = -1/2 ivar_n ((kn_n.qm - y_n)^2 + Knn_n - |kn_n|^2 + kn_n^2.qS) - log_sd_n - ln(2 pi)/2
+ *   lam[j] = sum_n ivar_n kn_nj^2,   dm[j] = -sum_n ivar_n (kn_n.qm - y_n) kn_nj
+ * All device arrays of dtype; deterministic (fixed reduction order), two reads of kn.
+ * Per rank these are the partial sums RCCL all-reduces across the RHS shards. */
+int hgp_meanfield_stats(int dtype, const void* kn, int64_t nrhs, int64_t Mp, const void* qm,
+                        const void* qS, const void* y, const void* ivar, const void* Knn_diag,
+                        const void* log_sd, void* an, void* lam, void* dm, void* hip_stream);
+
 /* Sizes of a plan: M, M' and the padded FFT lengths per axis (K-type and R-type ops). */
 int hgp_plan_info(const hgp_plan* plan, int64_t* M, int64_t* Mprime, int64_t* L_K,
                   int64_t* L_R);

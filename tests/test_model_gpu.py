@@ -95,3 +95,34 @@ def test_sharded_two_ranks_one_gpu():
         assert abs(elbo - float(fx["elbo"])) < 1e-8 * abs(float(fx["elbo"]))
         assert rel_err(g1, fx["theta1_grad"]) < 1e-7
     assert out[0][2] == out[1][2] and out[0][2] < 200
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32], ids=["f64", "f32"])
+@pytest.mark.parametrize("per_obs_noise", [False, True], ids=["noise2", "noise_std"])
+def test_meanfield_stats_kernel(dtype, per_obs_noise):
+    """hgp_meanfield_stats (two passes over kn) against the torch expression of the same batch
+    sums (hipgp.py:234-250, 370-414) on random kn of a C2-sized expanded grid slice."""
+    fx = load("G5", "f64")
+    mod = _model(fx, dtype=dtype)
+    g = torch.Generator().manual_seed(7)
+    B, Mp = 37, mod.Mprime
+    kn = (torch.randn(B, Mp, generator=g, dtype=torch.float64) * .05).to(DEV, dtype)
+    y = torch.randn(B, 1, generator=g, dtype=torch.float64).to(DEV, dtype)
+    knn = (torch.rand(B, generator=g, dtype=torch.float64) + 1).to(DEV, dtype)
+    nsd = (torch.rand(B, 1, generator=g, dtype=torch.float64) * .5 + .1).to(DEV, dtype) if per_obs_noise else None
+    st = mod.batch_stats(kn, y, knn, nsd)
+    # torch expression on the device (the reference's formulas)
+    torch.set_grad_enabled(False)
+    qm, qS = mod.standard_variational_params()
+    ivar, log_sd = mod.noise_terms(nsd)
+    iv = ivar.reshape(-1) if ivar.dim() > 0 else ivar
+    knm = kn.matmul(qm).reshape(-1)
+    an = -0.5 * iv * ((knm - y.reshape(-1)) ** 2 + knn - (kn * kn).sum(-1) + (kn * kn).matmul(qS).reshape(-1)) \
+        - (log_sd.reshape(-1) if log_sd.dim() > 0 else log_sd) - 0.5 * np.log(2 * np.pi)
+    lam = torch.sum((iv[:, None] if iv.dim() > 0 else iv) * kn * kn, dim=0)
+    dm = -((iv * (knm - y.reshape(-1)))[None, :].matmul(kn)).reshape(-1)
+    torch.set_grad_enabled(True)
+    tol = 1e-12 if dtype == torch.float64 else 2e-5
+    assert abs(float(st["an_sum"] - an.sum())) <= tol * float(an.abs().sum())
+    assert rel_err(st["lam_sum"].cpu().numpy(), lam.cpu().numpy()) < tol
+    assert rel_err(st["dm_sum"].cpu().numpy(), dm.cpu().numpy()) < tol
