@@ -43,6 +43,9 @@
 #ifndef HGP_MINW_STRIDED
 #define HGP_MINW_STRIDED 0       // waves/SIMD occupancy hint; 0 = from the LDS footprint
 #endif
+#ifndef HGP_MINW_STRIDED_SMALL
+#define HGP_MINW_STRIDED_SMALL 0 // short lines (< 16 threads per line): from the LDS footprint
+#endif
 #ifndef HGP_MINW_ROW
 #define HGP_MINW_ROW 0
 #endif
@@ -126,7 +129,7 @@ template <typename T, int H, int LAY> struct PassCfg {
   static constexpr int BLOCKS_BY_LDS = LDS_CAP / LDS;
   static constexpr int MINW_LDS = (BLOCKS_BY_LDS * WAVES_PER_BLOCK) / 4;
   static constexpr int MINW_AUTO = MINW_LDS < 1 ? 1 : (MINW_LDS > 4 ? 4 : MINW_LDS);
-  static constexpr int MINW_SET = (LAY == LAY_STRIDED) ? HGP_MINW_STRIDED
+  static constexpr int MINW_SET = (LAY == LAY_STRIDED) ? (TT >= 16 ? HGP_MINW_STRIDED : HGP_MINW_STRIDED_SMALL)
                                  : (LAY == LAY_CONTIG) ? HGP_MINW_CONTIG : HGP_MINW_ROW;
   static constexpr int MINW = MINW_SET > 0 ? MINW_SET : MINW_AUTO;
 };
