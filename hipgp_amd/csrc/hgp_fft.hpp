@@ -137,12 +137,15 @@ __device__ __forceinline__ void xsync() {
 }
 
 // Twiddles W_L^q (forward sign), q in [0, L = 2H), live in LDS, staged once per block:
-//  * half table (H * sizeof(complex) <= 32 KB): tab[q] = W_L^q for q < H, W_L^{q+H} = -W_L^q;
-//  * two-level table beyond that (fp64 at H >= 4096, fp32 at H >= 8192, where a half table
-//    would not fit next to the exchange image): tab = [A | B], A[j] = W_L^j (j < S),
+//  * half table (H * sizeof(complex) <= HGP_TW_FULL_MAX = 16 KB): tab[q] = W_L^q for q < H, W_L^{q+H} = -W_L^q;
+//  * two-level table beyond that (fp64 at H >= 2048, fp32 at H >= 4096: a whole table there
+//    halves the blocks a CU holds; 4096^2 K matvec 10.3 -> 6.2 ms): tab = [A | B], A[j] = W_L^j (j < S),
 //    B[i] = W_L^{iS} (i < H/S), W_L^q = A[q mod S] B[q div S] (one extra product, ~1 ulp).
+#ifndef HGP_TW_FULL_MAX
+#define HGP_TW_FULL_MAX (16 * 1024)   // largest half table (bytes) kept whole in LDS
+#endif
 template <typename T, int H> struct TwTab {
-  static constexpr bool TWO = H * (int)sizeof(C2<T>) > 32 * 1024;
+  static constexpr bool TWO = H * (int)sizeof(C2<T>) > HGP_TW_FULL_MAX;
   static constexpr int LG = [] { int l = 0; while ((1 << l) < H) ++l; return l; }();
   static constexpr int S = TWO ? (1 << ((LG + 1) / 2)) : H;
   static constexpr int ENTRIES = TWO ? S + H / S : H;

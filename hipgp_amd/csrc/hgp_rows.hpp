@@ -19,6 +19,9 @@
 #ifndef HGP_ROWT_PAIRS
 #define HGP_ROWT_PAIRS 8          // row pairs per block (16 rows = 128-B column segments)
 #endif
+#ifndef HGP_ROWT_PAIRS_BIG
+#define HGP_ROWT_PAIRS_BIG 16     // the same knob for rows longer than one wave's line (TT > 64)
+#endif
 
 namespace hgp {
 
@@ -32,7 +35,7 @@ template <typename T, int H> struct RowTCfg {
   static constexpr int area(int c) { return ex_elems(c) > tile_elems(c) ? ex_elems(c) : tile_elems(c); }
   static constexpr int lds_bytes_for(int c) { return area(c) * (int)sizeof(C2<T>) + TwTab<T, H>::BYTES; }
   static constexpr int c_pairs() {
-    int c = HGP_ROWT_PAIRS * 64 / TT;              // 512 threads at the default
+    int c = (TT > 64 ? HGP_ROWT_PAIRS_BIG : HGP_ROWT_PAIRS) * 64 / TT;   // 512 threads at the default
     if (c < 1) c = 1;
     if (c > 64) c = 64;                            // tiny rows: cap the tile height
     while (c > 1 && (c * TT > 1024 || lds_bytes_for(c) > LDS_CAP)) c >>= 1;
