@@ -1,8 +1,10 @@
 """Reduce the FETCH_SIZE / WRITE_SIZE passes of tools/pmc_kop.sh to bytes per batched K matvec.
 
-The timed region launches the op's kernels `steps + warmup` times each (plus the setup
-kernels, which are excluded by name); per kernel we take the median dispatch value, sum over
-the op's kernels, and apply the gfx950 FETCH_SIZE correction (x2, MI355X_MICROARCH.md §HBM)."""
+The run performs `nops = steps + warmup` batched K matvecs (argv[3], default 13); each op
+launches every pass kernel once per RHS chunk (two chunks on two streams at C2), so per
+kernel we take the median dispatch value times dispatches / nops, sum over the op's kernels
+(setup kernels are excluded by name) and apply the gfx950 FETCH_SIZE correction
+(x2, MI355X_MICROARCH.md §HBM)."""
 import collections
 import csv
 import glob
@@ -12,6 +14,7 @@ import statistics
 import sys
 
 root, out = sys.argv[1], sys.argv[2]
+nops = int(sys.argv[3]) if len(sys.argv) > 3 else 13
 OP_KERNELS = ("k_row_fwd_t", "k_row_inv_t", "k_pass<float")
 vals = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
@@ -22,7 +25,7 @@ for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursiv
                 vals[row["Counter_Name"]][name.split("(")[0]].append(float(row["Counter_Value"]))
 per = {}
 for cnt, ks in vals.items():
-    per[cnt] = {k: statistics.median(v) for k, v in ks.items()}
+    per[cnt] = {k: statistics.median(v) * len(v) / nops for k, v in ks.items()}
 fetch_kb = sum(per.get("FETCH_SIZE", {}).values())
 write_kb = sum(per.get("WRITE_SIZE", {}).values())
 res = {"workload": "C2 batched K matvec, 2-D 1024x1024, 32 RHS, fp32", "M": 1024 * 1024, "rhs": 32,
