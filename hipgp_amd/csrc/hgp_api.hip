@@ -219,6 +219,10 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
     B1 = std::max(g.in[0] * g.in[1], g.out[0] * g.out[1]) * Sl;
     B2 = std::max(g.in[0], g.out[0]) * g.L[1] * Sl;
   }
+  // the 2-D row passes address one RHS's intermediate slab (and the contiguous pass one line)
+  // with 32-bit byte offsets from a scalar base (raw buffer accesses, hgp_rows.hpp)
+  if (d == 2 && B1 * (int64_t)cs >= ((int64_t)1 << 31))
+    return fail(HGP_E_UNSUPPORTED, "2-D grid too large: one right-hand side's intermediate exceeds 2 GiB");
   // RHS chunks: 2-D ops spread them over NS streams, chunk j on stream (and workspace slot)
   // j % NS; each chunk's RHS are processed entirely on its stream (no cross-stream data).
   const int NS = (d == 2 && only_pass < 0) ? (int)std::min<int64_t>(std::max(1, P->nstreams), nrhs) : 1;

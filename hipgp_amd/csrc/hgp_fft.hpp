@@ -41,6 +41,48 @@ template <typename T> __device__ __forceinline__ C2<T> cmulc(C2<T> a, C2<T> b) {
 }
 template <typename T> __device__ __forceinline__ C2<T> cscale(C2<T> a, T s) { return mk<T>(a.x * s, a.y * s); }
 
+// Raw buffer access (gfx9 resource word 3 = 0x00020000, stride 0): a wave-uniform base in
+// scalar registers plus a 32-bit lane byte offset, so no 64-bit address is formed per access;
+// loads at offsets >= `bytes` return 0 and stores there are dropped (used for zero padding,
+// cropping and invalid lines without per-element selects).  The lane offset `off` is shared by
+// a thread's points; the per-point stride goes in the scalar offset `soff`.
+using BufRsrc = __amdgpu_buffer_rsrc_t;
+__device__ __forceinline__ BufRsrc buf_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+template <typename T> __device__ __forceinline__ C2<T> buf_ld_c2(BufRsrc r, uint32_t off, uint32_t soff = 0);
+template <> __device__ __forceinline__ C2<float> buf_ld_c2<float>(BufRsrc r, uint32_t off, uint32_t soff) {
+  return __builtin_bit_cast(C2<float>, __builtin_amdgcn_raw_buffer_load_b64(r, off, soff, 0));
+}
+template <> __device__ __forceinline__ C2<double> buf_ld_c2<double>(BufRsrc r, uint32_t off, uint32_t soff) {
+  return __builtin_bit_cast(C2<double>, __builtin_amdgcn_raw_buffer_load_b128(r, off, soff, 0));
+}
+template <typename T> __device__ __forceinline__ void buf_st_c2(C2<T> v, BufRsrc r, uint32_t off, uint32_t soff = 0);
+template <> __device__ __forceinline__ void buf_st_c2<float>(C2<float> v, BufRsrc r, uint32_t off, uint32_t soff) {
+  using V = decltype(__builtin_amdgcn_raw_buffer_load_b64(r, 0, 0, 0));
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(V, v), r, off, soff, 0);
+}
+template <> __device__ __forceinline__ void buf_st_c2<double>(C2<double> v, BufRsrc r, uint32_t off, uint32_t soff) {
+  using V = decltype(__builtin_amdgcn_raw_buffer_load_b128(r, 0, 0, 0));
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(V, v), r, off, soff, 0);
+}
+template <typename T> __device__ __forceinline__ T buf_ld(BufRsrc r, uint32_t off, uint32_t soff = 0);
+template <> __device__ __forceinline__ float buf_ld<float>(BufRsrc r, uint32_t off, uint32_t soff) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, soff, 0));
+}
+template <> __device__ __forceinline__ double buf_ld<double>(BufRsrc r, uint32_t off, uint32_t soff) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, soff, 0));
+}
+
+template <typename T> __device__ __forceinline__ void buf_st(T v, BufRsrc r, uint32_t off, uint32_t soff = 0);
+template <> __device__ __forceinline__ void buf_st<float>(float v, BufRsrc r, uint32_t off, uint32_t soff) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, soff, 0);
+}
+template <> __device__ __forceinline__ void buf_st<double>(double v, BufRsrc r, uint32_t off, uint32_t soff) {
+  using V = decltype(__builtin_amdgcn_raw_buffer_load_b64(r, 0, 0, 0));
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(V, v), r, off, soff, 0);
+}
+
 // points per thread: 16 complex in fp32 (32 VGPRs), 8 in fp64 (32 VGPRs)
 template <typename T> struct PMax;
 template <> struct PMax<float> { static constexpr int v = 16; };

@@ -205,7 +205,14 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
   int l, t, lbase;
   constexpr int LSTRIDE = (LAY == LAY_STRIDED) ? C : 1;
   if constexpr (LAY == LAY_STRIDED) { t = tid / C; l = tid - t * C; lbase = l; }
-  else { l = tid / TT; t = tid - l * TT; lbase = l * H; }
+  else {
+    // lines of whole waves: the line index is wave-uniform, kept in a scalar register so the
+    // line's base pointers are scalar and every load/store is base + 32-bit lane offset
+    l = (TT % 64 == 0) ? __builtin_amdgcn_readfirstlane(tid / TT) : tid / TT;
+    t = tid & (TT - 1);           // TT is a power of two: the known range of t folds the
+                                  // half-table sign tests of positions t + TT k < H
+    lbase = l * H;
+  }
 
   // ---- line coordinates (q = RHS, r = outer line, i = inner line) ----
   // Strided: q, r and the block's first column i0 are block-uniform (scalar registers); a lane
@@ -335,6 +342,14 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
     sp = (int)d.spec_p;
     so = (LAY == LAY_STRIDED ? lc * (int)d.spec_i : 0) + t * sp;
   }
+  // contiguous lines of whole waves: wave-uniform line bases -> raw buffer accesses (32-bit
+  // lane offsets; the zero padding beyond in_len and the crop beyond out_len come from the
+  // resource's range, invalid lines get an empty range)
+  constexpr bool BUF = (LAY == LAY_CONTIG) && (TT % 64 == 0) && !CAN_FOLD;
+  const BufRsrc rin = buf_rsrc(BUF ? (const void*)in_c : nullptr,
+                               (BUF && valid) ? (uint32_t)d.in.len * (uint32_t)sizeof(C2<T>) : 0u);
+  const BufRsrc rout = buf_rsrc(BUF ? (const void*)out_c : nullptr,
+                                (BUF && valid) ? (uint32_t)d.out.len * (uint32_t)sizeof(C2<T>) : 0u);
   if constexpr (MODE == PASS_FWD || CONV) {
     const int in_len = d.in.len;
     const int lim = in_len - 1;
@@ -342,8 +357,13 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
 #pragma unroll
     for (int k = 0; k < P; ++k) {
       const int p = t + TT * k;
-      C2<T> a = load_in(p < in_len ? p : lim);
-      if (p >= in_len) a = mk<T>(0, 0);
+      C2<T> a;
+      if constexpr (BUF) {
+        a = buf_ld_c2<T>(rin, (uint32_t)t * (uint32_t)sizeof(C2<T>), (uint32_t)(TT * k * (int)sizeof(C2<T>)));
+      } else {
+        a = load_in(p < in_len ? p : lim);
+        if (p >= in_len) a = mk<T>(0, 0);
+      }
       C2<T> c = mk<T>(0, 0);
       if constexpr (CAN_FOLD) {
         if (fold) c = load_hi(p);
@@ -397,10 +417,19 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
 #pragma unroll
       for (int k = 0; k < P; ++k) { sre[k] = (T)1; sre1[k] = (T)1; }
 #else
+      if constexpr (BUF) {
+        const BufRsrc rspec = buf_rsrc(sb, 0x7fffffffu);
 #pragma unroll
-      for (int k = 0; k < P; ++k) {
-        sre[k] = sb[so + TT * k * sp];
-        sre1[k] = sb[so + (H + TT * k) * sp];
+        for (int k = 0; k < P; ++k) {
+          sre[k] = buf_ld<T>(rspec, (uint32_t)so * (uint32_t)sizeof(T), (uint32_t)(TT * k * sp) * (uint32_t)sizeof(T));
+          sre1[k] = buf_ld<T>(rspec, (uint32_t)so * (uint32_t)sizeof(T), (uint32_t)((H + TT * k) * sp) * (uint32_t)sizeof(T));
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+          sre[k] = sb[so + TT * k * sp];
+          sre1[k] = sb[so + (H + TT * k) * sp];
+        }
       }
 #endif
       if (d.spart != nullptr) {   // uniform: spectral dot sum_k S_k |X_k|^2 of this line
@@ -463,7 +492,9 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
       for (int hh = 0; hh < 2; ++hh) {
         const C2<T> y = hh == 0 ? cadd<T>(va[k], wo) : csub<T>(va[k], wo);
         const int pp = p + hh * H;
-        if (valid && pp < out_len) {
+        // buffer stores: the resource range crops (and drops invalid lines); only the
+        // uniform test whether the half hh reaches the output at all remains
+        if (BUF ? (hh * H < out_len) : (valid && pp < out_len)) {
           if constexpr (REAL_OUT) {
             out_re[pp] = y.x;
             if (dot_re != nullptr) dsum += y.x * dot_re[pp];
@@ -473,6 +504,8 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
                 if (dot_re != nullptr) dsum += y.y * dot_im[pp];
               }
             }
+          } else if constexpr (BUF) {
+            buf_st_c2<T>(y, rout, (uint32_t)t * (uint32_t)sizeof(C2<T>), (uint32_t)((pp - t) * (int)sizeof(C2<T>)));
           } else {
             out_c[out_at(pp)] = y;
           }

@@ -71,8 +71,10 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
   const int nrb = (d.Rn + C - 1) / C;
   const int q = blockIdx.x / nrb;
   const int rb = blockIdx.x - q * nrb;
-  const int l = threadIdx.x / TT;
-  const int t = threadIdx.x - l * TT;
+  // a pair's line spans whole waves at every H used here (TT >= 64): l is wave-uniform (scalar
+  // register, scalar row bases), t's known range folds the half-table sign tests
+  const int l = (TT % 64 == 0) ? __builtin_amdgcn_readfirstlane(threadIdx.x / TT) : threadIdx.x / TT;
+  const int t = threadIdx.x & (TT - 1);
   const int lbase = l * H;
   const int rp = rb * C + l;                       // this group's pair
   const bool pvalid = (l < C) && (rp < d.Rn);
@@ -83,15 +85,13 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
   const int in_len = d.in.len;
 
   C2<T> va[P], vb[P];
+  // raw buffer loads: past the row length (zero padding) and for absent rows they return 0
+  const BufRsrc ra = buf_rsrc(in_a, pvalid ? (uint32_t)in_len * (uint32_t)sizeof(T) : 0u);
+  const BufRsrc rb_ = buf_rsrc(in_b, has2 ? (uint32_t)in_len * (uint32_t)sizeof(T) : 0u);
 #pragma unroll
   for (int k = 0; k < P; ++k) {
-    const int p = t + TT * k;
-    const int pc = p < in_len ? p : in_len - 1;
-    const T re = in_a[pc];
-    const T im = in_b[pc];
-    C2<T> a = mk<T>(re, has2 ? im : (T)0);
-    if (p >= in_len) a = mk<T>(0, 0);
-    va[k] = a;
+    const uint32_t lo = (uint32_t)t * (uint32_t)sizeof(T), so = (uint32_t)(TT * k * (int)sizeof(T));
+    va[k] = mk<T>(buf_ld<T>(ra, lo, so), buf_ld<T>(rb_, lo, so));
   }
   __syncthreads();   // twiddle table staged
 #pragma unroll
@@ -99,6 +99,7 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
 
   C2<T>* W = reinterpret_cast<C2<T>*>(d.out.ptr) + (int64_t)q * d.out.q_stride;
   const int64_t S0 = d.out.r_stride;
+  const BufRsrc rW = buf_rsrc(W, 0x7fffffffu);     // one RHS's slab: < 2 GiB (checked on the host)
   const int row0 = 2 * rb * C;                     // first row of this block's tile
   const int nrow_blk = d.nrows - row0 < 2 * C ? d.nrows - row0 : 2 * C;
 
@@ -143,7 +144,8 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
       const int e = threadIdx.x + j * Cfg::THREADS;
       const int col = e / (2 * C);
       const int row = e - col * (2 * C);
-      if (e < NE && row < nrow_blk) W[(int64_t)(C0 + col) * S0 + row0 + row] = lds[col * PITCH + row];
+      if (e < NE && row < nrow_blk)
+        buf_st_c2<T>(lds[col * PITCH + row], rW, ((uint32_t)(C0 + col) * (uint32_t)S0 + (uint32_t)(row0 + row)) * (uint32_t)sizeof(C2<T>));
     }
     __syncthreads();   // tile read before the next half's FFT reuses the area
   };
@@ -164,9 +166,11 @@ template <typename T, int EPI, int THREADS>
 __device__ __forceinline__ T cg_epilogue(const T* __restrict__ ys, int nrow, int out_len, T* __restrict__ xg,
                                          T* __restrict__ rg, T* __restrict__ pg, int64_t rpitch, T coef) {
   const int nel = nrow * out_len;
+  // the block's rows are one < 2 GiB window of each vector: raw buffers, 32-bit lane offsets
+  const BufRsrc rp = buf_rsrc(pg, 0x7fffffffu), rx = buf_rsrc(xg, 0x7fffffffu), rr = buf_rsrc(rg, 0x7fffffffu);
   T s = 0;
   for (int e0 = threadIdx.x; e0 < nel; e0 += 4 * THREADS) {
-    int64_t g[4];
+    uint32_t g[4];
     T yv[4], pv[4], xv[4], rv[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -174,24 +178,24 @@ __device__ __forceinline__ T cg_epilogue(const T* __restrict__ ys, int nrow, int
       const int ee = e < nel ? e : nel - 1;
       const int row = ee / out_len;
       const int c = ee - row * out_len;
-      g[u] = (int64_t)row * rpitch + c;
+      g[u] = ((uint32_t)row * (uint32_t)rpitch + (uint32_t)c) * (uint32_t)sizeof(T);
       yv[u] = ys[ee];
-      pv[u] = pg[g[u]];
+      pv[u] = buf_ld<T>(rp, g[u]);
       if constexpr (EPI == EPI_XR) {
-        xv[u] = xg[g[u]];
-        rv[u] = rg[g[u]];
+        xv[u] = buf_ld<T>(rx, g[u]);
+        rv[u] = buf_ld<T>(rr, g[u]);
       }
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if (e0 + u * THREADS < nel) {
         if constexpr (EPI == EPI_XR) {
-          xg[g[u]] = xv[u] + coef * pv[u];
+          buf_st<T>(xv[u] + coef * pv[u], rx, g[u]);
           const T rn = rv[u] - coef * yv[u];
-          rg[g[u]] = rn;
+          buf_st<T>(rn, rr, g[u]);
           s += rn * rn;
         } else {
-          pg[g[u]] = yv[u] + coef * pv[u];
+          buf_st<T>(yv[u] + coef * pv[u], rp, g[u]);
         }
       }
     }
@@ -214,14 +218,17 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
   const int nrb = (d.Rn + C - 1) / C;
   const int q = blockIdx.x / nrb;
   const int rb = blockIdx.x - q * nrb;
-  const int l = threadIdx.x / TT;
-  const int t = threadIdx.x - l * TT;
+  // a pair's line spans whole waves at every H used here (TT >= 64): l is wave-uniform (scalar
+  // register, scalar row bases), t's known range folds the half-table sign tests
+  const int l = (TT % 64 == 0) ? __builtin_amdgcn_readfirstlane(threadIdx.x / TT) : threadIdx.x / TT;
+  const int t = threadIdx.x & (TT - 1);
   const int lbase = l * H;
   const int rp = rb * C + l;
   const bool pvalid = (l < C) && (rp < d.Rn);
   const bool has2 = pvalid && (2 * rp + 1 < d.nrows);
   const C2<T>* W = reinterpret_cast<const C2<T>*>(d.in.ptr) + (int64_t)q * d.in.q_stride;
   const int64_t S0 = d.in.r_stride;
+  const BufRsrc rW = buf_rsrc(W, 0x7fffffffu);     // one RHS's slab: < 2 GiB (checked on the host)
   const int row0 = 2 * rb * C;
   const int nrow_blk = d.nrows - row0 < 2 * C ? d.nrows - row0 : 2 * C;
 
@@ -243,7 +250,7 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
       const int col = ee / (2 * C);
       const int row = ee - col * (2 * C);
       const int rr = row < nrow_blk ? row : 0;
-      C2<T> val = W[(int64_t)(C0 + col) * S0 + row0 + rr];
+      C2<T> val = buf_ld_c2<T>(rW, ((uint32_t)(C0 + col) * (uint32_t)S0 + (uint32_t)(row0 + rr)) * (uint32_t)sizeof(C2<T>));
       if (row >= nrow_blk) val = mk<T>(0, 0);
       buf[j] = val;
     }
@@ -339,6 +346,8 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
   }
   T* out_a = reinterpret_cast<T*>(d.out.ptr) + (int64_t)q * d.out.q_stride + (int64_t)(pvalid ? 2 * rp : 0) * d.out.r_stride;
   T* out_b = out_a + d.out.r_stride;
+  const BufRsrc roa = buf_rsrc(out_a, pvalid ? (uint32_t)out_len * (uint32_t)sizeof(T) : 0u);
+  const BufRsrc rob = buf_rsrc(out_b, has2 ? (uint32_t)out_len * (uint32_t)sizeof(T) : 0u);
   const T* dot_a = nullptr;
   const T* dot_b = nullptr;
   if (d.partial != nullptr) {
@@ -356,12 +365,18 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
     for (int hh = 0; hh < 2; ++hh) {
       const C2<T> y = hh == 0 ? cadd<T>(va[k], wo) : csub<T>(va[k], wo);
       const int pp = p + hh * H;
-      if (pvalid && pp < out_len) {
+      if (dot_a == nullptr) {   // uniform: buffer stores, the ranges crop and drop absent rows
+        if (hh * H < out_len) {
+          const uint32_t lo = (uint32_t)t * (uint32_t)sizeof(T), so = (uint32_t)((pp - t) * (int)sizeof(T));
+          buf_st<T>(y.x, roa, lo, so);
+          buf_st<T>(y.y, rob, lo, so);
+        }
+      } else if (pvalid && pp < out_len) {
         out_a[pp] = y.x;
-        if (dot_a != nullptr) dsum += y.x * dot_a[pp];
+        dsum += y.x * dot_a[pp];
         if (has2) {
           out_b[pp] = y.y;
-          if (dot_a != nullptr) dsum += y.y * dot_b[pp];
+          dsum += y.y * dot_b[pp];
         }
       }
     }
