@@ -280,6 +280,9 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
         const int me = pass_no++;
         if (only_pass >= 0 && only_pass != me) return 0;
         hipError_t e = launch_rowt<T>((int)H1, inv, epi_mode, D, st);
+        if (e == hipErrorNotSupported)
+          return fail(HGP_E_UNSUPPORTED, "row transform of H = " + std::to_string(H1) +
+                                             " points does not fit one CU's LDS in this dtype (use fp32)");
         if (e != hipSuccess) return fail(HGP_E_HIP, std::string("row pass launch: ") + hipGetErrorString(e));
         return 0;
       };

@@ -83,6 +83,7 @@ static hipError_t launch_rowt_inv(const PassDesc& d, int64_t nb, hipStream_t s) 
 template <typename T, int H>
 static hipError_t launch_rowt_h(int inv, int epi, const PassDesc& d, hipStream_t s) {
   using Cfg = RowTCfg<T, H>;
+  if constexpr (Cfg::LDS > LDS_CAP) return hipErrorNotSupported;   // e.g. fp64 rows of H = 8192
   const int64_t nb = (int64_t)d.Q * ((d.Rn + Cfg::C - 1) / Cfg::C);
   if (nb <= 0) return hipSuccess;
   if (inv) {

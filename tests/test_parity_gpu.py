@@ -223,3 +223,42 @@ def test_pcg_fp32_vs_fp64_full_size(dims):
     assert r64 < 0.2, r64
     rel = float(((x32 - x64).norm(dim=1) / x64.norm(dim=1)).max())
     assert rel < 1e-3, (rel, r64, r32)
+
+
+@pytest.mark.parametrize("m", [2048, 4096], ids=["C3_2048x2048", "C4_4096x4096"])
+def test_large_grid_fp32_vs_fp64(m):
+    """C3 / C4 grid sizes (rows longer than one wave's line: 16-pair row blocks, and at 4096
+    the fp32 two-level LDS twiddle table): the fp32 K, C^-1 (and R^T at 2048) agree with the
+    fp64 plan of the same well-conditioned problem (nugget 0.1; fp64 ops are pinned to the
+    oracle above); at 4096 R^T is checked through R(R^T v) = K v in fp32, since fp64 rows of
+    the R^T length (H = 8192) do not fit one CU's LDS and are refused explicitly."""
+    import ziggy.kernels as zk
+    from hipgp_amd._lib import HipgpError
+    from ziggy.misc.toeplitz_tensor import ToeplitzTensor
+    outs = {}
+    g = torch.Generator(device=DEV).manual_seed(2)
+    v64 = torch.randn(2, m * m, device=DEV, generator=g, dtype=torch.float64)
+    for dt in (torch.float64, torch.float32):
+        k = zk.Matern(nu=1.5, dtype=dt)
+        grids = [torch.linspace(-1, 1, m, device=DEV, dtype=dt) for _ in range(2)]
+        T = ToeplitzTensor(grids, lambda x, y: k.forward(x, y, params=(1., .1)), jitter_val=0.1)
+        T.set_batch_shape((2,))
+        v = v64.to(dt)
+        res = [T._matmul_by_K(v), T._matmul_by_Cinv(v)]
+        if m == 2048:
+            res.append(T._matmul_by_RT(v))
+        elif dt == torch.float32:
+            rr = T._matmul_by_R(T._matmul_by_RT(v))
+            assert float((rr - res[0]).abs().max() / res[0].abs().max()) < 1e-4
+        else:
+            with pytest.raises(HipgpError, match="does not fit"):
+                T._matmul_by_RT(v)
+        outs[dt] = [o.double() for o in res]
+        del T
+        torch.cuda.empty_cache()
+    # C^-1 applies 1/D over a spectrum spanning cond ~ 7e5 here: its fp32 error relative to the
+    # output's max is ~1e-4 (measured 2.2e-4 at 2048^2); R^T (sqrt D, 2.5e-5 measured) and K
+    # stay near FFT rounding
+    for name, a, b, tol in zip(("K", "Cinv", "RT"), outs[torch.float32], outs[torch.float64], (2e-5, 2e-3, 1e-4)):
+        err = float((a - b).abs().max() / b.abs().max())
+        assert err < tol, (name, err)
