@@ -539,7 +539,9 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
 // the odd group adds the even group's result after ONE block barrier (y = ye + conj(W) yo).
 // Half the registers of a one-group-per-line kernel (no second half held), so twice the
 // waves per SIMD hide the memory and LDS latency; the spectrum of the half is prefetched
-// with the data.
+// with the data.  NOT dispatched by the library: the one-group-per-line k_pass<CONTIG, CONV>
+// measured faster (its two halves share the exchange image and the line loads); kept only
+// for the side-by-side timing in tools/passbench.hip.
 // ------------------------------------------------------------------------------------------
 template <typename T, int H> struct ConvCfg {
   static constexpr int P = (H < PMax<T>::v) ? H : PMax<T>::v;
