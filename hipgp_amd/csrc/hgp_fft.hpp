@@ -186,12 +186,24 @@ __device__ __forceinline__ void xsync() {
 #ifndef HGP_TW_FULL_MAX
 #define HGP_TW_FULL_MAX (16 * 1024)   // largest half table (bytes) kept whole in LDS
 #endif
+//  * stage-1 power table (HGP_TW_T1, after the above): the second Stockham stage needs, per
+//    thread, the powers w^r (r < R1) of one twiddle w = W_H^{kk H/(NS1 R1)}, kk < NS1 (NS1, R1 =
+//    the first two radices).  There are only NS1 x R1 such values: they are tabulated once per
+//    block ([kk][r], pitch R1 + 1: the NS1 rows a wave reads start in distinct banks) and read
+//    with R1 - 1 LDS loads instead of one load and R1 - 2 complex products per butterfly.
+#ifndef HGP_TW_T1
+#define HGP_TW_T1 0   // measured slower (C2 column pass 0.149 -> 0.155 ms): LDS-bound, not VALU-bound
+#endif
 template <typename T, int H> struct TwTab {
   static constexpr bool TWO = H * (int)sizeof(C2<T>) > HGP_TW_FULL_MAX;
   static constexpr int LG = [] { int l = 0; while ((1 << l) < H) ++l; return l; }();
   static constexpr int S = TWO ? (1 << ((LG + 1) / 2)) : H;
   static constexpr int ENTRIES = TWO ? S + H / S : H;
-  static constexpr int BYTES = ENTRIES * (int)sizeof(C2<T>);
+  using St = Stages<H, (H < PMax<T>::v ? H : PMax<T>::v)>;
+  static constexpr bool T1 = HGP_TW_T1 && St::count() >= 2 && St::radix(1) > 2;
+  static constexpr int T1_NS = St::radix(0), T1_R = T1 ? St::radix(1) : 0, T1_PITCH = T1_R + 1;
+  static constexpr int T1_ENTRIES = T1 ? T1_NS * T1_PITCH : 0;
+  static constexpr int BYTES = (ENTRIES + T1_ENTRIES) * (int)sizeof(C2<T>);
 };
 
 // copy the table layout above from the global W_L^q array (all threads of the block)
@@ -201,6 +213,16 @@ __device__ __forceinline__ void stage_tw(C2<T>* tab, const C2<T>* __restrict__ t
   for (int q = tid; q < TW::ENTRIES; q += nthreads) {
     if constexpr (TW::TWO) tab[q] = q < TW::S ? twg[q] : twg[(q - TW::S) * TW::S];
     else tab[q] = twg[q];
+  }
+  if constexpr (TW::T1) {
+    constexpr int STEP = 2 * (H / (TW::T1_NS * TW::T1_R));      // W_H^e = W_L^{2e}
+    for (int e = tid; e < TW::T1_ENTRIES; e += nthreads) {
+      const int kk = e / TW::T1_PITCH, r = e - kk * TW::T1_PITCH;
+      const int q = STEP * kk * r;                               // < 2H: kk, r < 16
+      C2<T> w = twg[q & (H - 1)];
+      if (q & H) { w.x = -w.x; w.y = -w.y; }
+      tab[TW::ENTRIES + e] = w;
+    }
   }
 }
 
@@ -251,12 +273,18 @@ __device__ __forceinline__ void fft_stage(C2<T> (&v)[P], C2<T>* lds, int base, i
         // w^r with w = W_H^{kk*H/(NS*R)}: one LDS lookup, powers by binary powering
         // (at most 4 products deep, ~4 ulp) -- few LDS reads and few live registers.
         C2<T> wp[R];
-        wp[1] = tw_at<T, H>(tab, (2 * (H / (NS * R))) * kk);
+        if constexpr (TwTab<T, H>::T1 && S == 1) {
+          const C2<T>* t1 = tab + TwTab<T, H>::ENTRIES + kk * TwTab<T, H>::T1_PITCH;
 #pragma unroll
-        for (int r = 2; r < R; ++r) {
-          const int hi = (r & (r - 1)) == 0 ? r / 2 : (1 << (31 - __builtin_clz(r)));   // r = hi + lo
-          const int lo = r - hi;
-          wp[r] = cmul<T>(wp[hi], wp[lo]);
+          for (int r = 1; r < R; ++r) wp[r] = t1[r];
+        } else {
+          wp[1] = tw_at<T, H>(tab, (2 * (H / (NS * R))) * kk);
+#pragma unroll
+          for (int r = 2; r < R; ++r) {
+            const int hi = (r & (r - 1)) == 0 ? r / 2 : (1 << (31 - __builtin_clz(r)));   // r = hi + lo
+            const int lo = r - hi;
+            wp[r] = cmul<T>(wp[hi], wp[lo]);
+          }
         }
 #pragma unroll
         for (int r = 1; r < R; ++r) a[b][r] = (DIR < 0) ? cmul<T>(a[b][r], wp[r]) : cmulc<T>(a[b][r], wp[r]);
@@ -322,12 +350,18 @@ __device__ __forceinline__ void fft_bfly(const C2<T> (&v)[P], C2<T> (&a)[P], int
       const int j = t + b * TT;
       const int kk = j & (NS - 1);
       C2<T> wp[R];
-      wp[1] = tw_at<T, H>(tab, (2 * (H / (NS * R))) * kk);
+      if constexpr (TwTab<T, H>::T1 && S == 1) {   // stage-1 powers from the block's table
+        const C2<T>* t1 = tab + TwTab<T, H>::ENTRIES + kk * TwTab<T, H>::T1_PITCH;
 #pragma unroll
-      for (int r = 2; r < R; ++r) {
-        const int hi = (r & (r - 1)) == 0 ? r / 2 : (1 << (31 - __builtin_clz(r)));
-        const int lo = r - hi;
-        wp[r] = cmul<T>(wp[hi], wp[lo]);
+        for (int r = 1; r < R; ++r) wp[r] = t1[r];
+      } else {
+        wp[1] = tw_at<T, H>(tab, (2 * (H / (NS * R))) * kk);
+#pragma unroll
+        for (int r = 2; r < R; ++r) {
+          const int hi = (r & (r - 1)) == 0 ? r / 2 : (1 << (31 - __builtin_clz(r)));
+          const int lo = r - hi;
+          wp[r] = cmul<T>(wp[hi], wp[lo]);
+        }
       }
 #pragma unroll
       for (int r = 1; r < R; ++r)
