@@ -237,6 +237,24 @@ __device__ __forceinline__ C2<T> tw_at(const C2<T>* __restrict__ tab, int q) {
   return w;
 }
 
+// W_L^{t + TT k} at a thread's positions (t < TT, t + TT k < H): the lane's W_L^t (one LDS
+// lookup, `wt`) times the wave-uniform W_L^{TT k}, read from the global half table `twg` by
+// scalar loads -- one LDS access per thread instead of one per point (the column pass is
+// bound by LDS traffic more than by VALU; ~1 ulp more rounding, so fp32 only: the fp64 plans
+// reproduce the reference's break iteration at tol 1e-10 and keep the exact table values).
+#ifndef HGP_POS_TW
+#define HGP_POS_TW 0   // measured slower: the scalar loads share lgkmcnt with the LDS exchanges
+#endif
+template <typename T, int H, int TT>
+__device__ __forceinline__ C2<T> tw_pos(const C2<T>* tab, const C2<T>* __restrict__ twg, C2<T> wt, int t, int k) {
+  if constexpr (HGP_POS_TW && std::is_same<T, float>::value) {   // fp64 keeps exact lookups
+    if (k == 0) return wt;
+    return cmul<T>(wt, twg[TT * k]);
+  } else {
+    return tw_at<T, H>(tab, t + TT * k);
+  }
+}
+
 // LDS address of logical element e (padding breaks the power-of-two strides of the
 // Stockham write pattern: one complex slot per 16).
 __device__ __forceinline__ int lds_phys(int e) { return e + (e >> 4); }

@@ -196,10 +196,8 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   C2<T>* lds = reinterpret_cast<C2<T>*>(smem_raw);
   C2<T>* tab = lds + Cfg::EX_ELEMS;
-  {
-    const C2<T>* __restrict__ twg = reinterpret_cast<const C2<T>*>(d.tw);
-    stage_tw<T, H>(tab, twg, threadIdx.x, Cfg::THREADS);
-  }
+  const C2<T>* __restrict__ twg = reinterpret_cast<const C2<T>*>(d.tw);
+  stage_tw<T, H>(tab, twg, threadIdx.x, Cfg::THREADS);
 
   const int tid = threadIdx.x;
   int l, t, lbase;
@@ -354,6 +352,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
     const int in_len = d.in.len;
     const int lim = in_len - 1;
     const bool fold = CAN_FOLD && in_len > H;
+    const C2<T> wt = tw_at<T, H>(tab, t);
 #pragma unroll
     for (int k = 0; k < P; ++k) {
       const int p = t + TT * k;
@@ -369,7 +368,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
         if (fold) c = load_hi(p);
       }
       va[k] = cadd<T>(a, c);
-      vb[k] = cmul<T>(csub<T>(a, c), tw_at<T, H>(tab, p));
+      vb[k] = cmul<T>(csub<T>(a, c), tw_pos<T, H, TT>(tab, twg, wt, t, k));
     }
   }
 
@@ -484,10 +483,11 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
     // registers or scratch) from the loads at the top of the kernel
     asm volatile("" : "+v"(t));
     if constexpr (LAY == LAY_STRIDED) asm volatile("" : "+v"(lc));
+    const C2<T> wt = tw_at<T, H>(tab, t);
 #pragma unroll
     for (int k = 0; k < P; ++k) {
       const int p = t + TT * k;
-      const C2<T> wo = cmulc<T>(vb[k], tw_at<T, H>(tab, p));
+      const C2<T> wo = cmulc<T>(vb[k], tw_pos<T, H, TT>(tab, twg, wt, t, k));
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
         const C2<T> y = hh == 0 ? cadd<T>(va[k], wo) : csub<T>(va[k], wo);

@@ -64,10 +64,8 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   C2<T>* lds = reinterpret_cast<C2<T>*>(smem_raw);
   C2<T>* tab = lds + Cfg::AREA;
-  {
-    const C2<T>* __restrict__ twg = reinterpret_cast<const C2<T>*>(d.tw);
-    stage_tw<T, H>(tab, twg, threadIdx.x, Cfg::THREADS);
-  }
+  const C2<T>* __restrict__ twg = reinterpret_cast<const C2<T>*>(d.tw);
+  stage_tw<T, H>(tab, twg, threadIdx.x, Cfg::THREADS);
   const int nrb = (d.Rn + C - 1) / C;
   const int q = blockIdx.x / nrb;
   const int rb = blockIdx.x - q * nrb;
@@ -94,8 +92,9 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
     va[k] = mk<T>(buf_ld<T>(ra, lo, so), buf_ld<T>(rb_, lo, so));
   }
   __syncthreads();   // twiddle table staged
-#pragma unroll
-  for (int k = 0; k < P; ++k) vb[k] = cmul<T>(va[k], tw_at<T, H>(tab, t + TT * k));
+  const C2<T> wt0 = tw_at<T, H>(tab, t);
+  #pragma unroll
+  for (int k = 0; k < P; ++k) vb[k] = cmul<T>(va[k], tw_pos<T, H, TT>(tab, twg, wt0, t, k));
 
   C2<T>* W = reinterpret_cast<C2<T>*>(d.out.ptr) + (int64_t)q * d.out.q_stride;
   const int64_t S0 = d.out.r_stride;
@@ -211,10 +210,8 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   C2<T>* lds = reinterpret_cast<C2<T>*>(smem_raw);
   C2<T>* tab = lds + Cfg::AREA;
-  {
-    const C2<T>* __restrict__ twg = reinterpret_cast<const C2<T>*>(d.tw);
-    stage_tw<T, H>(tab, twg, threadIdx.x, Cfg::THREADS);
-  }
+  const C2<T>* __restrict__ twg = reinterpret_cast<const C2<T>*>(d.tw);
+  stage_tw<T, H>(tab, twg, threadIdx.x, Cfg::THREADS);
   const int nrb = (d.Rn + C - 1) / C;
   const int q = blockIdx.x / nrb;
   const int rb = blockIdx.x - q * nrb;
@@ -309,10 +306,11 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
     __syncthreads();   // every group is done with its exchange image
     int tt = t;
     asm volatile("" : "+v"(tt));
+    const C2<T> wtc = tw_at<T, H>(tab, tt);
 #pragma unroll
     for (int k = 0; k < P; ++k) {
       const int p = tt + TT * k;
-      const C2<T> wo = cmulc<T>(vb[k], tw_at<T, H>(tab, p));
+      const C2<T> wo = cmulc<T>(vb[k], tw_pos<T, H, TT>(tab, twg, wtc, tt, k));
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
         const C2<T> y = hh == 0 ? cadd<T>(va[k], wo) : csub<T>(va[k], wo);
@@ -357,10 +355,11 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
   T dsum = 0;
   int tt = t;
   asm volatile("" : "+v"(tt));
+  const C2<T> wtc = tw_at<T, H>(tab, tt);
 #pragma unroll
   for (int k = 0; k < P; ++k) {
     const int p = tt + TT * k;
-    const C2<T> wo = cmulc<T>(vb[k], tw_at<T, H>(tab, p));
+    const C2<T> wo = cmulc<T>(vb[k], tw_pos<T, H, TT>(tab, twg, wtc, tt, k));
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
       const C2<T> y = hh == 0 ? cadd<T>(va[k], wo) : csub<T>(va[k], wo);
