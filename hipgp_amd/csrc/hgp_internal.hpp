@@ -48,6 +48,16 @@ hipError_t doubly_diag(int dtype, int ndim, const void* x, int64_t nobs, double 
 hipError_t meanfield_stats(int dtype, const void* kn, int64_t nrhs, int64_t Mp, const void* qm, const void* qS,
                            const void* y, const void* iv, const void* knn, const void* lsd, void* an, void* lam,
                            void* dm, hipStream_t s);
+// expanded grid n[a] tiled by blocks of side b[a] (nb[a] per axis); bs points per block, nbw
+// blocks per workgroup
+struct BlockGeom {
+  int d, bs, nbw;
+  int64_t nblk, Mp;
+  int64_t n[3], b[3], nb[3];
+};
+int block_geom(int ndim, const int64_t* dims, const int64_t* blocks, BlockGeom* g, const char** why);
+hipError_t block_stats(int dtype, const BlockGeom& g, const void* kn, int64_t nrhs, const void* iv, const void* S,
+                       void* gram, void* knSkn, hipStream_t s);
 hipError_t kuf_semi_grid(int dtype, int kind, int method, int ndim, const int64_t* m, const void* const* grids,
                          const void* x, int64_t nobs, double sig2, double ell, const void* nodes,
                          const void* weights, int npts, void* out, hipStream_t s);

@@ -13,6 +13,8 @@
 #include "hgp_internal.hpp"
 #include "../../include/hipgp.h"
 
+#include <algorithm>
+
 namespace hgp {
 
 constexpr int ST_THREADS = 256;
@@ -132,6 +134,215 @@ hipError_t meanfield_stats(int dtype, const void* kn, int64_t nrhs, int64_t Mp, 
                            void* dm, hipStream_t s) {
   if (dtype == HGP_F64) return meanfield_stats_t<double>(kn, nrhs, Mp, qm, qS, y, iv, knn, lsd, an, lam, dm, s);
   return meanfield_stats_t<float>(kn, nrhs, Mp, qm, qS, y, iv, knn, lsd, an, lam, dm, s);
+}
+
+
+// ---- block-diagonal family (BlockToeplitzGP, hipgp.py:527-691) ---------------------------------
+// Blocks tile the expanded grid (dims n_a, block sides b_a, util.py:79-119): block beta enumerates
+// the block grid C-order, point i the block C-order, flat index sum_a (c_a b_a + i_a) stride_a.
+//   gram[beta]  = sum_n iv_n k_{n,beta} k_{n,beta}^T        (bs x bs; hipgp.py:252-256, get_lam :669-685)
+//   knSkn[n]    = sum_beta k_{n,beta}^T S_beta k_{n,beta}    (compute_knSkn :661-664)
+// One workgroup owns NBW = min(16, max(1, 256 / bs^2)) consecutive blocks; the RHS are streamed in chunks
+// of 64 through an LDS tile K[n][col] (col = local block * bs + i, row pitch padded by one).
+// gram: each thread owns entries e = t + 256 r of the workgroup's contiguous gram slab, so the
+// bs^2-per-block write (the dominant HBM term for bs ~ 100) is fully coalesced.
+// knSkn: lane = RHS within the chunk, wave = row (local block, i): u = sum_j S[i][j] K[n][j] with
+// S wave-uniform, v = K[n][i] u accumulated per (wave, n, local block) in LDS by its only writer,
+// then summed over the 4 waves in order -> part[n][beta]; rows reduced by k_reduce_rows.
+// Every sum has a fixed order (deterministic).
+constexpr int BK_THREADS = 256;
+constexpr int BK_NB = 64;          // RHS per chunk
+constexpr int BK_MAXBS = 128;
+
+// LDS row pitch of the K tile: covers the 16 * TA gram tile columns (zero beyond ncol), odd
+__host__ __device__ inline int bk_pitch(int ncol, int TA) { return (ncol > 16 * TA ? ncol : 16 * TA) + 1; }
+
+// TA = 0: bs <= 16, nbw = 256 / bs^2 blocks per workgroup, one gram entry per thread.
+// TA >= 1: bs > 16, one block per workgroup, a 16 x 16 thread grid, thread (ti, tj) owning the
+// TA x TA register tile i = ti + 16 a, j = tj + 16 b (per RHS: TA + TA LDS reads, TA^2 FMAs).
+template <typename T, int TA>
+__global__ __launch_bounds__(BK_THREADS) void k_block_stats(BlockGeom g, const T* __restrict__ kn, int nrhs,
+                                                           const T* __restrict__ iv, const T* __restrict__ S,
+                                                           T* __restrict__ gram, T* __restrict__ part) {
+  extern __shared__ unsigned char smem_raw[];
+  T* smem = reinterpret_cast<T*>(smem_raw);
+  const int bs = g.bs, nbw = g.nbw;
+  const int ncol = nbw * bs, pitch = bk_pitch(ncol, TA);
+  T* Kt = smem;                                   // [BK_NB][pitch]
+  T* ivs = Kt + BK_NB * pitch;                    // [BK_NB]
+  T* Q = ivs + BK_NB;                             // [4][BK_NB][nbw]
+  const int64_t beta0 = (int64_t)blockIdx.x * nbw;
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  constexpr int NA = TA > 0 ? TA : 1;
+  T acc[NA][NA];
+#pragma unroll
+  for (int a = 0; a < NA; ++a)
+#pragma unroll
+    for (int b = 0; b < NA; ++b) acc[a][b] = 0;
+  // thread's gram coordinates
+  int gi, gj, gbl;
+  if (TA == 0) {
+    gbl = t / (bs * bs);
+    const int ij = t - gbl * bs * bs;
+    gi = ij / bs;
+    gj = ij - gi * bs;
+  } else {
+    gbl = 0;
+    gi = t >> 4;
+    gj = t & 15;
+  }
+  const bool gram_thread = gram != nullptr && gbl < nbw;
+  for (int n0 = 0; n0 < nrhs; n0 += BK_NB) {
+    const int nn = min(BK_NB, nrhs - n0);
+    for (int q = t; q < BK_NB * pitch; q += BK_THREADS) {
+      const int rn = q / pitch, col = q - rn * pitch;
+      const int bl = col / bs, i = col - bl * bs;
+      const int64_t beta = beta0 + bl;
+      T v = 0;
+      if (rn < nn && col < ncol && beta < g.nblk) {
+        int64_t rem = beta, irem = i, flat = 0, stride = 1;
+        for (int a = g.d - 1; a >= 0; --a) {
+          const int64_t c = rem % g.nb[a], ii = irem % g.b[a];
+          rem /= g.nb[a];
+          irem /= g.b[a];
+          flat += (c * g.b[a] + ii) * stride;
+          stride *= g.n[a];
+        }
+        v = kn[(int64_t)(n0 + rn) * g.Mp + flat];
+      }
+      Kt[q] = v;
+    }
+    if (t < BK_NB) ivs[t] = (t < nn && iv != nullptr) ? iv[n0 + t] : (T)0;   // iv may be NULL without gram
+    if (part != nullptr)
+      for (int q = t; q < 4 * BK_NB * nbw; q += BK_THREADS) Q[q] = 0;
+    __syncthreads();
+    if (gram_thread) {
+      const T* ki = Kt + gbl * bs + gi;
+      const T* kj = Kt + gbl * bs + gj;
+      for (int k = 0; k < nn; ++k) {
+        const T ivk = ivs[k];
+        T vi[NA], vj[NA];
+#pragma unroll
+        for (int a = 0; a < NA; ++a) {
+          vi[a] = ivk * ki[k * pitch + 16 * a];
+          vj[a] = kj[k * pitch + 16 * a];
+        }
+#pragma unroll
+        for (int a = 0; a < NA; ++a)
+#pragma unroll
+          for (int b = 0; b < NA; ++b) acc[a][b] += vi[a] * vj[b];
+      }
+    }
+    if (part != nullptr && lane < nn) {
+      const T* kr = Kt + lane * pitch;
+      for (int row = w; row < ncol; row += 4) {
+        const int bl = row / bs, i = row - bl * bs;
+        if (beta0 + bl >= g.nblk) continue;
+        const T* srow = S + ((beta0 + bl) * bs + i) * bs;
+        const T* kb = kr + bl * bs;
+        T u = 0;
+        for (int j = 0; j < bs; ++j) u += srow[j] * kb[j];
+        Q[(w * BK_NB + lane) * nbw + bl] += kb[i] * u;
+      }
+    }
+    __syncthreads();
+    if (part != nullptr) {
+      for (int q = t; q < nn * nbw; q += BK_THREADS) {
+        const int rn = q / nbw, bl = q - rn * nbw;
+        if (beta0 + bl < g.nblk) {
+          T s = 0;
+#pragma unroll
+          for (int ww = 0; ww < 4; ++ww) s += Q[(ww * BK_NB + rn) * nbw + bl];
+          part[(int64_t)(n0 + rn) * g.nblk + beta0 + bl] = s;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (gram_thread && beta0 + gbl < g.nblk) {
+    T* gb = gram + (beta0 + gbl) * bs * bs;
+#pragma unroll
+    for (int a = 0; a < NA; ++a)
+#pragma unroll
+      for (int b = 0; b < NA; ++b) {
+        const int i = gi + 16 * a, j = gj + 16 * b;
+        if (i < bs && j < bs) gb[i * bs + j] = acc[a][b];
+      }
+  }
+}
+
+template <typename T, int TA>
+void launch_block_stats(const BlockGeom& g, int64_t grid, const void* kn, int nrhs, const void* iv, const void* S,
+                        void* gram, void* part, hipStream_t s) {
+  const size_t lds = (size_t)(BK_NB * bk_pitch(g.nbw * g.bs, TA) + BK_NB + 4 * BK_NB * g.nbw) * sizeof(T);
+  if (lds > 65536)
+    (void)hipFuncSetAttribute((const void*)k_block_stats<T, TA>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL((k_block_stats<T, TA>), dim3((unsigned)grid), dim3(BK_THREADS), lds, s, g, (const T*)kn, nrhs,
+                     (const T*)iv, (const T*)S, (T*)gram, (T*)part);
+}
+
+template <typename T>
+hipError_t block_stats_t(const BlockGeom& g, const void* kn, int64_t nrhs, const void* iv, const void* S, void* gram,
+                         void* knSkn, hipStream_t s) {
+  const int64_t grid = (g.nblk + g.nbw - 1) / g.nbw;
+  T* part = nullptr;
+  if (knSkn != nullptr && nrhs > 0) {
+    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&part), (size_t)(nrhs * g.nblk) * sizeof(T), s);
+    if (e != hipSuccess) return e;
+  }
+  void* gp = gram;
+  if (nrhs == 0 && gram != nullptr) {     // empty batch: the sum over no observations
+    hipError_t e = hipMemsetAsync(gram, 0, (size_t)(g.nblk * g.bs * g.bs) * sizeof(T), s);
+    if (e != hipSuccess) return e;
+    gp = nullptr;
+  }
+  if (nrhs > 0) {
+    const int TA = g.bs <= 16 ? 0 : (g.bs + 15) / 16;
+    switch (TA) {
+      case 0: launch_block_stats<T, 0>(g, grid, kn, (int)nrhs, iv, S, gp, part, s); break;
+      case 2: launch_block_stats<T, 2>(g, grid, kn, (int)nrhs, iv, S, gp, part, s); break;
+      case 3: launch_block_stats<T, 3>(g, grid, kn, (int)nrhs, iv, S, gp, part, s); break;
+      case 4: launch_block_stats<T, 4>(g, grid, kn, (int)nrhs, iv, S, gp, part, s); break;
+      case 5: launch_block_stats<T, 5>(g, grid, kn, (int)nrhs, iv, S, gp, part, s); break;
+      case 6: launch_block_stats<T, 6>(g, grid, kn, (int)nrhs, iv, S, gp, part, s); break;
+      case 7: launch_block_stats<T, 7>(g, grid, kn, (int)nrhs, iv, S, gp, part, s); break;
+      default: launch_block_stats<T, 8>(g, grid, kn, (int)nrhs, iv, S, gp, part, s); break;
+    }
+    if (knSkn != nullptr) reduce_rows<T>(part, (int)g.nblk, (int)nrhs, knSkn, s);
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  if (part != nullptr) return hipFreeAsync(part, s);
+  return hipSuccess;
+}
+
+int block_geom(int ndim, const int64_t* dims, const int64_t* blocks, BlockGeom* g, const char** why) {
+  if (ndim < 2 || ndim > 3) { *why = "block family supports 2-D and 3-D grids only (util.py:88)"; return -1; }
+  g->d = ndim;
+  g->Mp = 1;
+  g->nblk = 1;
+  int64_t bs = 1;
+  for (int a = 0; a < ndim; ++a) {
+    if (dims[a] <= 0 || blocks[a] <= 0) { *why = "dims and blocks must be positive"; return -1; }
+    if (dims[a] % blocks[a] != 0) { *why = "each expanded-grid size must be divisible by its block side"; return -1; }
+    g->n[a] = dims[a];
+    g->b[a] = blocks[a];
+    g->nb[a] = dims[a] / blocks[a];
+    g->Mp *= dims[a];
+    g->nblk *= g->nb[a];
+    bs *= blocks[a];
+  }
+  if (bs > BK_MAXBS) { *why = "block size (points per block) must be <= 128"; return -1; }
+  g->bs = (int)bs;
+  // blocks per workgroup: fill the 256 gram threads, at most 16 (bounds the LDS of the knSkn partials)
+  g->nbw = (int)std::min<int64_t>(16, std::max<int64_t>(1, BK_THREADS / (bs * bs)));
+  return 0;
+}
+
+hipError_t block_stats(int dtype, const BlockGeom& g, const void* kn, int64_t nrhs, const void* iv, const void* S,
+                       void* gram, void* knSkn, hipStream_t s) {
+  if (dtype == HGP_F64) return block_stats_t<double>(g, kn, nrhs, iv, S, gram, knSkn, s);
+  return block_stats_t<float>(g, kn, nrhs, iv, S, gram, knSkn, s);
 }
 
 }  // namespace hgp

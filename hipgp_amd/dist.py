@@ -7,9 +7,10 @@ for its own rows with NO collective inside the solve.  Two places couple ranks:
 * the all-RHS break rule of `cg.py:70` — `ToeplitzPlan.pcg_allranks` applies it exactly with one
   all-reduce(MIN) of an int flag per iteration (only when `exact_break=True`; with the usual
   fp32 / tol 1e-8 it never fires and ranks run `maxiter` steps on their own);
-* the mean-field natural-gradient statistics (`hipgp.py:234-250`): sum_n a_n, sum_n ivar kn^2
-  and -sum_n ivar (kn.m - y) kn — one all-reduce(SUM) of a packed (2M' + 1) buffer per
-  minibatch, after which every rank holds identical theta gradients.
+* the natural-gradient statistics (`hipgp.py:234-266`): sum_n a_n, -sum_n ivar (kn.m - y) kn and
+  sum_n ivar kn^2 (mean-field) or the per-block grams sum_n ivar kn_blk kn_blk^T (block family)
+  — one all-reduce(SUM) of a packed buffer per minibatch, after which every rank holds identical
+  theta gradients.
 
 Backend: "nccl" (= RCCL over xGMI on ROCm) on GPUs, "gloo" for the CPU tests.
 """
@@ -46,8 +47,9 @@ def allreduce_stats(stats, group=None):
         buf = host.to(lam.device)
     else:
         dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
-    k = lam.numel()
-    return {"lam_sum": buf[:k], "dm_sum": buf[k:2 * k], "an_sum": buf[2 * k], "n": int(round(float(buf[2 * k + 1])))}
+    k, kd = lam.numel(), dm.numel()     # lam_sum: (M',) mean-field or (nblk, bs, bs) block gram
+    return {"lam_sum": buf[:k].reshape(lam.shape), "dm_sum": buf[k:k + kd], "an_sum": buf[k + kd],
+            "n": int(round(float(buf[k + kd + 1])))}
 
 
 def sharded_compute_kn(model, Knm_local, maxiter_cg=20, tol=1e-8, exact_break=False, group=None, Kmm=None):

@@ -11,9 +11,12 @@ The natural-gradient statistics are split into per-RHS sums (`batch_stats`) and 
 built from them (`apply_stats`), so a caller that shards the minibatch over GPUs
 (`hipgp_amd.dist`) all-reduces exactly those sums.
 
-Not built here (OUT of the hot path): integrated observations (row f2), block /
-full-rank variational families, kernel-hyper-parameter learning through the solve (row f4),
-`batch_solve`'s dense M'xM' system.
+Line-integral observations come from the fused kernels of `hipgp_amd.kuf`.
+The block-diagonal family's statistics (per-block grams, kn^T S kn) are the fused kernel
+hgp_block_stats.
+
+Not built here (OUT of the hot path): the full-rank variational family,
+kernel-hyper-parameter learning through the solve (row f4), `batch_solve`'s dense M'xM' system.
 """
 import numpy as np
 import torch
@@ -206,7 +209,9 @@ class ToeplitzInducingGP(SviGP):
             kn = self.compute_kn(Knm, maxiter_cg=maxiter_cg, Kmm=Kmm)
         ivar, log_sd = self.noise_terms(noise_std_batch)
         if noise_std_batch is not None:
-            ivar, log_sd = ivar.squeeze(), log_sd.squeeze()
+            # reference shapes (hipgp.py:396-398): ivar squeezed, log(noise_std) kept (bsz, 1), so
+            # with per-observation noise a_n broadcasts to (bsz, bsz); its mean is the ELBO term
+            ivar = ivar.squeeze()
         mse = (kn.matmul(qm).squeeze() - ybatch.squeeze()) ** 2
         variance = Knn_diag.squeeze() - torch.sum(kn * kn, dim=-1).squeeze() + self.compute_knSkn(kn, qS)
         if print_debug_info:
@@ -358,6 +363,209 @@ class MeanFieldToeplitzGP(ToeplitzInducingGP):
             lam_diag = bscale * stats["lam_sum"] + 1
             dS = -.5 * lam_diag[:, None] - self.global_theta2.data
             deta1 = dm + dS * (-2 * qm)
+        self.global_theta1.grad = -deta1
+        self.global_theta2.grad = -dS
+        return elbo
+
+
+# ---- block-diagonal variational family -------------------------------------------------------
+def block_chunks(dims, chunk_sizes):
+    """Block ordering of a 2-D / 3-D grid (`ziggy/misc/util.py:79-130`, define_block_chunks):
+    blocks C-order over the block grid, points C-order inside a block.  Returns
+    (block_idx (num_blocks, block_size) int64 on the CPU, to_blocks, from_blocks); the two maps are
+    reshape/permute views (no gather table on the device)."""
+    dims, chunks = [int(d) for d in dims], [int(c) for c in chunk_sizes]
+    assert len(dims) == len(chunks), "xgrids ndim = {}, chunk_sizes ndim = {}".format(len(dims), len(chunks))
+    assert len(dims) in (2, 3), "only 2d or 3d inputs"
+    for d, (n, c) in enumerate(zip(dims, chunks)):
+        assert n % c == 0, "xgrid-{}={} not divis by chunk_size={}".format(d, n, c)
+    nd = len(dims)
+    split = []
+    for n, c in zip(dims, chunks):
+        split += [n // c, c]
+    perm = [2 * a for a in range(nd)] + [2 * a + 1 for a in range(nd)]
+    inv = [perm.index(a) for a in range(2 * nd)]
+    nblk, bs = int(np.prod([n // c for n, c in zip(dims, chunks)])), int(np.prod(chunks))
+
+    def to_blocks(m):
+        lead = m.shape[:-1]
+        t = m.reshape(*lead, *split).permute(*range(len(lead)), *[len(lead) + p for p in perm])
+        return t.reshape(*lead, nblk, bs)
+
+    def from_blocks(block_m):
+        b = block_m.shape[0]
+        t = block_m.reshape(b, *[split[p] for p in perm]).permute(0, *[1 + p for p in inv])
+        return t.reshape(b, -1)
+
+    block_idx = to_blocks(torch.arange(int(np.prod(dims))))
+    return block_idx, to_blocks, from_blocks
+
+
+def block_kl_to_standard(blk_m, blk_S):
+    """KL(N(m, blockdiag S) || N(0, I)) with a 1e-4 nugget in the log det (`ziggy/misc/stats.py:15-29`)."""
+    eye = torch.eye(blk_S.shape[1], dtype=blk_S.dtype, device=blk_S.device)
+    L = torch.linalg.cholesky(blk_S + 1e-4 * eye)
+    lndet = 2.0 * torch.sum(torch.log(torch.diagonal(L, dim1=-2, dim2=-1)))
+    n_blk, blk_size, _ = blk_S.shape
+    Strace = torch.sum(torch.diagonal(blk_S, dim1=-2, dim2=-1))
+    return .5 * (Strace + torch.sum(blk_m * blk_m) - lndet - n_blk * blk_size)
+
+
+class BlockToeplitzGP(ToeplitzInducingGP):
+    """Block-diagonal variational covariance over neighbouring points of the (expanded) grid
+    (`hipgp.py:527-691`).  qm lives in grid order, qS / theta2 in block order
+    (num_blocks, block_size, block_size).  On the device the per-block statistics are one fused
+    kernel (hgp_block_stats): sum_n ivar_n kn_blk kn_blk^T and kn^T S kn in a single read of kn."""
+
+    def __init__(self, kernel, xgrids, num_obs, xblock_size=10, block_sizes=None, sig2_init=1., ell_init=.05,
+                 noise2_init=1., init_Svar=.1, learn_kernel=False, learn_noise=False, dtype=torch.float,
+                 whitened_type='ziggy', parameterization='expectation-family', jitter_val=1e-3):
+        super().__init__(kernel, xgrids, num_obs, sig2_init=sig2_init, ell_init=ell_init,
+                         noise2_init=noise2_init, learn_kernel=learn_kernel, learn_noise=learn_noise,
+                         dtype=dtype, whitened_type=whitened_type, parameterization=parameterization,
+                         jitter_val=jitter_val)
+        input_dim = len(xgrids)
+        if block_sizes is not None:
+            assert input_dim == len(block_sizes), "xgrids ndim = {}, block ndim = {}".format(input_dim, len(block_sizes))
+        else:
+            block_sizes = [xblock_size for _ in range(input_dim)]
+        if self.whitened_type == 'cholesky':
+            self.block_dims = [len(x) for x in xgrids]
+        else:      # blocks of the expanded grid arange(2m - 2)  (hipgp.py:599-601, 629-634)
+            self.block_dims = [2 * len(x) - 2 for x in xgrids]
+        self.block_sides = [int(b) for b in block_sizes]
+        self.block_idx, self.to_blocks, self.from_blocks = block_chunks(self.block_dims, self.block_sides)
+        self.num_blocks, self.block_size = self.block_idx.shape
+        eye = torch.eye(self.block_size, dtype=dtype)
+        col = lambda: torch.zeros(self.Mprime, 1, dtype=dtype)
+        if parameterization == 'standard':
+            self.global_m = nn.Parameter(nn.init.xavier_normal_(col()), requires_grad=True)
+            self.global_S = nn.Parameter((init_Svar * eye)[None].repeat(self.num_blocks, 1, 1), requires_grad=True)
+        else:
+            self.global_theta1 = nn.Parameter(nn.init.xavier_normal_(col()), requires_grad=True)
+            self.global_theta2 = nn.Parameter(((-.5 / init_Svar) * eye)[None].repeat(self.num_blocks, 1, 1),
+                                              requires_grad=True)
+
+    @property
+    def name(self):
+        return 'block'
+
+    def get_expanded_xgrids(self, xgrids):
+        return [torch.arange(2 * len(x) - 2) for x in xgrids]
+
+    def standard_variational_params(self):
+        if self.parameterization == 'standard':
+            return self.global_m, self.global_S
+        S = torch.inverse(-2 * self.global_theta2)                      # block inverse
+        m = self.block_diag_multiply(S, self.global_theta1.t()).t()
+        return m, S
+
+    def block_diag_multiply(self, S_block, v):
+        """rows of v (bsz, M') times the block-diagonal S (num_blocks, bs, bs)  (`hipgp.py:645-656`)."""
+        Sv_block = S_block.matmul(self.to_blocks(v)[..., None])
+        return self.from_blocks(Sv_block)
+
+    def get_S_from_lam(self, lam):
+        return torch.inverse(lam)
+
+    def _block_kernel(self, kn, ivar=None, S=None, gram=True, knSkn=True):
+        import ctypes
+        from hipgp_amd import _lib
+        B, Mp = kn.shape
+        dev, dt = kn.device, kn.dtype
+        nd = len(self.block_dims)
+        dims = (ctypes.c_int64 * nd)(*self.block_dims)
+        blks = (ctypes.c_int64 * nd)(*self.block_sides)
+        knc = kn.detach().contiguous()
+        p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
+        ivv = None if ivar is None else torch.as_tensor(ivar, dtype=dt, device=dev).reshape(-1).expand(B).contiguous()
+        Sc = None if S is None else S.detach().to(dt).contiguous()
+        G = torch.empty(self.num_blocks, self.block_size, self.block_size, dtype=dt, device=dev) if gram else None
+        q = torch.empty(B, dtype=dt, device=dev) if knSkn else None
+        _lib.check(_lib.lib().hgp_block_stats(_lib.dtype_code(dt), nd, dims, blks, p(knc), B, p(ivv), p(Sc),
+                                              p(G), p(q), _lib.stream_ptr(dev)))
+        return G, q
+
+    def compute_knSkn(self, kn, qS):
+        """kn_n^T S kn_n per row (`hipgp.py:661-664`)."""
+        if kn.is_cuda and not (torch.is_grad_enabled() and (kn.requires_grad or qS.requires_grad)):
+            return self._block_kernel(kn, S=qS, gram=False)[1].squeeze()
+        Skn = self.block_diag_multiply(qS, kn)
+        return torch.sum(kn * Skn, dim=-1).squeeze()
+
+    def get_identity_for_lam(self):
+        return torch.eye(self.block_size, device=self.xgrids[0].device, dtype=self.dtype)
+
+    def get_lam(self, ivar_noise, kn, bscale=1, add_identity=True):
+        """bscale sum_n ivar_n kn_blk kn_blk^T (+ I), (num_blocks, bs, bs)  (`hipgp.py:669-685`)."""
+        if kn.is_cuda:
+            G = self._block_kernel(kn, ivar=ivar_noise, knSkn=False)[0]
+        else:
+            blk_kn = self.to_blocks(kn).transpose(0, 1)
+            G = torch.matmul(blk_kn.transpose(1, 2), ivar_noise * blk_kn)
+        return bscale * G + (self.get_identity_for_lam() if add_identity else 0)
+
+    def get_kl_to_prior(self, qm=None, qS=None):
+        if qm is None or qS is None:
+            qm, qS = self.standard_variational_params()
+        return block_kl_to_standard(qm, qS)
+
+    # ---- natural gradient as batch sums + update (sharding-friendly) ------------------------
+    def batch_stats(self, kn, ybatch, Knn_diag, noise_std_batch=None):
+        """Sums over this minibatch (or this rank's shard of it):
+           an_sum  = sum_n a_n                                         `hipgp.py:370-414`
+           lam_sum = sum_n ivar_n kn_blk kn_blk^T   (num_blocks, bs, bs)  `hipgp.py:252-256`
+           dm_sum  = -sum_n ivar_n (kn_n.m - y_n) kn_n   (M',)          `hipgp.py:234-236`"""
+        with torch.no_grad():
+            qm, qS = self.standard_variational_params()
+            qm, qS = qm.detach(), qS.detach()
+            ivar, log_sd = self.noise_terms(noise_std_batch)
+            B = kn.shape[0]
+            if kn.is_cuda:
+                import ctypes
+                from hipgp_amd import _lib
+                dev, dt = kn.device, kn.dtype
+                colv = lambda v: torch.as_tensor(v, dtype=dt, device=dev).reshape(-1).expand(B).contiguous()
+                G, knSkn = self._block_kernel(kn, ivar=ivar, S=qS)
+                # a_n without the kn S kn term and dm from the streaming row/column passes
+                knc = kn.detach().contiguous()
+                zero = torch.zeros(kn.shape[1], dtype=dt, device=dev)
+                qmv = qm.reshape(-1).to(dt).contiguous()
+                y, iv, kd, lsd = colv(ybatch), colv(ivar), colv(Knn_diag), colv(log_sd)
+                an = torch.empty(B, dtype=dt, device=dev)
+                lam_diag = torch.empty(kn.shape[1], dtype=dt, device=dev)
+                dm = torch.empty(kn.shape[1], dtype=dt, device=dev)
+                p = lambda t: ctypes.c_void_p(t.data_ptr())
+                _lib.check(_lib.lib().hgp_meanfield_stats(_lib.dtype_code(dt), p(knc), B, kn.shape[1], p(qmv),
+                                                          p(zero), p(y), p(iv), p(kd), p(lsd), p(an), p(lam_diag),
+                                                          p(dm), _lib.stream_ptr(dev)))
+                an = an - 0.5 * iv * knSkn
+                return {"an_sum": an.sum(), "lam_sum": G, "dm_sum": dm, "n": B}
+            # CPU tensors only reach here in the gloo host-logic tests
+            y = ybatch.reshape(-1)
+            knm = kn.matmul(qm).reshape(-1)
+            knSkn = torch.sum(kn * self.block_diag_multiply(qS, kn), dim=-1)
+            iv = torch.as_tensor(ivar, dtype=kn.dtype).reshape(-1).expand(B)
+            lsd = torch.as_tensor(log_sd, dtype=kn.dtype).reshape(-1).expand(B)
+            an = -0.5 * iv * ((knm - y) ** 2 + Knn_diag.reshape(-1) - (kn * kn).sum(-1) + knSkn) - lsd - 0.5 * LN_2PI
+            blk_kn = self.to_blocks(kn).transpose(0, 1)                     # (nblk, B, bs)
+            G = torch.matmul(blk_kn.transpose(1, 2), iv[None, :, None] * blk_kn)
+            dm_sum = -((iv * (knm - y))[None, :].matmul(kn)).reshape(-1)
+        return {"an_sum": an.sum(), "lam_sum": G, "dm_sum": dm_sum, "n": B}
+
+    def apply_stats(self, stats, bsz):
+        """ELBO estimate and theta grads from (all-reduced) batch sums of `bsz` observations
+        (`hipgp.py:222-276`, 'block' branch)."""
+        qm, qS = self.standard_variational_params()
+        with torch.no_grad():
+            qm, qS = qm.detach(), qS.detach()
+            bscale = self.N / bsz
+            elbo = stats["an_sum"] / bsz - self.get_kl_to_prior(qm, qS) / self.N
+            dm = bscale * stats["dm_sum"][:, None] - qm
+            lam_block = bscale * stats["lam_sum"] + self.get_identity_for_lam().to(qm.device)
+            dS = -.5 * lam_block - self.global_theta2.data
+            dSdeta1 = self.block_diag_multiply(dS, -2 * qm[None, :, 0])
+            deta1 = dm + dSdeta1.squeeze().unsqueeze(-1)
         self.global_theta1.grad = -deta1
         self.global_theta2.grad = -dS
         return elbo

@@ -158,6 +158,18 @@ int hgp_meanfield_stats(int dtype, const void* kn, int64_t nrhs, int64_t Mp, con
                         const void* qS, const void* y, const void* ivar, const void* Knn_diag,
                         const void* log_sd, void* an, void* lam, void* dm, void* hip_stream);
 
+/* Block-diagonal variational family (BlockToeplitzGP, ziggy/hipgp.py:527-691), SURVEY §8(f) row 3.
+ * The expanded grid dims[ndim] (ndim 2 or 3, n_a = 2 m_a - 2) is tiled by blocks[ndim] (each n_a
+ * divisible by blocks[a]; points per block bs = prod blocks <= 128), blocks enumerated C-order
+ * over the block grid and points C-order inside a block (ziggy/misc/util.py:79-119).
+ *   gram[nblk][bs][bs] = sum_n ivar_n kn_{n,blk} kn_{n,blk}^T     (hipgp.py:252-256, get_lam :669-685)
+ *   knSkn[nrhs]        = sum_blk kn_{n,blk}^T S_blk kn_{n,blk}    (compute_knSkn :661-664; S [nblk][bs][bs])
+ * kn (nrhs, M') row layout; gram or knSkn may be NULL to skip that output (then ivar resp. S may
+ * be NULL).  gram is the per-shard sum RCCL all-reduces across RHS shards.  Deterministic. */
+int hgp_block_stats(int dtype, int ndim, const int64_t* dims, const int64_t* blocks, const void* kn,
+                    int64_t nrhs, const void* ivar, const void* S, void* gram, void* knSkn,
+                    void* hip_stream);
+
 /* Sizes of a plan: M, M' and the padded FFT lengths per axis (K-type and R-type ops). */
 int hgp_plan_info(const hgp_plan* plan, int64_t* M, int64_t* Mprime, int64_t* L_K,
                   int64_t* L_R);

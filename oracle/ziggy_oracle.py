@@ -281,3 +281,69 @@ def compute_kn(T, Knm, maxiter_cg=10, tol=1e-8):
     """`hipgp.py:117-146` (ziggy whitening): kn = R^T K^{-1} Knm^T."""
     d0 = T.solve(Knm, do_precond=True, maxiter=maxiter_cg, tol=tol)
     return T.matmul_RT(d0)
+
+
+# --------------------------------------------------------------------------------------
+# block-diagonal variational family (ziggy/hipgp.py:527-691, ziggy/misc/util.py:79-130)
+# --------------------------------------------------------------------------------------
+def block_index(dims, blocks):
+    """(num_blocks, block_size) table of flat indices into the (expanded) grid `dims`:
+    blocks enumerated C-order over the block grid, points C-order inside a block
+    (`util.py:79-119`, `define_block_chunks`; the ziggy family blocks the expanded grid
+    `arange(2m-2)`, `hipgp.py:599-601,629-634`)."""
+    dims, blocks = tuple(int(d) for d in dims), tuple(int(b) for b in blocks)
+    assert len(dims) in (2, 3) and len(dims) == len(blocks)
+    assert all(d % b == 0 for d, b in zip(dims, blocks)), (dims, blocks)
+    flat = np.arange(int(np.prod(dims))).reshape(dims)
+    nb = [d // b for d, b in zip(dims, blocks)]
+    shp = []
+    for n, b in zip(nb, blocks):
+        shp += [n, b]
+    t = flat.reshape(shp)                         # (n0, b0, n1, b1[, n2, b2])
+    d = len(dims)
+    t = t.transpose([2 * i for i in range(d)] + [2 * i + 1 for i in range(d)])
+    return t.reshape(int(np.prod(nb)), int(np.prod(blocks)))
+
+
+def block_diag_multiply(S, v, idx):
+    """`hipgp.py:645-656`: rows of v (bsz, M') times the block-diagonal S (nb, bs, bs)."""
+    vb = v[:, idx]                                  # (bsz, nb, bs)
+    out = np.empty_like(v)
+    out[:, idx] = np.einsum("kij,bkj->bki", S, vb)
+    return out
+
+
+def block_kl_to_standard(m, S):
+    """`stats.py:15-29`: KL(N(m, blockdiag S) || N(0, I)) with the 1e-4 nugget in the log det."""
+    bs = S.shape[1]
+    L = np.linalg.cholesky(S + 1e-4 * np.eye(bs)[None])
+    lndet = 2.0 * np.sum(np.log(np.diagonal(L, axis1=-2, axis2=-1)))
+    return 0.5 * (np.trace(S, axis1=-2, axis2=-1).sum() + np.sum(m * m) - lndet - S.shape[0] * bs)
+
+
+def block_elbo_and_grad(kn, y, Knn_diag, theta1, theta2, idx, N, ivar, log_sd):
+    """BlockToeplitzGP ELBO estimate and natural-gradient theta grads given kn (bsz, M')
+    (`hipgp.py:194-276` 'block' branch, `compute_batch_an` :370-414, `standard_variational_params`
+    :636-643, `compute_knSkn` :661-664, `get_kl_to_prior` :687-691).  ivar/log_sd are scalars
+    (shared noise) or (bsz,) arrays (per-observation noise).
+    Returns (elbo, theta1_grad (M',1), theta2_grad (nb,bs,bs), batch_an, knSkn)."""
+    bsz = kn.shape[0]
+    S = np.linalg.inv(-2 * theta2)
+    qm = block_diag_multiply(S, theta1.T, idx).T                    # (M', 1)
+    knm = (kn @ qm).reshape(-1)
+    knSkn = np.sum(kn * block_diag_multiply(S, kn, idx), axis=-1)
+    iv = np.broadcast_to(np.asarray(ivar, dtype=kn.dtype).reshape(-1), (bsz,))
+    lsd = np.broadcast_to(np.asarray(log_sd, dtype=kn.dtype).reshape(-1), (bsz,))
+    y = y.reshape(-1)
+    an = (-0.5 * iv * ((knm - y) ** 2 + Knn_diag.reshape(-1) - np.sum(kn * kn, axis=-1) + knSkn)
+          - lsd - 0.5 * np.log(2 * np.pi))
+    elbo = np.mean(an) - block_kl_to_standard(qm, S) / N
+    bscale = N / bsz
+    bdiff = iv * (knm - y)
+    dm = bscale * (-(bdiff[None, :] @ kn).T) - qm
+    kb = kn[:, idx]                                                  # (bsz, nb, bs)
+    G = np.einsum("b,bki,bkj->kij", iv, kb, kb)
+    lam = bscale * G + np.eye(idx.shape[1])[None]
+    dS = -0.5 * lam - theta2
+    deta1 = dm + block_diag_multiply(dS, -2 * qm.T, idx).T
+    return elbo, -deta1, -dS, an, knSkn

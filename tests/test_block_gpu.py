@@ -1,0 +1,133 @@
+"""Block-diagonal variational family on the GPU: the fused hgp_block_stats
+kernel (per-block grams sum_n ivar kn_blk kn_blk^T and kn^T S kn) against the torch expression of
+the same sums, and BlockToeplitzGP.elbo_and_grad / predict with kn from the HIP path against the
+reference's own outputs (G11 2-D shared noise, G12 3-D per-observation noise)."""
+import numpy as np
+import pytest
+import torch
+
+from block_cases import block_model, noise_of
+from golden_cases import load, rel_err
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _ref_stats(kn, iv, S, idx):
+    kb = kn[:, idx]                                               # (B, nblk, bs)
+    G = torch.einsum("b,bki,bkj->kij", iv, kb, kb)
+    q = torch.einsum("bki,kij,bkj->b", kb, S, kb)
+    return G, q
+
+
+@pytest.mark.parametrize("dims,blocks,B", [
+    ((20, 16), (4, 4), 48),         # bs 16 (one gram entry per thread, one block per workgroup)
+    ((10, 8, 6), (2, 2, 3), 40),    # 3-D, bs 12
+    ((30, 14), (2, 2), 70),         # bs 4: 16 blocks per workgroup, two RHS chunks
+    ((18, 6), (3, 1), 5),           # bs 3, ragged last workgroup
+    ((40, 30), (10, 10), 33),       # bs 100 (the experiments' 10x10 blocks), 7x7 register tiles
+    ((16, 32), (8, 16), 130),       # bs 128 (the maximum), three RHS chunks
+    ((6, 6), (1, 1), 7),            # bs 1
+])
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_block_stats_kernel(dims, blocks, B, dtype):
+    from hipgp_amd.ziggy.hipgp import BlockToeplitzGP, block_chunks
+    idx, _, _ = block_chunks(dims, blocks)
+    g = torch.Generator().manual_seed(B)
+    kn = torch.randn(B, int(np.prod(dims)), generator=g, dtype=torch.float64)
+    iv = torch.rand(B, generator=g, dtype=torch.float64) + .5
+    A = torch.randn(idx.shape[0], idx.shape[1], idx.shape[1], generator=g, dtype=torch.float64)
+    S = A @ A.transpose(1, 2) / idx.shape[1]
+    Gr, qr = _ref_stats(kn, iv, S, idx)
+
+    class _M:
+        pass
+    m = _M()
+    m.block_dims, m.block_sides = list(dims), list(blocks)
+    m.num_blocks, m.block_size = idx.shape
+    G, q = BlockToeplitzGP._block_kernel(m, kn.to(DEV, dtype), ivar=iv.to(DEV, dtype), S=S.to(DEV, dtype))
+    tol = 1e-12 if dtype == torch.float64 else 2e-6
+    assert rel_err(G.double().cpu().numpy(), Gr.numpy()) < tol
+    assert rel_err(q.double().cpu().numpy(), qr.numpy()) < tol
+    # deterministic: a second launch is bit-identical
+    G2, q2 = BlockToeplitzGP._block_kernel(m, kn.to(DEV, dtype), ivar=iv.to(DEV, dtype), S=S.to(DEV, dtype))
+    assert torch.equal(G, G2) and torch.equal(q, q2)
+
+
+def test_block_stats_edge_cases():
+    import ctypes
+    from hipgp_amd import _lib
+    L = _lib.lib()
+    dims = (ctypes.c_int64 * 2)(20, 16)
+    G = torch.full((20, 16, 16), 7., dtype=torch.float64, device=DEV)
+    # empty batch: the gram is the sum over no observations
+    _lib.check(L.hgp_block_stats(_lib.HGP_F64, 2, dims, (ctypes.c_int64 * 2)(4, 4), None, 0, None, None,
+                                 ctypes.c_void_p(G.data_ptr()), None, _lib.stream_ptr(G.device)))
+    assert float(G.abs().max()) == 0.
+    # refused shapes: not divisible, block > 128 points, 1-D
+    for nd, d, b in ((2, (20, 16), (3, 4)), (2, (32, 32), (16, 16)), (1, (20,), (4,))):
+        rc = L.hgp_block_stats(_lib.HGP_F64, nd, (ctypes.c_int64 * nd)(*d), (ctypes.c_int64 * nd)(*b),
+                               ctypes.c_void_p(G.data_ptr()), 1, ctypes.c_void_p(G.data_ptr()), None,
+                               ctypes.c_void_p(G.data_ptr()), None, None)
+        assert rc == -4, (nd, d, b)
+
+
+@pytest.mark.parametrize("name", ["G11", "G12"])
+def test_block_model_reference_fp64(name):
+    """hipgp.py:117-146 (kn), 194-276 (elbo_and_grad, 'block'), 416-446 (predict), fp64."""
+    mod, fx = block_model(name, device=DEV)
+    x = torch.tensor(fx["xobs"], device=DEV)
+    y = torch.tensor(fx["yobs"], device=DEV)
+    nstd = noise_of(fx, device=DEV)
+    Knm, _ = mod._make_grams(x)
+    kn = mod.compute_kn(Knm, maxiter_cg=20)
+    assert rel_err(kn.cpu().numpy(), fx["kn"]) < 1e-8
+    qm, qS = mod.standard_variational_params()
+    assert rel_err(mod.compute_knSkn(kn, qS.detach()).cpu().numpy(), fx["knSkn"]) < 1e-8
+    elbo = mod.elbo_and_grad(x, y, noise_std_batch=nstd, maxiter_cg=20)
+    assert abs(float(elbo) - float(fx["elbo"])) < 1e-8 * abs(float(fx["elbo"]))
+    assert rel_err(mod.global_theta1.grad.cpu().numpy(), fx["theta1_grad"]) < 1e-7
+    assert rel_err(mod.global_theta2.grad.cpu().numpy(), fx["theta2_grad"]) < 1e-7
+    mu, sig = mod.predict(x[:20], maxiter_cg=50)
+    assert rel_err(mu.numpy(), fx["pred_mu"]) < 1e-7
+    assert rel_err(sig.numpy(), fx["pred_sig"]) < 1e-7
+
+
+@pytest.mark.parametrize("name", ["G11", "G12"])
+def test_block_model_fp32(name):
+    """fp32 model against the fp64 reference: no worse than 4x the reference's own fp32 error
+     on the theta gradients and the ELBO."""
+    fx32, fx64 = load(name, "f32"), load(name, "f64")
+    mod, _ = block_model(name, tag="f32", dtype=torch.float32, device=DEV)
+    x = torch.tensor(fx32["xobs"], device=DEV)
+    y = torch.tensor(fx32["yobs"], device=DEV)
+    nstd = noise_of(fx32, dtype=torch.float32, device=DEV)
+    elbo = float(mod.elbo_and_grad(x, y, noise_std_batch=nstd, maxiter_cg=20))
+    for key, mine in (("theta1_grad", mod.global_theta1.grad), ("theta2_grad", mod.global_theta2.grad)):
+        e_me = np.linalg.norm(mine.double().cpu().numpy() - fx64[key])
+        e_ref = np.linalg.norm(fx32[key].astype(np.float64) - fx64[key])
+        assert e_me <= 4 * e_ref + 1e-6 * np.linalg.norm(fx64[key]), (key, e_me, e_ref)
+    e_ref = abs(float(fx32["elbo"]) - float(fx64["elbo"]))
+    assert abs(elbo - float(fx64["elbo"])) <= 4 * e_ref + 1e-6 * abs(float(fx64["elbo"]))
+
+
+def test_block_stats_large_grid():
+    """Expanded 1000 x 1000 grid (m = 501), 10 x 10 blocks (10^4 blocks of 100 points), 32 RHS,
+    fp32: 64 sampled blocks of the kernel's grams and the full kn^T S kn against torch fp64."""
+    import ziggy.hipgp as hg
+    import ziggy.kernels as zk
+    grids = [torch.linspace(-1, 1, 501, dtype=torch.float32)] * 2
+    mod = hg.BlockToeplitzGP(zk.SqExp(dtype=torch.float32), grids, num_obs=1000, xblock_size=10,
+                             dtype=torch.float32).cuda_params(0)
+    assert (mod.num_blocks, mod.block_size) == (10000, 100)
+    g = torch.Generator(device=DEV).manual_seed(3)
+    kn = torch.randn(32, mod.Mprime, generator=g, device=DEV)
+    iv = torch.rand(32, generator=g, device=DEV) + .5
+    S = torch.randn(mod.num_blocks, 100, 100, generator=g, device=DEV) * .1
+    G, q = mod._block_kernel(kn, ivar=iv, S=S)
+    pick = torch.randint(0, mod.num_blocks, (64,), generator=g, device=DEV)
+    kb = kn.double()[:, mod.block_idx.to(DEV)[pick]]
+    Gr = torch.einsum("b,bki,bkj->kij", iv.double(), kb, kb)
+    assert rel_err(G[pick].double().cpu().numpy(), Gr.cpu().numpy()) < 2e-6
+    qr = torch.sum(kn.double() * mod.block_diag_multiply(S.double(), kn.double()), dim=-1)
+    assert rel_err(q.double().cpu().numpy(), qr.cpu().numpy()) < 1e-5
