@@ -70,7 +70,7 @@ def lib():
         "hgp_kuf_semi_sqexp": (i32, [i32, i32, pi64, ctypes.POINTER(vp), vp, i64, dbl, dbl, vp, vp]),
         "hgp_knn_doubly_diag": (i32, [i32, i32, vp, i64, dbl, dbl, vp, i32, vp, vp]),
         "hgp_meanfield_stats": (i32, [i32, vp, i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
-        "hgp_block_stats": (i32, [i32, i32, pi64, pi64, vp, i64, vp, vp, vp, vp, vp]),
+        "hgp_block_stats": (i32, [i32, i32, pi64, pi64, vp, i64, vp, vp, vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

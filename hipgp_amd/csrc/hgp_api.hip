@@ -968,18 +968,19 @@ int hgp_meanfield_stats(int dtype, const void* kn, int64_t nrhs, int64_t Mp, con
 }
 
 int hgp_block_stats(int dtype, int ndim, const int64_t* dims, const int64_t* blocks, const void* kn, int64_t nrhs,
-                    const void* ivar, const void* S, void* gram, void* knSkn, void* hip_stream) {
+                    const void* ivar, const void* S, void* gram, void* knSkn, void* trSG, void* hip_stream) {
   if (dtype != HGP_F32 && dtype != HGP_F64) return fail(HGP_E_ARG, "dtype must be HGP_F32 or HGP_F64");
   if (dims == nullptr || blocks == nullptr) return fail(HGP_E_ARG, "null dims/blocks");
   if (nrhs < 0 || nrhs > (int64_t)1 << 30) return fail(HGP_E_ARG, "nrhs out of range");
   BlockGeom g;
   const char* why = nullptr;
   if (block_geom(ndim, dims, blocks, &g, &why) != 0) return fail(HGP_E_UNSUPPORTED, std::string("hgp_block_stats: ") + why);
-  if (gram == nullptr && knSkn == nullptr) return 0;
+  if (gram == nullptr && knSkn == nullptr && trSG == nullptr) return 0;
+  if (trSG != nullptr && gram == nullptr) return fail(HGP_E_ARG, "trSG needs the gram output");
   if (nrhs > 0 && kn == nullptr) return fail(HGP_E_ARG, "null kn");
   if (gram != nullptr && nrhs > 0 && ivar == nullptr) return fail(HGP_E_ARG, "null ivar");
-  if (knSkn != nullptr && S == nullptr) return fail(HGP_E_ARG, "null S");
-  hipError_t e = block_stats(dtype, g, kn, nrhs, ivar, S, gram, knSkn, reinterpret_cast<hipStream_t>(hip_stream));
+  if ((knSkn != nullptr || trSG != nullptr) && S == nullptr) return fail(HGP_E_ARG, "null S");
+  hipError_t e = block_stats(dtype, g, kn, nrhs, ivar, S, gram, knSkn, trSG, reinterpret_cast<hipStream_t>(hip_stream));
   if (e != hipSuccess) return fail(HGP_E_HIP, std::string("hgp_block_stats: ") + hipGetErrorString(e));
   return 0;
 }

@@ -57,7 +57,7 @@ struct BlockGeom {
 };
 int block_geom(int ndim, const int64_t* dims, const int64_t* blocks, BlockGeom* g, const char** why);
 hipError_t block_stats(int dtype, const BlockGeom& g, const void* kn, int64_t nrhs, const void* iv, const void* S,
-                       void* gram, void* knSkn, hipStream_t s);
+                       void* gram, void* knSkn, void* trSG, hipStream_t s);
 hipError_t kuf_semi_grid(int dtype, int kind, int method, int ndim, const int64_t* m, const void* const* grids,
                          const void* x, int64_t nobs, double sig2, double ell, const void* nodes,
                          const void* weights, int npts, void* out, hipStream_t s);

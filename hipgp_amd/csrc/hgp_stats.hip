@@ -142,83 +142,124 @@ hipError_t meanfield_stats(int dtype, const void* kn, int64_t nrhs, int64_t Mp, 
 // the block grid C-order, point i the block C-order, flat index sum_a (c_a b_a + i_a) stride_a.
 //   gram[beta]  = sum_n iv_n k_{n,beta} k_{n,beta}^T        (bs x bs; hipgp.py:252-256, get_lam :669-685)
 //   knSkn[n]    = sum_beta k_{n,beta}^T S_beta k_{n,beta}    (compute_knSkn :661-664)
-// One workgroup owns NBW = min(16, max(1, 256 / bs^2)) consecutive blocks; the RHS are streamed in chunks
-// of 64 through an LDS tile K[n][col] (col = local block * bs + i, row pitch padded by one).
-// gram: each thread owns entries e = t + 256 r of the workgroup's contiguous gram slab, so the
-// bs^2-per-block write (the dominant HBM term for bs ~ 100) is fully coalesced.
-// knSkn: lane = RHS within the chunk, wave = row (local block, i): u = sum_j S[i][j] K[n][j] with
-// S wave-uniform, v = K[n][i] u accumulated per (wave, n, local block) in LDS by its only writer,
-// then summed over the 4 waves in order -> part[n][beta]; rows reduced by k_reduce_rows.
+// One workgroup owns NBW = min(16, max(1, 1024 / bs^2)) consecutive blocks.  The flat kn column of
+// each of its NBW * bs points is computed once (32-bit, LDS); S of its blocks is staged in LDS once
+// (SL, when it fits); the RHS stream through an LDS tile K[n][col] in chunks of 64 rows, one row
+// per wave and pass, lanes along the columns.
+// gram (TA = 0, bs <= 16): thread t owns entries t + 256 r (r < 4) of the workgroup's contiguous
+// gram slab;
+// (TA >= 1) a 16 x 16 thread grid, thread (ti, tj) owning the TA x TA register tile
+// i = ti + 16 a, j = tj + 16 b (per RHS: 2 TA LDS reads, TA^2 FMAs).
+// knSkn: lane = RHS of the chunk, wave = row (local block, i): u = sum_j S[i][j] K[n][j] (S
+// wave-uniform), v = K[n][i] u accumulated per (wave, n) in LDS by its only writer, then summed over
+// the 4 waves in order -> part[n][workgroup]; rows reduced by k_reduce_rows.
+// trSG = sum_beta <S_beta, gram_beta>_F = sum_n iv_n knSkn_n (the ELBO needs only this sum): formed
+// from the gram registers as they are stored, S read along the same coalesced slab.
 // Every sum has a fixed order (deterministic).
 constexpr int BK_THREADS = 256;
 constexpr int BK_NB = 64;          // RHS per chunk
 constexpr int BK_MAXBS = 128;
+constexpr int BK_UNR = 8;          // rows per load batch of the K-tile fill
+constexpr int BK_ER = 4;           // gram entries per thread for small blocks (TA = 0)
+constexpr size_t BK_LDS_MAX = 160 * 1024;
 
 // LDS row pitch of the K tile: covers the 16 * TA gram tile columns (zero beyond ncol), odd
 __host__ __device__ inline int bk_pitch(int ncol, int TA) { return (ncol > 16 * TA ? ncol : 16 * TA) + 1; }
 
-// TA = 0: bs <= 16, nbw = 256 / bs^2 blocks per workgroup, one gram entry per thread.
-// TA >= 1: bs > 16, one block per workgroup, a 16 x 16 thread grid, thread (ti, tj) owning the
-// TA x TA register tile i = ti + 16 a, j = tj + 16 b (per RHS: TA + TA LDS reads, TA^2 FMAs).
-template <typename T, int TA>
+template <typename T>
+__host__ __device__ inline size_t bk_lds(int nbw, int bs, int TA, bool SL) {
+  const int ncol = nbw * bs;
+  return (size_t)(BK_NB * bk_pitch(ncol, TA) + BK_NB + 4 * BK_NB + (SL ? nbw * bs * bs : 0)) * sizeof(T) +
+         (size_t)ncol * sizeof(int);
+}
+
+template <typename T, int TA, bool SL>
 __global__ __launch_bounds__(BK_THREADS) void k_block_stats(BlockGeom g, const T* __restrict__ kn, int nrhs,
                                                            const T* __restrict__ iv, const T* __restrict__ S,
-                                                           T* __restrict__ gram, T* __restrict__ part) {
+                                                           T* __restrict__ gram, T* __restrict__ part,
+                                                           T* __restrict__ tpart) {
   extern __shared__ unsigned char smem_raw[];
   T* smem = reinterpret_cast<T*>(smem_raw);
-  const int bs = g.bs, nbw = g.nbw;
+  const int bs = g.bs, nbw = g.nbw, bs2 = bs * bs;
   const int ncol = nbw * bs, pitch = bk_pitch(ncol, TA);
   T* Kt = smem;                                   // [BK_NB][pitch]
   T* ivs = Kt + BK_NB * pitch;                    // [BK_NB]
-  T* Q = ivs + BK_NB;                             // [4][BK_NB][nbw]
+  T* Q = ivs + BK_NB;                             // [4][BK_NB]
+  T* Ss = Q + 4 * BK_NB;                          // [nbw][bs][bs] (SL)
+  int* colofs = reinterpret_cast<int*>(Ss + (SL ? nbw * bs2 : 0));   // [ncol], -1 = no block
   const int64_t beta0 = (int64_t)blockIdx.x * nbw;
+  const int nvalid = (int)min<int64_t>(nbw, g.nblk - beta0);
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  for (int col = t; col < ncol; col += BK_THREADS) {
+    const int bl = col / bs, i = col - bl * bs;
+    int64_t rem = beta0 + bl, irem = i, flat = 0, stride = 1;
+    for (int a = g.d - 1; a >= 0; --a) {
+      const int64_t c = rem % g.nb[a], ii = irem % g.b[a];
+      rem /= g.nb[a];
+      irem /= g.b[a];
+      flat += (c * g.b[a] + ii) * stride;
+      stride *= g.n[a];
+    }
+    colofs[col] = bl < nvalid ? (int)flat : -1;
+  }
+  if (SL && part != nullptr) {
+    const T* Sg = S + beta0 * bs2;
+    for (int q = t; q < nbw * bs2; q += BK_THREADS) Ss[q] = (q < nvalid * bs2) ? Sg[q] : (T)0;
+  }
   constexpr int NA = TA > 0 ? TA : 1;
   T acc[NA][NA];
 #pragma unroll
   for (int a = 0; a < NA; ++a)
 #pragma unroll
     for (int b = 0; b < NA; ++b) acc[a][b] = 0;
-  // thread's gram coordinates
-  int gi, gj, gbl;
-  if (TA == 0) {
-    gbl = t / (bs * bs);
-    const int ij = t - gbl * bs * bs;
-    gi = ij / bs;
-    gj = ij - gi * bs;
-  } else {
-    gbl = 0;
-    gi = t >> 4;
-    gj = t & 15;
+  // TA = 0: entries e = t + 256 r (r < BK_ER) of the workgroup's contiguous gram slab
+  T acc0[BK_ER];
+  int oi[BK_ER], oj[BK_ER];
+  const int nent = nvalid * bs2;
+#pragma unroll
+  for (int r = 0; r < BK_ER; ++r) {
+    acc0[r] = 0;
+    const int e = min(t + BK_THREADS * r, nbw * bs2 - 1);
+    const int bl = e / bs2, ij = e - bl * bs2, i = ij / bs;
+    oi[r] = bl * bs + i;
+    oj[r] = bl * bs + (ij - i * bs);
   }
-  const bool gram_thread = gram != nullptr && gbl < nbw;
+  const int gi = t >> 4, gj = t & 15;
+  const bool gram_thread = gram != nullptr && (TA > 0 || t < nent);
+  const int nwg = gridDim.x;
+  __syncthreads();
   for (int n0 = 0; n0 < nrhs; n0 += BK_NB) {
     const int nn = min(BK_NB, nrhs - n0);
-    for (int q = t; q < BK_NB * pitch; q += BK_THREADS) {
-      const int rn = q / pitch, col = q - rn * pitch;
-      const int bl = col / bs, i = col - bl * bs;
-      const int64_t beta = beta0 + bl;
-      T v = 0;
-      if (rn < nn && col < ncol && beta < g.nblk) {
-        int64_t rem = beta, irem = i, flat = 0, stride = 1;
-        for (int a = g.d - 1; a >= 0; --a) {
-          const int64_t c = rem % g.nb[a], ii = irem % g.b[a];
-          rem /= g.nb[a];
-          irem /= g.b[a];
-          flat += (c * g.b[a] + ii) * stride;
-          stride *= g.n[a];
+    // BK_UNR independent row loads in flight.  Columns >= ncol (tile padding) stay unset: they only
+    // feed gram entries i or j >= bs, which are never stored.
+    for (int col = lane; col < ncol; col += 64) {
+      const int o = col < ncol ? colofs[col] : -1;
+      for (int rn0 = w; rn0 < nn; rn0 += 4 * BK_UNR) {
+        T v[BK_UNR];
+#pragma unroll
+        for (int u = 0; u < BK_UNR; ++u) {
+          const int rn = rn0 + 4 * u;
+          v[u] = 0;
+          if (o >= 0 && rn < nn) v[u] = kn[(int64_t)(n0 + rn) * g.Mp + o];
         }
-        v = kn[(int64_t)(n0 + rn) * g.Mp + flat];
+#pragma unroll
+        for (int u = 0; u < BK_UNR; ++u)
+          if (rn0 + 4 * u < nn) Kt[(rn0 + 4 * u) * pitch + col] = v[u];
       }
-      Kt[q] = v;
     }
     if (t < BK_NB) ivs[t] = (t < nn && iv != nullptr) ? iv[n0 + t] : (T)0;   // iv may be NULL without gram
-    if (part != nullptr)
-      for (int q = t; q < 4 * BK_NB * nbw; q += BK_THREADS) Q[q] = 0;
     __syncthreads();
-    if (gram_thread) {
-      const T* ki = Kt + gbl * bs + gi;
-      const T* kj = Kt + gbl * bs + gj;
+    if (TA == 0 && gram_thread) {
+      for (int k = 0; k < nn; ++k) {
+        const T ivk = ivs[k];
+        const T* kr = Kt + k * pitch;
+#pragma unroll
+        for (int r = 0; r < BK_ER; ++r)
+          if (t + BK_THREADS * r < nent) acc0[r] += ivk * kr[oi[r]] * kr[oj[r]];
+      }
+    } else if (gram_thread) {
+      const T* ki = Kt + gi;
+      const T* kj = Kt + gj;
       for (int k = 0; k < nn; ++k) {
         const T ivk = ivs[k];
         T vi[NA], vj[NA];
@@ -233,86 +274,120 @@ __global__ __launch_bounds__(BK_THREADS) void k_block_stats(BlockGeom g, const T
           for (int b = 0; b < NA; ++b) acc[a][b] += vi[a] * vj[b];
       }
     }
-    if (part != nullptr && lane < nn) {
-      const T* kr = Kt + lane * pitch;
-      for (int row = w; row < ncol; row += 4) {
-        const int bl = row / bs, i = row - bl * bs;
-        if (beta0 + bl >= g.nblk) continue;
-        const T* srow = S + ((beta0 + bl) * bs + i) * bs;
-        const T* kb = kr + bl * bs;
-        T u = 0;
-        for (int j = 0; j < bs; ++j) u += srow[j] * kb[j];
-        Q[(w * BK_NB + lane) * nbw + bl] += kb[i] * u;
-      }
-    }
-    __syncthreads();
     if (part != nullptr) {
-      for (int q = t; q < nn * nbw; q += BK_THREADS) {
-        const int rn = q / nbw, bl = q - rn * nbw;
-        if (beta0 + bl < g.nblk) {
-          T s = 0;
-#pragma unroll
-          for (int ww = 0; ww < 4; ++ww) s += Q[(ww * BK_NB + rn) * nbw + bl];
-          part[(int64_t)(n0 + rn) * g.nblk + beta0 + bl] = s;
+      T qv = 0;
+      if (lane < nn) {
+        const T* kr = Kt + lane * pitch;
+        for (int row = w; row < nvalid * bs; row += 4) {
+          const int bl = row / bs, i = row - bl * bs;
+          const T* srow = SL ? Ss + (bl * bs + i) * bs : S + ((beta0 + bl) * bs + i) * bs;
+          const T* kb = kr + bl * bs;
+          T u = 0;
+          for (int j = 0; j < bs; ++j) u += srow[j] * kb[j];
+          qv += kb[i] * u;
         }
       }
+      Q[w * BK_NB + lane] = qv;
     }
     __syncthreads();
+    if (part != nullptr && t < nn)
+      part[(int64_t)(n0 + t) * nwg + blockIdx.x] = (Q[t] + Q[BK_NB + t]) + (Q[2 * BK_NB + t] + Q[3 * BK_NB + t]);
+    __syncthreads();
   }
-  if (gram_thread && beta0 + gbl < g.nblk) {
-    T* gb = gram + (beta0 + gbl) * bs * bs;
+  T tr = 0;
+  if (TA == 0 && gram_thread) {
+    T* gb = gram + beta0 * bs2;
+    const T* sb = S + beta0 * bs2;
+#pragma unroll
+    for (int r = 0; r < BK_ER; ++r) {
+      const int e = t + BK_THREADS * r;
+      if (e < nent) {
+        gb[e] = acc0[r];
+        if (tpart != nullptr) tr += sb[e] * acc0[r];
+      }
+    }
+  } else if (gram_thread) {        // TA > 0: one block per workgroup
+    T* gb = gram + beta0 * bs2;
+    const T* sb = S + beta0 * bs2;
 #pragma unroll
     for (int a = 0; a < NA; ++a)
 #pragma unroll
       for (int b = 0; b < NA; ++b) {
         const int i = gi + 16 * a, j = gj + 16 * b;
-        if (i < bs && j < bs) gb[i * bs + j] = acc[a][b];
+        if (i < bs && j < bs) {
+          gb[i * bs + j] = acc[a][b];
+          if (tpart != nullptr) tr += sb[i * bs + j] * acc[a][b];
+        }
       }
+  }
+  if (tpart != nullptr) {          // <S, G>_F of the workgroup's blocks, fixed-order reduction
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) tr += __shfl_xor(tr, off, 64);
+    if (lane == 0) Q[w] = tr;
+    __syncthreads();
+    if (t == 0) tpart[blockIdx.x] = (Q[0] + Q[1]) + (Q[2] + Q[3]);
   }
 }
 
 template <typename T, int TA>
 void launch_block_stats(const BlockGeom& g, int64_t grid, const void* kn, int nrhs, const void* iv, const void* S,
-                        void* gram, void* part, hipStream_t s) {
-  const size_t lds = (size_t)(BK_NB * bk_pitch(g.nbw * g.bs, TA) + BK_NB + 4 * BK_NB * g.nbw) * sizeof(T);
-  if (lds > 65536)
-    (void)hipFuncSetAttribute((const void*)k_block_stats<T, TA>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((k_block_stats<T, TA>), dim3((unsigned)grid), dim3(BK_THREADS), lds, s, g, (const T*)kn, nrhs,
-                     (const T*)iv, (const T*)S, (T*)gram, (T*)part);
+                        void* gram, void* part, void* tpart, hipStream_t s) {
+  const bool sl = part != nullptr && bk_lds<T>(g.nbw, g.bs, TA, true) <= BK_LDS_MAX;
+  const size_t lds = bk_lds<T>(g.nbw, g.bs, TA, sl);
+  auto launch = [&](auto kern) {
+    if (lds > 65536) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(BK_THREADS), lds, s, g, (const T*)kn, nrhs, (const T*)iv,
+                       (const T*)S, (T*)gram, (T*)part, (T*)tpart);
+  };
+  if (sl) launch(k_block_stats<T, TA, true>);
+  else launch(k_block_stats<T, TA, false>);
 }
 
 template <typename T>
 hipError_t block_stats_t(const BlockGeom& g, const void* kn, int64_t nrhs, const void* iv, const void* S, void* gram,
-                         void* knSkn, hipStream_t s) {
+                         void* knSkn, void* trSG, hipStream_t s) {
   const int64_t grid = (g.nblk + g.nbw - 1) / g.nbw;
   T* part = nullptr;
+  T* tpart = nullptr;
   if (knSkn != nullptr && nrhs > 0) {
-    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&part), (size_t)(nrhs * g.nblk) * sizeof(T), s);
+    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&part), (size_t)(nrhs * grid) * sizeof(T), s);
+    if (e != hipSuccess) return e;
+  }
+  if (trSG != nullptr && nrhs > 0) {
+    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&tpart), (size_t)grid * sizeof(T), s);
     if (e != hipSuccess) return e;
   }
   void* gp = gram;
-  if (nrhs == 0 && gram != nullptr) {     // empty batch: the sum over no observations
-    hipError_t e = hipMemsetAsync(gram, 0, (size_t)(g.nblk * g.bs * g.bs) * sizeof(T), s);
-    if (e != hipSuccess) return e;
+  if (nrhs == 0) {     // empty batch: sums over no observations
+    if (gram != nullptr) {
+      hipError_t e = hipMemsetAsync(gram, 0, (size_t)(g.nblk * g.bs * g.bs) * sizeof(T), s);
+      if (e != hipSuccess) return e;
+    }
+    if (trSG != nullptr) {
+      hipError_t e = hipMemsetAsync(trSG, 0, sizeof(T), s);
+      if (e != hipSuccess) return e;
+    }
     gp = nullptr;
   }
   if (nrhs > 0) {
     const int TA = g.bs <= 16 ? 0 : (g.bs + 15) / 16;
     switch (TA) {
-      case 0: launch_block_stats<T, 0>(g, grid, kn, (int)nrhs, iv, S, gp, part, s); break;
-      case 2: launch_block_stats<T, 2>(g, grid, kn, (int)nrhs, iv, S, gp, part, s); break;
-      case 3: launch_block_stats<T, 3>(g, grid, kn, (int)nrhs, iv, S, gp, part, s); break;
-      case 4: launch_block_stats<T, 4>(g, grid, kn, (int)nrhs, iv, S, gp, part, s); break;
-      case 5: launch_block_stats<T, 5>(g, grid, kn, (int)nrhs, iv, S, gp, part, s); break;
-      case 6: launch_block_stats<T, 6>(g, grid, kn, (int)nrhs, iv, S, gp, part, s); break;
-      case 7: launch_block_stats<T, 7>(g, grid, kn, (int)nrhs, iv, S, gp, part, s); break;
-      default: launch_block_stats<T, 8>(g, grid, kn, (int)nrhs, iv, S, gp, part, s); break;
+      case 0: launch_block_stats<T, 0>(g, grid, kn, (int)nrhs, iv, S, gp, part, tpart, s); break;
+      case 2: launch_block_stats<T, 2>(g, grid, kn, (int)nrhs, iv, S, gp, part, tpart, s); break;
+      case 3: launch_block_stats<T, 3>(g, grid, kn, (int)nrhs, iv, S, gp, part, tpart, s); break;
+      case 4: launch_block_stats<T, 4>(g, grid, kn, (int)nrhs, iv, S, gp, part, tpart, s); break;
+      case 5: launch_block_stats<T, 5>(g, grid, kn, (int)nrhs, iv, S, gp, part, tpart, s); break;
+      case 6: launch_block_stats<T, 6>(g, grid, kn, (int)nrhs, iv, S, gp, part, tpart, s); break;
+      case 7: launch_block_stats<T, 7>(g, grid, kn, (int)nrhs, iv, S, gp, part, tpart, s); break;
+      default: launch_block_stats<T, 8>(g, grid, kn, (int)nrhs, iv, S, gp, part, tpart, s); break;
     }
-    if (knSkn != nullptr) reduce_rows<T>(part, (int)g.nblk, (int)nrhs, knSkn, s);
+    if (knSkn != nullptr) reduce_rows<T>(part, (int)grid, (int)nrhs, knSkn, s);
+    if (trSG != nullptr) reduce_rows<T>(tpart, (int)grid, 1, trSG, s);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  if (part != nullptr) return hipFreeAsync(part, s);
+  if (part != nullptr && (e = hipFreeAsync(part, s)) != hipSuccess) return e;
+  if (tpart != nullptr) return hipFreeAsync(tpart, s);
   return hipSuccess;
 }
 
@@ -333,16 +408,17 @@ int block_geom(int ndim, const int64_t* dims, const int64_t* blocks, BlockGeom* 
     bs *= blocks[a];
   }
   if (bs > BK_MAXBS) { *why = "block size (points per block) must be <= 128"; return -1; }
+  if (g->Mp >= ((int64_t)1 << 31)) { *why = "expanded grid must have < 2^31 points"; return -1; }
   g->bs = (int)bs;
-  // blocks per workgroup: fill the 256 gram threads, at most 16 (bounds the LDS of the knSkn partials)
-  g->nbw = (int)std::min<int64_t>(16, std::max<int64_t>(1, BK_THREADS / (bs * bs)));
+  // blocks per workgroup: up to 4 gram entries per thread, at most 16 (longer contiguous kn runs)
+  g->nbw = bs > 16 ? 1 : (int)std::min<int64_t>(16, std::max<int64_t>(1, BK_THREADS * BK_ER / (bs * bs)));
   return 0;
 }
 
 hipError_t block_stats(int dtype, const BlockGeom& g, const void* kn, int64_t nrhs, const void* iv, const void* S,
-                       void* gram, void* knSkn, hipStream_t s) {
-  if (dtype == HGP_F64) return block_stats_t<double>(g, kn, nrhs, iv, S, gram, knSkn, s);
-  return block_stats_t<float>(g, kn, nrhs, iv, S, gram, knSkn, s);
+                       void* gram, void* knSkn, void* trSG, hipStream_t s) {
+  if (dtype == HGP_F64) return block_stats_t<double>(g, kn, nrhs, iv, S, gram, knSkn, trSG, s);
+  return block_stats_t<float>(g, kn, nrhs, iv, S, gram, knSkn, trSG, s);
 }
 
 }  // namespace hgp

@@ -468,7 +468,7 @@ class BlockToeplitzGP(ToeplitzInducingGP):
     def get_S_from_lam(self, lam):
         return torch.inverse(lam)
 
-    def _block_kernel(self, kn, ivar=None, S=None, gram=True, knSkn=True):
+    def _block_kernel(self, kn, ivar=None, S=None, gram=True, knSkn=True, trace=False):
         import ctypes
         from hipgp_amd import _lib
         B, Mp = kn.shape
@@ -482,9 +482,10 @@ class BlockToeplitzGP(ToeplitzInducingGP):
         Sc = None if S is None else S.detach().to(dt).contiguous()
         G = torch.empty(self.num_blocks, self.block_size, self.block_size, dtype=dt, device=dev) if gram else None
         q = torch.empty(B, dtype=dt, device=dev) if knSkn else None
+        tr = torch.empty((), dtype=dt, device=dev) if trace else None
         _lib.check(_lib.lib().hgp_block_stats(_lib.dtype_code(dt), nd, dims, blks, p(knc), B, p(ivv), p(Sc),
-                                              p(G), p(q), _lib.stream_ptr(dev)))
-        return G, q
+                                              p(G), p(q), p(tr), _lib.stream_ptr(dev)))
+        return (G, q, tr) if trace else (G, q)
 
     def compute_knSkn(self, kn, qS):
         """kn_n^T S kn_n per row (`hipgp.py:661-664`)."""
@@ -526,7 +527,8 @@ class BlockToeplitzGP(ToeplitzInducingGP):
                 from hipgp_amd import _lib
                 dev, dt = kn.device, kn.dtype
                 colv = lambda v: torch.as_tensor(v, dtype=dt, device=dev).reshape(-1).expand(B).contiguous()
-                G, knSkn = self._block_kernel(kn, ivar=ivar, S=qS)
+                # per-block grams and sum_n ivar_n kn_n^T S kn_n = sum_blk <S, G>_F in one read of kn
+                G, _, trSG = self._block_kernel(kn, ivar=ivar, S=qS, knSkn=False, trace=True)
                 # a_n without the kn S kn term and dm from the streaming row/column passes
                 knc = kn.detach().contiguous()
                 zero = torch.zeros(kn.shape[1], dtype=dt, device=dev)
@@ -539,8 +541,7 @@ class BlockToeplitzGP(ToeplitzInducingGP):
                 _lib.check(_lib.lib().hgp_meanfield_stats(_lib.dtype_code(dt), p(knc), B, kn.shape[1], p(qmv),
                                                           p(zero), p(y), p(iv), p(kd), p(lsd), p(an), p(lam_diag),
                                                           p(dm), _lib.stream_ptr(dev)))
-                an = an - 0.5 * iv * knSkn
-                return {"an_sum": an.sum(), "lam_sum": G, "dm_sum": dm, "n": B}
+                return {"an_sum": an.sum() - 0.5 * trSG, "lam_sum": G, "dm_sum": dm, "n": B}
             # CPU tensors only reach here in the gloo host-logic tests
             y = ybatch.reshape(-1)
             knm = kn.matmul(qm).reshape(-1)

@@ -164,11 +164,13 @@ int hgp_meanfield_stats(int dtype, const void* kn, int64_t nrhs, int64_t Mp, con
  * over the block grid and points C-order inside a block (ziggy/misc/util.py:79-119).
  *   gram[nblk][bs][bs] = sum_n ivar_n kn_{n,blk} kn_{n,blk}^T     (hipgp.py:252-256, get_lam :669-685)
  *   knSkn[nrhs]        = sum_blk kn_{n,blk}^T S_blk kn_{n,blk}    (compute_knSkn :661-664; S [nblk][bs][bs])
- * kn (nrhs, M') row layout; gram or knSkn may be NULL to skip that output (then ivar resp. S may
- * be NULL).  gram is the per-shard sum RCCL all-reduces across RHS shards.  Deterministic. */
+ *   trSG[1]            = sum_blk <S_blk, gram_blk>_F = sum_n ivar_n knSkn_n   (the ELBO's a_n sum needs only this)
+ * kn (nrhs, M') row layout; gram, knSkn, trSG may each be NULL to skip that output (trSG needs
+ * gram; ivar may be NULL without gram, S without knSkn/trSG).  gram is the per-shard sum RCCL
+ * all-reduces across RHS shards.  Deterministic. */
 int hgp_block_stats(int dtype, int ndim, const int64_t* dims, const int64_t* blocks, const void* kn,
                     int64_t nrhs, const void* ivar, const void* S, void* gram, void* knSkn,
-                    void* hip_stream);
+                    void* trSG, void* hip_stream);
 
 /* Sizes of a plan: M, M' and the padded FFT lengths per axis (K-type and R-type ops). */
 int hgp_plan_info(const hgp_plan* plan, int64_t* M, int64_t* Mprime, int64_t* L_K,

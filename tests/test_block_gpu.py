@@ -45,10 +45,12 @@ def test_block_stats_kernel(dims, blocks, B, dtype):
     m = _M()
     m.block_dims, m.block_sides = list(dims), list(blocks)
     m.num_blocks, m.block_size = idx.shape
-    G, q = BlockToeplitzGP._block_kernel(m, kn.to(DEV, dtype), ivar=iv.to(DEV, dtype), S=S.to(DEV, dtype))
+    G, q, tr = BlockToeplitzGP._block_kernel(m, kn.to(DEV, dtype), ivar=iv.to(DEV, dtype), S=S.to(DEV, dtype),
+                                             trace=True)
     tol = 1e-12 if dtype == torch.float64 else 2e-6
     assert rel_err(G.double().cpu().numpy(), Gr.numpy()) < tol
     assert rel_err(q.double().cpu().numpy(), qr.numpy()) < tol
+    assert abs(float(tr) - float(iv @ qr)) <= tol * float((iv * qr.abs()).sum())
     # deterministic: a second launch is bit-identical
     G2, q2 = BlockToeplitzGP._block_kernel(m, kn.to(DEV, dtype), ivar=iv.to(DEV, dtype), S=S.to(DEV, dtype))
     assert torch.equal(G, G2) and torch.equal(q, q2)
@@ -61,14 +63,17 @@ def test_block_stats_edge_cases():
     dims = (ctypes.c_int64 * 2)(20, 16)
     G = torch.full((20, 16, 16), 7., dtype=torch.float64, device=DEV)
     # empty batch: the gram is the sum over no observations
-    _lib.check(L.hgp_block_stats(_lib.HGP_F64, 2, dims, (ctypes.c_int64 * 2)(4, 4), None, 0, None, None,
-                                 ctypes.c_void_p(G.data_ptr()), None, _lib.stream_ptr(G.device)))
-    assert float(G.abs().max()) == 0.
+    tr = torch.ones((), dtype=torch.float64, device=DEV)
+    S = torch.ones_like(G)
+    _lib.check(L.hgp_block_stats(_lib.HGP_F64, 2, dims, (ctypes.c_int64 * 2)(4, 4), None, 0, None,
+                                 ctypes.c_void_p(S.data_ptr()), ctypes.c_void_p(G.data_ptr()), None,
+                                 ctypes.c_void_p(tr.data_ptr()), _lib.stream_ptr(G.device)))
+    assert float(G.abs().max()) == 0. and float(tr) == 0.
     # refused shapes: not divisible, block > 128 points, 1-D
     for nd, d, b in ((2, (20, 16), (3, 4)), (2, (32, 32), (16, 16)), (1, (20,), (4,))):
         rc = L.hgp_block_stats(_lib.HGP_F64, nd, (ctypes.c_int64 * nd)(*d), (ctypes.c_int64 * nd)(*b),
                                ctypes.c_void_p(G.data_ptr()), 1, ctypes.c_void_p(G.data_ptr()), None,
-                               ctypes.c_void_p(G.data_ptr()), None, None)
+                               ctypes.c_void_p(G.data_ptr()), None, None, None)
         assert rc == -4, (nd, d, b)
 
 
