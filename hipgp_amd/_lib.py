@@ -26,7 +26,7 @@ EXPORTS = (
     "hgp_plan_info", "hgp_plan_destroy", "hgp_last_error", "hgp_version",
     "hgp_toeplitz_apply_pass", "hgp_op_pass_count", "hgp_pcg_rnorm2", "hgp_kuf_grid",
     "hgp_kuf_semi_mc", "hgp_kuf_semi_sqexp", "hgp_knn_doubly_diag", "hgp_meanfield_stats",
-    "hgp_block_stats",
+    "hgp_block_stats", "hgp_sym_toeplitz_dqf", "hgp_plan_column_grad",
 )
 KERN_SQEXP, KERN_MATERN12, KERN_MATERN32, KERN_MATERN52, KERN_GNEITING = 0, 1, 2, 3, 4
 
@@ -71,6 +71,8 @@ def lib():
         "hgp_knn_doubly_diag": (i32, [i32, i32, vp, i64, dbl, dbl, vp, i32, vp, vp]),
         "hgp_meanfield_stats": (i32, [i32, vp, i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
         "hgp_block_stats": (i32, [i32, i32, pi64, pi64, vp, i64, vp, vp, vp, vp, vp, vp]),
+        "hgp_sym_toeplitz_dqf": (i32, [i32, vp, vp, i64, i64, vp, vp]),
+        "hgp_plan_column_grad": (i32, [vp, i32, vp, vp, i64, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

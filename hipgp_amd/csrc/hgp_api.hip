@@ -78,6 +78,7 @@ struct hgp_plan {
   // spectra
   DevBuf specK, specI, specR, Dm3;
   bool have_spec = false;
+  double clamp_min = 1e-6;                // of the last set_column (the clamp's gradient mask)
   DevBuf nclamp;
   // scratch
   DevBuf ws1, ws2, set1, set2, setM1, setM2, setC;
@@ -493,6 +494,7 @@ int set_column_t(hgp_plan* P, const void* column, double jitter, double clamp_mi
   double* a = reinterpret_cast<double*>(P->setM1.ptr);
   double* b = reinterpret_cast<double*>(P->setM2.ptr);
   to_f64<T>(column, a, M, jitter, s);
+  P->clamp_min = clamp_min;
   // D_raw = DCT-I over every axis (length-n FFT of the circulant embedding, real part)
   for (int ax = 0; ax < d; ++ax) {
     HGP_TRY(dct_axis(P, ax, a, b, 1, 1.0));
@@ -982,6 +984,71 @@ int hgp_block_stats(int dtype, int ndim, const int64_t* dims, const int64_t* blo
   if ((knSkn != nullptr || trSG != nullptr) && S == nullptr) return fail(HGP_E_ARG, "null S");
   hipError_t e = block_stats(dtype, g, kn, nrhs, ivar, S, gram, knSkn, trSG, reinterpret_cast<hipStream_t>(hip_stream));
   if (e != hipSuccess) return fail(HGP_E_HIP, std::string("hgp_block_stats: ") + hipGetErrorString(e));
+  return 0;
+}
+
+int hgp_sym_toeplitz_dqf(int dtype, const void* left, const void* right, int64_t nvec, int64_t n, void* out,
+                         void* hip_stream) {
+  if (dtype != HGP_F32 && dtype != HGP_F64) return fail(HGP_E_ARG, "bad dtype");
+  if (nvec < 0 || n <= 0) return fail(HGP_E_ARG, "bad nvec/n");
+  if (out == nullptr || (nvec > 0 && (left == nullptr || right == nullptr))) return fail(HGP_E_ARG, "null pointer");
+  hipError_t e = sym_toeplitz_dqf(dtype, left, right, nvec, n, out, reinterpret_cast<hipStream_t>(hip_stream));
+  if (e != hipSuccess) return fail(HGP_E_HIP, std::string("hgp_sym_toeplitz_dqf: ") + hipGetErrorString(e));
+  return 0;
+}
+
+// d/dcolumn <g, op x> through the operator's spectrum S(D) (toeplitz_tensor.py:20-31, ops :70-125).
+// With A = DCT-I on the m-grid (A[f][x] = mu(x) cos(2 pi f x / n) per axis, dct_axis), D = A column
+// and the operator's generator c = A S(D) / N on the n-grid:
+//   gs = fold(X) (X = dL/dc on the n-grid, hgp_grad.hip), dL/dS = A^T gs / N,
+//   dL/dD = dL/dS * S'(D) * [D > cmin], dL/dcolumn = A^T dL/dD,  A^T y = mu (A (y / mu)).
+int hgp_plan_column_grad(hgp_plan* plan, int op, const void* x, const void* g, int64_t nrhs, void* column_grad) {
+  HGP_TRY(check_plan(plan));
+  if (!plan->have_spec) return fail(HGP_E_STATE, "hgp_plan_set_column has not been called");
+  if (op < HGP_OP_K || op > HGP_OP_R) return fail(HGP_E_ARG, "bad op");
+  if (nrhs < 0 || column_grad == nullptr || (nrhs > 0 && (x == nullptr || g == nullptr)))
+    return fail(HGP_E_ARG, "bad nrhs or null pointer");
+  if (plan->d < 1) return fail(HGP_E_UNSUPPORTED, "a grid with a single point has no column gradient");
+  HGP_TRY(use_device(plan));
+  hgp_plan* P = plan;
+  hipStream_t s = P->stream;
+  const int64_t M = P->M, Mp = P->Mp;
+  GridDims gd;
+  gd.d = P->d;
+  for (int a = 0; a < 3; ++a) { gd.m[a] = P->m[a]; gd.n[a] = P->n[a]; gd.L[a] = P->LK[a]; }
+  DevBuf X, y1, y2;
+  HGP_TRY(X.ensure((size_t)Mp * sizeof(double)));
+  HGP_TRY(y1.ensure((size_t)M * sizeof(double)));
+  HGP_TRY(y2.ensure((size_t)M * sizeof(double)));
+  double* Xp = reinterpret_cast<double*>(X.ptr);
+  double* a = reinterpret_cast<double*>(y1.ptr);
+  double* b = reinterpret_cast<double*>(y2.ptr);
+  if (nrhs == 0) HIP_TRY(hipMemsetAsync(Xp, 0, (size_t)Mp * sizeof(double), s));
+  else {
+    // <g, op x> = sum_b sum_{j in m-grid} v_b[j] sum_w c[w] h_b[(j + w) mod n] with (v, h) =
+    // (x, g) for R^T (g on the n-grid), (g, x) for R (x on the n-grid), (x, g) for K / C^-1
+    // (g on the m-grid, zero elsewhere: the crop)
+    const void* vv = op == HGP_OP_R ? g : x;
+    const void* hh = op == HGP_OP_R ? x : g;
+    const int h_on_m = (op == HGP_OP_K || op == HGP_OP_CINV) ? 1 : 0;
+    hipError_t e = circ_xcorr(P->dtype, vv, hh, h_on_m, nrhs, gd, M, Mp, Xp, s);
+    if (e != hipSuccess) return fail(HGP_E_HIP, std::string("circ_xcorr: ") + hipGetErrorString(e));
+  }
+  fold_div_mu(Xp, M, gd, a, s);
+  for (int ax = 0; ax < P->d; ++ax) {
+    HGP_TRY(dct_axis(P, ax, a, b, 1, 1.0 / (double)P->n[ax]));
+    std::swap(a, b);
+  }
+  const int kind = op == HGP_OP_K ? 0 : (op == HGP_OP_CINV ? 1 : 2);
+  spec_bwd(a, reinterpret_cast<const double*>(P->Dm3.ptr), M, kind, P->clamp_min, s);
+  for (int ax = 0; ax < P->d; ++ax) {
+    HGP_TRY(dct_axis(P, ax, a, b, 1, 1.0));
+    std::swap(a, b);
+  }
+  mul_mu_out(P->dtype, a, M, gd, column_grad, s);
+  HIP_TRY(hipGetLastError());
+  // the scratch is freed on return: finish its users first
+  HIP_TRY(hipStreamSynchronize(s));
   return 0;
 }
 

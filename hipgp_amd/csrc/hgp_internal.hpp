@@ -62,6 +62,14 @@ hipError_t kuf_semi_grid(int dtype, int kind, int method, int ndim, const int64_
                          const void* x, int64_t nobs, double sig2, double ell, const void* nodes,
                          const void* weights, int npts, void* out, hipStream_t s);
 
+// backward w.r.t. the Toeplitz column (hgp_grad.hip)
+hipError_t sym_toeplitz_dqf(int dtype, const void* u, const void* v, int64_t nvec, int64_t n, void* out,
+                            hipStream_t s);
+hipError_t circ_xcorr(int dtype, const void* v, const void* g, int g_on_m, int64_t nrhs, const GridDims& gd,
+                      int64_t M, int64_t Mp, double* X, hipStream_t s);
+void fold_div_mu(const double* X, int64_t M, const GridDims& gd, double* y, hipStream_t s);
+void spec_bwd(double* y, const double* D3, int64_t M, int kind, double cmin, hipStream_t s);
+void mul_mu_out(int dtype, const double* r, int64_t M, const GridDims& gd, void* out, hipStream_t s);
 // CG
 int update_np(int64_t M);
 template <typename T> void cg_init(const void* b, void* x, void* r, int64_t n, hipStream_t s);

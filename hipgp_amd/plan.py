@@ -106,6 +106,22 @@ class ToeplitzPlan:
                                        ctypes.c_void_p(out.data_ptr()), x.shape[0]))
         return out
 
+    def column_grad(self, op, x, g):
+        """d/dcolumn of sum(g * op(x)) through the operator's spectrum (hgp_plan_column_grad),
+        (M,) in the plan dtype; x, g shaped like op's input / output (`toeplitz_tensor.py:20-125`)."""
+        nin = self.Mprime if op == _lib.OP_R else self.M
+        nout = self.Mprime if op == _lib.OP_RT else self.M
+        x = self._vec(x, "x", nin)
+        g = self._vec(g, "g", nout)
+        if x.shape[0] != g.shape[0]:
+            raise ValueError(f"x has {x.shape[0]} rows, g has {g.shape[0]}")
+        out = torch.empty(self.M, dtype=self.dtype, device=self.device)
+        self._bind_stream()
+        check(lib().hgp_plan_column_grad(self._h, int(op), ctypes.c_void_p(x.data_ptr()),
+                                         ctypes.c_void_p(g.data_ptr()), x.shape[0],
+                                         ctypes.c_void_p(out.data_ptr())))
+        return out
+
     # -- PCG ---------------------------------------------------------------------------------
     def pcg(self, b, maxiter, tol, precond=True, out=None, return_iters=False):
         """Batched PCG with the conj_grad2 recurrence (`cg.py:44-80`), row layout (nrhs, M)."""
@@ -172,6 +188,27 @@ class ToeplitzPlan:
                     lib().hgp_plan_destroy(h)
             except Exception:
                 pass
+
+
+def sym_toeplitz_dqf(left_vectors, right_vectors):
+    """gpytorch's sym_toeplitz_derivative_quadratic_form (`ziggy/misc/gpt_toeplitz.py:169-209`):
+    left/right (n,) or (n, s) as the reference takes them; returns (n,) with
+    out[i] = sum_j left[:, j]^T (dT/dc_i) right[:, j]  (ones on the i-th sub/super-diagonal)."""
+    _lib.require_device_tensor(left_vectors, "left_vectors")
+    if left_vectors.ndimension() == 1:
+        left_vectors = left_vectors.unsqueeze(1)
+        right_vectors = right_vectors.unsqueeze(1)
+    if left_vectors.shape != right_vectors.shape or left_vectors.dim() != 2:
+        raise ValueError(f"left {tuple(left_vectors.shape)} / right {tuple(right_vectors.shape)}: "
+                         "expected matching (n, s)")
+    n = left_vectors.shape[0]
+    u = left_vectors.t().contiguous()
+    v = right_vectors.t().contiguous().to(u.dtype)
+    out = torch.empty(n, dtype=u.dtype, device=u.device)
+    check(lib().hgp_sym_toeplitz_dqf(_lib.dtype_code(u.dtype), ctypes.c_void_p(u.data_ptr()),
+                                     ctypes.c_void_p(v.data_ptr()), u.shape[0], n,
+                                     ctypes.c_void_p(out.data_ptr()), _lib.stream_ptr(u.device)))
+    return out
 
 
 def rowdot(a, c):

@@ -1,12 +1,15 @@
 """InvMatmul autograd Function (`ziggy/misc/_inv_matmul.py:9-64`).
 
-forward: no-grad PCG solve (hgp_pcg_solve).  backward: right_grad = K^{-1} grad_output by a
-second solve, as the reference does (`:27-50`).  The Toeplitz-column gradient
-(`:52`, gpytorch's sym_toeplitz_derivative_quadratic_form) is SURVEY §8(f) row 4 and is
-not built in this round: asking for it raises instead of returning something wrong.
+forward: no-grad PCG solve (hgp_pcg_solve).  backward (`:27-64`): left solves
+L = K^{-1} grad_output by a second solve (always preconditioned, as the reference); the
+right-hand-side gradient is L; the Toeplitz-column gradient is gpytorch's
+sym_toeplitz_derivative_quadratic_form([L; R]^T, -0.5 [R; L]^T) over the flattened column
+(`:52-60`, hgp_sym_toeplitz_dqf), summed to the column's shape (`:62-63`).
 """
 import torch
 from torch.autograd import Function
+
+from hipgp_amd.plan import sym_toeplitz_dqf
 
 
 class InvMatmul(Function):
@@ -25,11 +28,19 @@ class InvMatmul(Function):
     @staticmethod
     def backward(ctx, grad_output):
         (right_solves,) = ctx.saved_tensors
+        left_solves = None
+        if any(ctx.needs_input_grad):
+            left_solves = InvMatmul.apply(ctx.toeplitz_tensor, ctx.toeplitz_tensor.column,
+                                          grad_output, True, ctx.maxiter, ctx.tol)
+        column_grad = None
         if ctx.needs_input_grad[1]:
-            raise NotImplementedError("gradient w.r.t. the Toeplitz column (kernel "
-                                      "hyper-parameters) is SURVEY §8(f) row 4, not built yet")
-        right_grad = None
-        if ctx.needs_input_grad[2]:
-            right_grad = InvMatmul.apply(ctx.toeplitz_tensor, ctx.toeplitz_tensor.column,
-                                         grad_output, True, ctx.maxiter, ctx.tol)
-        return None, None, right_grad, None, None, None
+            with torch.no_grad():
+                left_vecs = torch.cat([left_solves, right_solves], 0).t()
+                right_vecs = torch.cat([right_solves, left_solves], 0).t().mul(-0.5)
+                column_grad = sym_toeplitz_dqf(left_vecs, right_vecs)
+            column = ctx.toeplitz_tensor.column
+            if column_grad.dim() > column.dim():
+                column_grad = column_grad.view(-1, *column.shape).sum(0)
+            column_grad = column_grad.view(column.shape)
+        right_grad = left_solves if ctx.needs_input_grad[2] else None
+        return None, column_grad, right_grad, None, None, None

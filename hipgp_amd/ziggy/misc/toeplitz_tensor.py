@@ -10,14 +10,43 @@ Operator map (reference line -> here):
   _solve / conj_grad2 (:54-68)          -> hgp_pcg_solve (device-side early-exit flag)
 The spectrum attributes C, D, D_sqrt, Di, Di_sqrt are materialised lazily (they are
 M'-sized and the operators never need them).
+
+Autograd: in the reference every operator is torch arithmetic on D = clamp(Re FFT(embed(column)))
+(`:20-31`), so gradients reach the vector AND the column (kernel hyper-parameters).  Here
+`_ToeplitzOp` gives the same: vector gradient = the adjoint operator (K, C^-1 self-adjoint;
+R <-> R^T), column gradient = hgp_plan_column_grad.  Without a grad-requiring input the
+operators call the plan directly.
 """
 import numpy as np
 import torch
+from torch.autograd import Function
 
 from hipgp_amd import _lib
 from hipgp_amd.plan import ToeplitzPlan
 from hipgp_amd.ziggy.misc._inv_matmul import InvMatmul
 from hipgp_amd.ziggy.misc.cg import conj_grad2
+
+
+_ADJOINT = {_lib.OP_K: _lib.OP_K, _lib.OP_CINV: _lib.OP_CINV, _lib.OP_RT: _lib.OP_R, _lib.OP_R: _lib.OP_RT}
+
+
+class _ToeplitzOp(Function):
+    @staticmethod
+    def forward(ctx, plan, op, column, vec):
+        ctx.plan, ctx.op = plan, op
+        ctx.save_for_backward(vec)
+        return plan.apply(op, vec.detach())
+
+    @staticmethod
+    def backward(ctx, grad):
+        (vec,) = ctx.saved_tensors
+        grad = grad.contiguous()
+        gcol = gvec = None
+        if ctx.needs_input_grad[2]:
+            gcol = ctx.plan.column_grad(ctx.op, vec.detach(), grad)
+        if ctx.needs_input_grad[3]:
+            gvec = ctx.plan.apply(_ADJOINT[ctx.op], grad)
+        return None, None, gcol, gvec
 
 
 class ToeplitzTensor:
@@ -54,21 +83,26 @@ class ToeplitzTensor:
         # from it, toeplitz_tensor.py:150): keep the same AttributeError behaviour.
         return self.cvec_shape
 
+    def _op(self, op, vec):
+        if torch.is_grad_enabled() and (vec.requires_grad or self.column.requires_grad):
+            return _ToeplitzOp.apply(self._plan, op, self.column, vec)
+        return self._plan.apply(op, vec)
+
     def _matmul_by_K(self, vec):
         self._check_batch()
-        return self._plan.apply(_lib.OP_K, vec)
+        return self._op(_lib.OP_K, vec)
 
     def _matmul_by_RT(self, vec):
         self._check_batch()
-        return self._plan.apply(_lib.OP_RT, vec)
+        return self._op(_lib.OP_RT, vec)
 
     def _matmul_by_R(self, vec):
         self._check_batch()
-        return self._plan.apply(_lib.OP_R, vec.reshape(vec.shape[0], -1))
+        return self._op(_lib.OP_R, vec.reshape(vec.shape[0], -1))
 
     def _matmul_by_Cinv(self, vec):
         self._check_batch()
-        return self._plan.apply(_lib.OP_CINV, vec)
+        return self._op(_lib.OP_CINV, vec)
 
     def toeplitz_gram(self, xgrids, kernel, jitter_val):
         """first row k(x0, x_j) plus nugget on c0 (`toeplitz_tensor.py:127-133`)."""

@@ -172,6 +172,26 @@ int hgp_block_stats(int dtype, int ndim, const int64_t* dims, const int64_t* blo
                     int64_t nrhs, const void* ivar, const void* S, void* gram, void* knSkn,
                     void* trSG, void* hip_stream);
 
+/* Backward of the solve w.r.t. the Toeplitz column, SURVEY §8(f) row 4.  Replaces gpytorch's
+ * sym_toeplitz_derivative_quadratic_form (reference ziggy/misc/gpt_toeplitz.py:169-209) as
+ * InvMatmul.backward calls it (ziggy/misc/_inv_matmul.py:52-60, left_vecs = [L; R],
+ * right_vecs = -0.5 [R; L] over the FLATTENED column):
+ *   out[i] = sum_j sum_k left_j[k] (right_j[k+i] + right_j[k-i])  (i >= 1, out-of-range terms 0)
+ *   out[0] = sum_j left_j . right_j
+ * left, right: (nvec, n) row layout (the reference's (n, s) input transposed), out: (n,), all
+ * device arrays of dtype.  Direct lagged sums (O(nvec n^2)), deterministic. */
+int hgp_sym_toeplitz_dqf(int dtype, const void* left, const void* right, int64_t nvec, int64_t n,
+                         void* out, void* hip_stream);
+
+/* Gradient of sum(g * op(x)) w.r.t. the plan's column through the operator's spectrum
+ * (K: D, CINV: 1/D, RT and R: D_sqrt; D = clamp(Re FFT_n(circulant_embed(column)), clamp_min),
+ * reference toeplitz_tensor.py:20-31, ops :70-125).  The x-gradient is the adjoint operator
+ * (K, CINV self-adjoint; R <-> RT) through hgp_toeplitz_apply.  x (nrhs, M) or (nrhs, M') for R,
+ * g shaped like op(x); column_grad (M,); device arrays of the plan dtype; fp64 chain (DCT-I pair
+ * on the m-grid); the filter correlation is direct, O(nrhs M M').  Synchronises the plan stream. */
+int hgp_plan_column_grad(hgp_plan* plan, int op, const void* x, const void* g, int64_t nrhs,
+                         void* column_grad);
+
 /* Sizes of a plan: M, M' and the padded FFT lengths per axis (K-type and R-type ops). */
 int hgp_plan_info(const hgp_plan* plan, int64_t* M, int64_t* Mprime, int64_t* L_K,
                   int64_t* L_R);

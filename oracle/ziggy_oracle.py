@@ -217,6 +217,70 @@ class ToeplitzOracle:
                           callback=callback)
 
 
+    # ---- backward w.r.t. the column ------------------------------------
+    def column_grad(self, op, x, g):
+        """d/dcolumn of sum(g * op(x)) as torch autograd differentiates the reference:
+        op = crop?(Re IFFT(S . FFT(pad? x))) with S in {D, 1/D, sqrt D} (`toeplitz_tensor.py:70-125`),
+        D = clamp(Re FFT(C), 1e-6) (`:25-31`), C = circulant_embed(column) (`:20, 135-143`).
+        dL/dS = sum_b Re(FFT(x_b) conj(FFT(g_b))) / N; dL/dD = dL/dS S'(D) [Draw >= 1e-6];
+        dL/dC = Re FFT(dL/dD); dL/dcolumn = adjoint of the embedding (sum of the copies)."""
+        ax = tuple(range(1, self.ndim + 1))
+        N = float(self.Mp)
+        x = np.asarray(x, np.float64)
+        g = np.asarray(g, np.float64)
+        B = x.shape[0]
+        if op == "R":       # input on the n-grid, output cropped to the m-grid
+            X = sfft.fftn(x.reshape((B,) + self.ndims), axes=ax)
+            G = sfft.fftn(self._pad(g).astype(np.complex128), axes=ax)
+        elif op == "RT":    # input padded, output the full n-grid
+            X = sfft.fftn(self._pad(x).astype(np.complex128), axes=ax)
+            G = sfft.fftn(g.reshape((B,) + self.ndims), axes=ax)
+        else:               # K / Cinv: padded input, cropped output
+            X = sfft.fftn(self._pad(x).astype(np.complex128), axes=ax)
+            G = sfft.fftn(self._pad(g).astype(np.complex128), axes=ax)
+        dS = np.sum((X * np.conj(G)).real, axis=0) / N
+        D = self.D.astype(np.float64)
+        mask = sfft.fftn(self.C.astype(np.complex128)).real >= 1e-6
+        fac = {"K": np.ones_like(D), "Cinv": -1.0 / D ** 2}.get(op, 0.5 / np.sqrt(D))
+        dD = np.where(mask, dS * fac, 0.0)
+        dC = sfft.fftn(dD.astype(np.complex128)).real
+        for a, m in enumerate(self.dims):        # adjoint of cat([K, flip(K)[1:-1]]) per axis
+            if m < 2:
+                continue
+            head = np.take(dC, np.arange(m), axis=a)
+            tail = np.flip(np.take(dC, np.arange(m, dC.shape[a]), axis=a), axis=a)
+            idx = [slice(None)] * dC.ndim
+            idx[a] = slice(1, m - 1)
+            head[tuple(idx)] += tail
+            dC = head
+        return dC.reshape(-1)
+
+
+def sym_toeplitz_dqf(left_vectors, right_vectors):
+    """gpytorch's sym_toeplitz_derivative_quadratic_form (`ziggy/misc/gpt_toeplitz.py:169-209`):
+    left/right (n, s); out[i] = sum_j sum_k l_j[k] (r_j[k+i] + r_j[k-i]) for i >= 1 (terms outside
+    [0, n) vanish), out[0] = sum_j l_j . r_j.  Linear correlations by FFT of length >= 2n."""
+    l = np.asarray(left_vectors, np.float64)
+    r = np.asarray(right_vectors, np.float64)
+    if l.ndim == 1:
+        l, r = l[:, None], r[:, None]
+    n = l.shape[0]
+    L = 1 << int(np.ceil(np.log2(2 * n)))
+    corr = np.fft.irfft(np.sum(np.conj(np.fft.rfft(l, L, axis=0)) * np.fft.rfft(r, L, axis=0), axis=1), L)
+    out = corr[:n].copy()                          # sum_k l[k] r[k+i]
+    out[1:] += corr[L - 1:L - n:-1]                # sum_k l[k] r[k-i]
+    return out
+
+
+def inv_matmul_column_grad(T, solves, grad_output, maxiter, tol):
+    """`InvMatmul.backward` (`ziggy/misc/_inv_matmul.py:27-64`): left solves (preconditioned) and
+    the column gradient over the flattened column; returns (column_grad, right_grad)."""
+    left = T.solve(grad_output, do_precond=True, maxiter=maxiter, tol=tol)
+    lv = np.concatenate([left, solves], 0).T
+    rv = np.concatenate([solves, left], 0).T * -0.5
+    return sym_toeplitz_dqf(lv, rv), left
+
+
 # --------------------------------------------------------------------------------------
 # CG (ziggy/misc/cg.py)
 # --------------------------------------------------------------------------------------

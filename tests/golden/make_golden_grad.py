@@ -9,6 +9,7 @@ Per case (G13: 1-D m=40; G14: 2-D 9x7; G15: 3-D 5x4x3), fp64 and fp32:
     and right-hand-side gradient for a random grad_output;
   * the whitening R^T (`toeplitz_tensor.py:85-97`) differentiated w.r.t. the column through
     D_sqrt = sqrt(clamp(Re FFT(embed(column)), 1e-6)) (`:20-31`);
+  * K, C^-1 and R differentiated w.r.t. the column through D, 1/D, D_sqrt (`:70-83, 99-125`);
   * end to end (ziggy whitening with learn_kernel): d/d(sig2, ell) of sum(W * R^T K^{-1} Knm^T)
     with Knm and the Toeplitz column from the same kernel parameters (`hipgp.py:117-146`).
 
@@ -76,6 +77,16 @@ def gen_case(zk, tt, dtype, tag, name, dims, kern, params, B, seed):
     gs, ge = torch.autograd.grad(loss, (sig2, ell))
     out.update({"x": _np(x), "W": _np(W), "kn": _np(kn), "loss": np.array(float(loss)),
                 "dsig2": np.array(float(gs)), "dell": np.array(float(ge))})
+    # (4) the other operators differentiated w.r.t. the column through D / 1/D / D_sqrt
+    #     (`toeplitz_tensor.py:70-83, 99-125`); drawn last so (1)-(3) keep their values
+    T4 = tt.ToeplitzTensor(grids, kfun, batch_shape=None, jitter_val=1e-3)
+    T4.set_batch_shape((B,))
+    for key, fn, nin, nout in (("K", T4._matmul_by_K, M, M), ("Cinv", T4._matmul_by_Cinv, M, M),
+                               ("R", T4._matmul_by_R, Mp, M)):
+        xv = torch.tensor(rs.randn(B, nin), dtype=dtype)
+        gv = torch.tensor(rs.randn(B, nout), dtype=dtype)
+        (gc,) = torch.autograd.grad((fn(xv) * gv).sum(), T4.column, retain_graph=True)
+        out.update({f"{key}_x": _np(xv), f"{key}_g": _np(gv), f"{key}_column_grad": _np(gc)})
     np.savez_compressed(os.path.join(OUT, f"{name}_{tag}.npz"), **out)
 
 
