@@ -27,6 +27,7 @@ EXPORTS = (
     "hgp_toeplitz_apply_pass", "hgp_op_pass_count", "hgp_pcg_rnorm2", "hgp_kuf_grid",
     "hgp_kuf_semi_mc", "hgp_kuf_semi_sqexp", "hgp_knn_doubly_diag", "hgp_meanfield_stats",
     "hgp_block_stats", "hgp_sym_toeplitz_dqf", "hgp_plan_column_grad",
+    "hgp_plan_dqf",
 )
 KERN_SQEXP, KERN_MATERN12, KERN_MATERN32, KERN_MATERN52, KERN_GNEITING = 0, 1, 2, 3, 4
 
@@ -73,6 +74,7 @@ def lib():
         "hgp_block_stats": (i32, [i32, i32, pi64, pi64, vp, i64, vp, vp, vp, vp, vp, vp]),
         "hgp_sym_toeplitz_dqf": (i32, [i32, vp, vp, i64, i64, vp, vp]),
         "hgp_plan_column_grad": (i32, [vp, i32, vp, vp, i64, vp]),
+        "hgp_plan_dqf": (i32, [vp, vp, vp, i64, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

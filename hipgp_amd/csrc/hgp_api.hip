@@ -44,6 +44,10 @@ int64_t next_pow2(int64_t v) {
 struct DevBuf {
   void* ptr = nullptr;
   size_t bytes = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { release(); }
   int ensure(size_t need) {
     if (need <= bytes) return 0;
     if (ptr) (void)hipFree(ptr);
@@ -997,6 +1001,39 @@ int hgp_sym_toeplitz_dqf(int dtype, const void* left, const void* right, int64_t
   return 0;
 }
 
+// F = FFT_L(conj(sum_b conj(V_b) H_b)) on the L-grid (L = L_K or L_R, fp64): Re F[t mod L] / prod L
+// = sum_b sum_j v_b[j] h_b[j + t] (hgp_grad.hip).  v rows on the m-grid (stride M); h rows on the
+// m-grid (zero-padded) or, h_periodic, on the n-grid (stride M').  Scratch: three L-grids.
+int xcorr_grid(hgp_plan* P, int useR, const void* v, const void* h, int h_periodic, int64_t nb, DevBuf* buf,
+               double2** F, GridDims* gout) {
+  hipStream_t s = P->stream;
+  const int64_t* L = useR ? P->LR : P->LK;
+  const DevBuf* tw = useR ? P->tw64R : P->tw64K;
+  const int64_t prodL = useR ? P->prodLR : P->prodLK;
+  GridDims gd;
+  gd.d = P->d;
+  for (int a = 0; a < 3; ++a) { gd.m[a] = P->m[a]; gd.n[a] = P->n[a]; gd.L[a] = L[a]; }
+  for (int i = 0; i < 3; ++i) HGP_TRY(buf[i].ensure((size_t)prodL * sizeof(double2)));
+  double2* z = reinterpret_cast<double2*>(buf[0].ptr);
+  double2* w = reinterpret_cast<double2*>(buf[1].ptr);
+  double2* S = reinterpret_cast<double2*>(buf[2].ptr);
+  const size_t es = P->esz;
+  const int64_t hs = h_periodic ? P->Mp : P->M;
+  for (int64_t b = 0; b < nb; ++b) {
+    pack_pair(P->dtype, static_cast<const char*>(v) + (size_t)(b * P->M) * es,
+              static_cast<const char*>(h) + (size_t)(b * hs) * es, h_periodic, gd, prodL, z, s);
+    double2* Z = nullptr;
+    HGP_TRY(fwd_grid_f64(P, L, tw, z, w, &Z));
+    xspec_acc(Z, S, gd, prodL, b == 0 ? 1 : 0, s);
+  }
+  if (nb == 0) HIP_TRY(hipMemsetAsync(S, 0, (size_t)prodL * sizeof(double2), s));
+  conj_inplace(S, prodL, s);
+  HGP_TRY(fwd_grid_f64(P, L, tw, S, z, F));
+  HIP_TRY(hipGetLastError());
+  *gout = gd;
+  return 0;
+}
+
 // d/dcolumn <g, op x> through the operator's spectrum S(D) (toeplitz_tensor.py:20-31, ops :70-125).
 // With A = DCT-I on the m-grid (A[f][x] = mu(x) cos(2 pi f x / n) per axis, dct_axis), D = A column
 // and the operator's generator c = A S(D) / N on the n-grid:
@@ -1016,23 +1053,24 @@ int hgp_plan_column_grad(hgp_plan* plan, int op, const void* x, const void* g, i
   GridDims gd;
   gd.d = P->d;
   for (int a = 0; a < 3; ++a) { gd.m[a] = P->m[a]; gd.n[a] = P->n[a]; gd.L[a] = P->LK[a]; }
-  DevBuf X, y1, y2;
+  DevBuf X, y1, y2, big[3];   // freed on return (after the stream sync below)
   HGP_TRY(X.ensure((size_t)Mp * sizeof(double)));
   HGP_TRY(y1.ensure((size_t)M * sizeof(double)));
   HGP_TRY(y2.ensure((size_t)M * sizeof(double)));
   double* Xp = reinterpret_cast<double*>(X.ptr);
   double* a = reinterpret_cast<double*>(y1.ptr);
   double* b = reinterpret_cast<double*>(y2.ptr);
-  if (nrhs == 0) HIP_TRY(hipMemsetAsync(Xp, 0, (size_t)Mp * sizeof(double), s));
-  else {
+  {
     // <g, op x> = sum_b sum_{j in m-grid} v_b[j] sum_w c[w] h_b[(j + w) mod n] with (v, h) =
     // (x, g) for R^T (g on the n-grid), (g, x) for R (x on the n-grid), (x, g) for K / C^-1
-    // (g on the m-grid, zero elsewhere: the crop)
+    // (g on the m-grid, zero elsewhere: the crop); X[w] = dL/dc[w] by one cross spectrum
     const void* vv = op == HGP_OP_R ? g : x;
     const void* hh = op == HGP_OP_R ? x : g;
-    const int h_on_m = (op == HGP_OP_K || op == HGP_OP_CINV) ? 1 : 0;
-    hipError_t e = circ_xcorr(P->dtype, vv, hh, h_on_m, nrhs, gd, M, Mp, Xp, s);
-    if (e != hipSuccess) return fail(HGP_E_HIP, std::string("circ_xcorr: ") + hipGetErrorString(e));
+    const int periodic = (op == HGP_OP_R || op == HGP_OP_RT) ? 1 : 0;
+    double2* F = nullptr;
+    GridDims gl;
+    HGP_TRY(xcorr_grid(P, periodic, vv, hh, periodic, nrhs, big, &F, &gl));
+    gather_n(F, gl, periodic, Mp, 1.0 / (double)(periodic ? P->prodLR : P->prodLK), Xp, s);
   }
   fold_div_mu(Xp, M, gd, a, s);
   for (int ax = 0; ax < P->d; ++ax) {
@@ -1049,6 +1087,22 @@ int hgp_plan_column_grad(hgp_plan* plan, int op, const void* x, const void* g, i
   HIP_TRY(hipGetLastError());
   // the scratch is freed on return: finish its users first
   HIP_TRY(hipStreamSynchronize(s));
+  return 0;
+}
+
+int hgp_plan_dqf(hgp_plan* plan, const void* left, const void* right, int64_t nvec, void* out) {
+  HGP_TRY(check_plan(plan));
+  if (nvec < 0 || out == nullptr || (nvec > 0 && (left == nullptr || right == nullptr)))
+    return fail(HGP_E_ARG, "bad nvec or null pointer");
+  if (plan->d < 1) return fail(HGP_E_UNSUPPORTED, "a grid with a single point");
+  HGP_TRY(use_device(plan));
+  DevBuf big[3];
+  double2* F = nullptr;
+  GridDims gl;
+  HGP_TRY(xcorr_grid(plan, 0, left, right, 0, nvec, big, &F, &gl));
+  gather_flat(plan->dtype, F, gl, plan->M, 1.0 / (double)plan->prodLK, out, plan->stream);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(plan->stream));
   return 0;
 }
 

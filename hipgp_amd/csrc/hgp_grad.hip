@@ -8,11 +8,13 @@
 //   Direct lagged sums, O(nvec * n^2): a block owns 256 lags, u and the two v windows of a
 //   256-wide k tile are staged in LDS (u read as a broadcast, the windows conflict-free), partial
 //   sums per tile in T, tiles accumulated in fp64.  Deterministic (fixed order).
-// * k_circ_xcorr + fold/mask/scale helpers: gradient of <g, op v> w.r.t. the column through the
-//   operator's spectrum (D, 1/D or D_sqrt = sqrt(clamp(Re FFT_n(embed(column)), cmin)),
-//   toeplitz_tensor.py:20-31; ops :70-125), e.g. for R^T:
-//     X[w]   = sum_b sum_{j in m-grid} v_b[j] g_b[(j + w) mod n]         (n-grid, = dL/ds[w])
-//   then folded to the unique m-grid values and chained through the DCT-I pair in hgp_api.hip.
+// * gradient of <g, op v> w.r.t. the column through the operator's spectrum (D, 1/D or
+//   D_sqrt = sqrt(clamp(Re FFT_n(embed(column)), cmin)), toeplitz_tensor.py:20-31; ops :70-125),
+//   e.g. for R^T:  X[w] = sum_b sum_{j in m-grid} v_b[j] g_b[(j + w) mod n]   (n-grid, = dL/ds[w])
+//   by one fp64 cross spectrum per RHS on the power-of-two grid (k_pack_pair, k_xspec_acc,
+//   k_gather_n), then folded to the unique m-grid values (k_fold_div) and chained through the
+//   DCT-I pair in hgp_api.hip.  The plan-based dqf (k_gather_flat) folds the d-D correlation
+//   onto the flattened lags, so InvMatmul's column gradient is O(M log M) as well.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -70,50 +72,6 @@ __device__ __forceinline__ void decode(int64_t f, const int* ext, int d, int* c)
   }
 }
 
-// X[w] = sum_b sum_j v_b[j] g_b[(j + w) mod n], w over the n-grid; thread per w, j tiles in LDS.
-// g rows live on the n-grid, or (g_on_m) on the m-grid, zero outside it (the K / C^-1 crop).
-template <typename T>
-__global__ __launch_bounds__(GT) void k_circ_xcorr(const T* __restrict__ v, const T* __restrict__ g, int64_t nrhs,
-                                                   int64_t M, int64_t Mp, Geo G, int g_on_m,
-                                                   double* __restrict__ X) {
-  __shared__ T sv[GT];
-  __shared__ int sj[3][GT];
-  const int t = threadIdx.x;
-  const int64_t w = (int64_t)blockIdx.x * GT + t;
-  int wc[3] = {0, 0, 0};
-  decode(w < Mp ? w : 0, G.n, G.d, wc);
-  double acc = 0.0;
-  for (int64_t b = 0; b < nrhs; ++b) {
-    const T* vb = v + b * M;
-    const T* gb = g + b * (g_on_m ? M : Mp);
-    for (int64_t j0 = 0; j0 < M; j0 += GT) {
-      __syncthreads();
-      const int64_t j = j0 + t;
-      int jc[3] = {0, 0, 0};
-      if (j < M) decode(j, G.m, G.d, jc);
-      sv[t] = (j < M) ? vb[j] : T(0);
-      sj[0][t] = jc[0]; sj[1][t] = jc[1]; sj[2][t] = jc[2];
-      __syncthreads();
-      const int cnt = (int)((M - j0) < GT ? (M - j0) : GT);
-      T s = 0;
-      for (int q = 0; q < cnt; ++q) {
-        int64_t idx = 0;
-        bool in = true;
-        for (int a = 0; a < G.d; ++a) {
-          int e = sj[a][q] + wc[a];
-          if (e >= G.n[a]) e -= G.n[a];
-          const int ext = g_on_m ? G.m[a] : G.n[a];
-          in = in && e < ext;
-          idx = idx * ext + e;
-        }
-        if (in) s += sv[q] * gb[idx];
-      }
-      acc += (double)s;
-    }
-  }
-  if (w < Mp) X[w] = acc;
-}
-
 __device__ __forceinline__ double mu_of(const int* c, const Geo& G) {
   double mu = 1.0;
   for (int a = 0; a < G.d; ++a)
@@ -167,6 +125,153 @@ __global__ void k_mul_mu_out(const double* __restrict__ r, int64_t M, Geo G, T* 
   out[x] = (T)(r[x] * mu_of(c, G));
 }
 
+// ---- FFT route: cross-correlations on the power-of-two grids --------------------------------
+// corr[t] = sum_b sum_j v_b[j] h_b[j + t] is computed as IFFT_L(sum_b conj(V_b) H_b) on an L-grid
+// large enough that the lags needed do not alias (L_K >= 2m - 1 for lags in (-m, m) with h on the
+// m-grid; L_R >= n + m - 1 for lags [0, n) with h the n-periodic extension).  One complex fp64
+// FFT per RHS: z = pad(v) + i h_ext, split by Hermitian symmetry.
+struct LGeo {
+  int d;
+  int m[3], n[3], L[3];
+};
+
+// The FWD passes store frequency k of a length-L line at position pos_of(k): even k = 2s at s,
+// odd k = 2s + 1 at L/2 + s (hgp_pass.hpp: the even / odd frequency halves).
+__device__ __forceinline__ int pos_of(int k, int L) { return (k & 1) ? (L >> 1) + (k >> 1) : (k >> 1); }
+__device__ __forceinline__ int freq_of(int s, int L) { return s < (L >> 1) ? 2 * s : 2 * (s - (L >> 1)) + 1; }
+
+__device__ __forceinline__ void decodeL(int64_t f, const LGeo& G, int* c) {
+  for (int a = G.d - 1; a >= 0; --a) {
+    c[a] = (int)(f & (G.L[a] - 1));
+    f >>= __ffs(G.L[a]) - 1;
+  }
+}
+
+template <typename T>
+__global__ void k_pack_pair(const T* __restrict__ v, const T* __restrict__ h, int h_periodic, LGeo G,
+                            int64_t prodL, double2* __restrict__ z) {
+  const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= prodL) return;
+  int c[3];
+  decodeL(f, G, c);
+  bool inm = true, inh = true;
+  int64_t im = 0, ih = 0;
+  for (int a = 0; a < G.d; ++a) {
+    inm = inm && c[a] < G.m[a];
+    im = im * G.m[a] + c[a];
+    if (h_periodic) {
+      inh = inh && c[a] < G.n[a] + G.m[a] - 1;
+      ih = ih * G.n[a] + (c[a] >= G.n[a] ? c[a] - G.n[a] : c[a]);
+    }
+  }
+  double2 r;
+  r.x = inm ? (double)v[im] : 0.0;
+  r.y = h_periodic ? (inh ? (double)h[ih] : 0.0) : (inm ? (double)h[im] : 0.0);
+  z[f] = r;
+}
+
+// S (+)= conj(V) H with V = (Z + conj Z(-f)) / 2, H = (Z - conj Z(-f)) / 2i; Z in the FWD
+// passes' stored order, S written in natural frequency order (the input of the inverse FFT)
+__global__ void k_xspec_acc(const double2* __restrict__ Z, double2* __restrict__ S, LGeo G, int64_t prodL,
+                            int first) {
+  const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= prodL) return;
+  int c[3];
+  decodeL(f, G, c);
+  int64_t nf = 0, fn = 0;
+  for (int a = 0; a < G.d; ++a) {
+    const int k = freq_of(c[a], G.L[a]);
+    nf = nf * G.L[a] + pos_of((G.L[a] - k) & (G.L[a] - 1), G.L[a]);
+    fn = fn * G.L[a] + k;
+  }
+  const double2 zf = Z[f], zn = Z[nf];
+  const double vr = 0.5 * (zf.x + zn.x), vi = 0.5 * (zf.y - zn.y);      // V
+  const double hr = 0.5 * (zf.y + zn.y), hi = -0.5 * (zf.x - zn.x);     // H
+  double2 p;
+  p.x = vr * hr + vi * hi;                                              // conj(V) H
+  p.y = vr * hi - vi * hr;
+  if (!first) { const double2 o = S[fn]; p.x += o.x; p.y += o.y; }
+  S[fn] = p;
+}
+
+__global__ void k_conj(double2* __restrict__ S, int64_t n) {
+  const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (f < n) S[f].y = -S[f].y;
+}
+
+// X[w] (n-grid) = sum of corr[t] over the lags t == w (mod n) of the window; F = FFT(conj S) in
+// stored order, so corr[t] = Re F[pos_of(t mod L)] / prodL.  Window: [0, n) (periodic h) or (-m, m) (h on the m-grid).
+__global__ void k_gather_n(const double2* __restrict__ F, LGeo G, int h_periodic, int64_t Mp, double invL,
+                           double* __restrict__ X) {
+  const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= Mp) return;
+  int c[3] = {0, 0, 0};
+  int64_t r = w;
+  for (int a = G.d - 1; a >= 0; --a) { c[a] = (int)(r % G.n[a]); r /= G.n[a]; }
+  int t[3][2], nt[3];
+  for (int a = 0; a < G.d; ++a) {
+    nt[a] = 0;
+    if (h_periodic || c[a] < G.m[a]) t[a][nt[a]++] = c[a];
+    if (!h_periodic && c[a] >= G.m[a] - 1) t[a][nt[a]++] = c[a] - G.n[a];
+  }
+  double s = 0.0;
+  const int combos = 1 << G.d;
+  for (int k = 0; k < combos; ++k) {
+    int64_t idx = 0;
+    bool ok = true;
+    for (int a = 0; a < G.d; ++a) {
+      const int sel = (k >> a) & 1;
+      if (sel >= nt[a]) { ok = false; break; }
+      idx = idx * G.L[a] + pos_of((t[a][sel] + G.L[a]) & (G.L[a] - 1), G.L[a]);
+    }
+    if (ok) s += F[idx].x;
+  }
+  X[w] = s * invL;
+}
+
+// dqf over the flattened m-grid from the d-D correlation C (lags (-m, m), corr = Re F / prodL):
+// out[i] = sum over the signed-digit preimages a of i (flat(a) = i) of C[a] + C[-a]; out[0] = C[0]
+template <typename T>
+__global__ void k_gather_flat(const double2* __restrict__ F, LGeo G, int64_t M, double invL, T* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M) return;
+  double s = 0.0;
+  const int combos = 1 << (G.d - 1);
+  for (int k = 0; k < combos; ++k) {
+    int64_t rem = i;
+    int dig[3];
+    bool ok = true;
+    for (int a = G.d - 1; a >= 1; --a) {
+      const int r = (int)(rem % G.m[a]);
+      int64_t q = rem / G.m[a];
+      if ((k >> (a - 1)) & 1) {            // borrow: digit r - m (needs r > 0)
+        if (r == 0) { ok = false; break; }
+        dig[a] = r - G.m[a];
+        q += 1;
+      } else {
+        dig[a] = r;
+      }
+      rem = q;
+    }
+    if (!ok || rem >= G.m[0]) continue;
+    dig[0] = (int)rem;
+    int64_t ip = 0, in = 0;
+    for (int a = 0; a < G.d; ++a) {
+      ip = ip * G.L[a] + pos_of((dig[a] + G.L[a]) & (G.L[a] - 1), G.L[a]);
+      in = in * G.L[a] + pos_of((G.L[a] - dig[a]) & (G.L[a] - 1), G.L[a]);
+    }
+    s += i == 0 ? F[ip].x : F[ip].x + F[in].x;
+  }
+  out[i] = (T)(s * invL);
+}
+
+LGeo make_lgeo(const GridDims& g) {
+  LGeo G;
+  G.d = g.d;
+  for (int a = 0; a < 3; ++a) { G.m[a] = (int)g.m[a]; G.n[a] = (int)g.n[a]; G.L[a] = (int)g.L[a]; }
+  return G;
+}
+
 Geo make_geo(const GridDims& g) {
   Geo G;
   G.d = g.d;
@@ -187,16 +292,6 @@ hipError_t sym_toeplitz_dqf(int dtype, const void* u, const void* v, int64_t nve
   return hipGetLastError();
 }
 
-hipError_t circ_xcorr(int dtype, const void* v, const void* g, int g_on_m, int64_t nrhs, const GridDims& gd,
-                      int64_t M, int64_t Mp, double* X, hipStream_t s) {
-  const Geo G = make_geo(gd);
-  if (dtype == 1)
-    k_circ_xcorr<double><<<nblk(Mp, GT), GT, 0, s>>>((const double*)v, (const double*)g, nrhs, M, Mp, G, g_on_m, X);
-  else
-    k_circ_xcorr<float><<<nblk(Mp, GT), GT, 0, s>>>((const float*)v, (const float*)g, nrhs, M, Mp, G, g_on_m, X);
-  return hipGetLastError();
-}
-
 void fold_div_mu(const double* X, int64_t M, const GridDims& gd, double* y, hipStream_t s) {
   k_fold_div<<<nblk(M, 256), 256, 0, s>>>(X, M, make_geo(gd), y);
 }
@@ -208,6 +303,29 @@ void spec_bwd(double* y, const double* D3, int64_t M, int kind, double cmin, hip
 void mul_mu_out(int dtype, const double* r, int64_t M, const GridDims& gd, void* out, hipStream_t s) {
   if (dtype == 1) k_mul_mu_out<double><<<nblk(M, 256), 256, 0, s>>>(r, M, make_geo(gd), (double*)out);
   else k_mul_mu_out<float><<<nblk(M, 256), 256, 0, s>>>(r, M, make_geo(gd), (float*)out);
+}
+
+void pack_pair(int dtype, const void* v, const void* h, int h_periodic, const GridDims& gd, int64_t prodL, double2* z,
+               hipStream_t s) {
+  const LGeo G = make_lgeo(gd);
+  if (dtype == 1) k_pack_pair<double><<<nblk(prodL, 256), 256, 0, s>>>((const double*)v, (const double*)h, h_periodic, G, prodL, z);
+  else k_pack_pair<float><<<nblk(prodL, 256), 256, 0, s>>>((const float*)v, (const float*)h, h_periodic, G, prodL, z);
+}
+
+void xspec_acc(const double2* Z, double2* S, const GridDims& gd, int64_t prodL, int first, hipStream_t s) {
+  k_xspec_acc<<<nblk(prodL, 256), 256, 0, s>>>(Z, S, make_lgeo(gd), prodL, first);
+}
+
+void conj_inplace(double2* S, int64_t n, hipStream_t s) { k_conj<<<nblk(n, 256), 256, 0, s>>>(S, n); }
+
+void gather_n(const double2* F, const GridDims& gd, int h_periodic, int64_t Mp, double invL, double* X, hipStream_t s) {
+  k_gather_n<<<nblk(Mp, 256), 256, 0, s>>>(F, make_lgeo(gd), h_periodic, Mp, invL, X);
+}
+
+void gather_flat(int dtype, const double2* F, const GridDims& gd, int64_t M, double invL, void* out, hipStream_t s) {
+  const LGeo G = make_lgeo(gd);
+  if (dtype == 1) k_gather_flat<double><<<nblk(M, 256), 256, 0, s>>>(F, G, M, invL, (double*)out);
+  else k_gather_flat<float><<<nblk(M, 256), 256, 0, s>>>(F, G, M, invL, (float*)out);
 }
 
 }  // namespace hgp

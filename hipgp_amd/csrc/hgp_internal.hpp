@@ -65,11 +65,15 @@ hipError_t kuf_semi_grid(int dtype, int kind, int method, int ndim, const int64_
 // backward w.r.t. the Toeplitz column (hgp_grad.hip)
 hipError_t sym_toeplitz_dqf(int dtype, const void* u, const void* v, int64_t nvec, int64_t n, void* out,
                             hipStream_t s);
-hipError_t circ_xcorr(int dtype, const void* v, const void* g, int g_on_m, int64_t nrhs, const GridDims& gd,
-                      int64_t M, int64_t Mp, double* X, hipStream_t s);
 void fold_div_mu(const double* X, int64_t M, const GridDims& gd, double* y, hipStream_t s);
 void spec_bwd(double* y, const double* D3, int64_t M, int kind, double cmin, hipStream_t s);
 void mul_mu_out(int dtype, const double* r, int64_t M, const GridDims& gd, void* out, hipStream_t s);
+void pack_pair(int dtype, const void* v, const void* h, int h_periodic, const GridDims& gd, int64_t prodL, double2* z,
+               hipStream_t s);
+void xspec_acc(const double2* Z, double2* S, const GridDims& gd, int64_t prodL, int first, hipStream_t s);
+void conj_inplace(double2* S, int64_t n, hipStream_t s);
+void gather_n(const double2* F, const GridDims& gd, int h_periodic, int64_t Mp, double invL, double* X, hipStream_t s);
+void gather_flat(int dtype, const double2* F, const GridDims& gd, int64_t M, double invL, void* out, hipStream_t s);
 // CG
 int update_np(int64_t M);
 template <typename T> void cg_init(const void* b, void* x, void* r, int64_t n, hipStream_t s);

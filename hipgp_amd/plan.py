@@ -122,6 +122,19 @@ class ToeplitzPlan:
                                          ctypes.c_void_p(out.data_ptr())))
         return out
 
+    def dqf(self, left, right):
+        """sym_toeplitz_derivative_quadratic_form over the flattened grid (`gpt_toeplitz.py:169-209`)
+        through the grid's own factorisation (hgp_plan_dqf): left/right (nvec, M) row layout."""
+        left = self._vec(left, "left", self.M)
+        right = self._vec(right, "right", self.M)
+        if left.shape != right.shape:
+            raise ValueError(f"left {tuple(left.shape)} / right {tuple(right.shape)}")
+        out = torch.empty(self.M, dtype=self.dtype, device=self.device)
+        self._bind_stream()
+        check(lib().hgp_plan_dqf(self._h, ctypes.c_void_p(left.data_ptr()), ctypes.c_void_p(right.data_ptr()),
+                                 left.shape[0], ctypes.c_void_p(out.data_ptr())))
+        return out
+
     # -- PCG ---------------------------------------------------------------------------------
     def pcg(self, b, maxiter, tol, precond=True, out=None, return_iters=False):
         """Batched PCG with the conj_grad2 recurrence (`cg.py:44-80`), row layout (nrhs, M)."""

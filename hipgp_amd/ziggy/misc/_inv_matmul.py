@@ -4,7 +4,9 @@ forward: no-grad PCG solve (hgp_pcg_solve).  backward (`:27-64`): left solves
 L = K^{-1} grad_output by a second solve (always preconditioned, as the reference); the
 right-hand-side gradient is L; the Toeplitz-column gradient is gpytorch's
 sym_toeplitz_derivative_quadratic_form([L; R]^T, -0.5 [R; L]^T) over the flattened column
-(`:52-60`, hgp_sym_toeplitz_dqf), summed to the column's shape (`:62-63`).
+(`:52-60`), summed to the column's shape (`:62-63`).  The quadratic form runs through the
+grid's factorisation (hgp_plan_dqf: the flattened-index correlation is a fold of the d-D one,
+one fp64 FFT per vector pair) -- the reference's 1-D rule, evaluated in O(M log M).
 """
 import torch
 from torch.autograd import Function
@@ -35,9 +37,13 @@ class InvMatmul(Function):
         column_grad = None
         if ctx.needs_input_grad[1]:
             with torch.no_grad():
-                left_vecs = torch.cat([left_solves, right_solves], 0).t()
-                right_vecs = torch.cat([right_solves, left_solves], 0).t().mul(-0.5)
-                column_grad = sym_toeplitz_dqf(left_vecs, right_vecs)
+                left_vecs = torch.cat([left_solves, right_solves], 0)
+                right_vecs = torch.cat([right_solves, left_solves], 0).mul(-0.5)
+                plan = getattr(ctx.toeplitz_tensor, "_plan", None)
+                if plan is not None:
+                    column_grad = plan.dqf(left_vecs, right_vecs)
+                else:
+                    column_grad = sym_toeplitz_dqf(left_vecs.t(), right_vecs.t())
             column = ctx.toeplitz_tensor.column
             if column_grad.dim() > column.dim():
                 column_grad = column_grad.view(-1, *column.shape).sum(0)

@@ -183,12 +183,19 @@ int hgp_block_stats(int dtype, int ndim, const int64_t* dims, const int64_t* blo
 int hgp_sym_toeplitz_dqf(int dtype, const void* left, const void* right, int64_t nvec, int64_t n,
                          void* out, void* hip_stream);
 
+/* hgp_sym_toeplitz_dqf for n = the plan's M, through the grid's factorisation: the flattened-index
+ * correlation sum_k u[k] v[k+i] is the fold of the d-D correlation over its signed-digit lags,
+ * computed as one fp64 FFT per vector pair on the L_K grid (O(nvec prod L_K log)).  left, right
+ * (nvec, M) row layout, out (M,), plan dtype.  Synchronises the plan stream. */
+int hgp_plan_dqf(hgp_plan* plan, const void* left, const void* right, int64_t nvec, void* out);
+
 /* Gradient of sum(g * op(x)) w.r.t. the plan's column through the operator's spectrum
  * (K: D, CINV: 1/D, RT and R: D_sqrt; D = clamp(Re FFT_n(circulant_embed(column)), clamp_min),
  * reference toeplitz_tensor.py:20-31, ops :70-125).  The x-gradient is the adjoint operator
  * (K, CINV self-adjoint; R <-> RT) through hgp_toeplitz_apply.  x (nrhs, M) or (nrhs, M') for R,
  * g shaped like op(x); column_grad (M,); device arrays of the plan dtype; fp64 chain (DCT-I pair
- * on the m-grid); the filter correlation is direct, O(nrhs M M').  Synchronises the plan stream. */
+ * on the m-grid); the filter correlation is one fp64 cross spectrum per RHS on the L_K / L_R grid.
+ * Synchronises the plan stream. */
 int hgp_plan_column_grad(hgp_plan* plan, int op, const void* x, const void* g, int64_t nrhs,
                          void* column_grad);
 

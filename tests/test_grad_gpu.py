@@ -152,3 +152,23 @@ def test_column_grad_vs_oracle(dims):
         x, g = rs.randn(3, nin), rs.randn(3, nout)
         got = P.column_grad(op, torch.tensor(x, device=DEV), torch.tensor(g, device=DEV))
         assert rel_err(_np(got), T.column_grad(name, x, g)) < 1e-9, name
+
+
+@pytest.mark.parametrize("dims", [(300,), (12, 10), (2, 9), (6, 5, 4), (3, 2, 7)], ids=lambda d: "x".join(map(str, d)))
+@pytest.mark.parametrize("tag", ["f64", "f32"])
+def test_plan_dqf_vs_oracle(dims, tag):
+    """hgp_plan_dqf (the flattened-index quadratic form through the grid's factorisation) against
+    the oracle's 1-D restatement and the direct-sum kernel, incl. axes of 2 points."""
+    from hipgp_amd.plan import ToeplitzPlan, sym_toeplitz_dqf
+    rs = np.random.RandomState(len(dims) * 7 + dims[-1])
+    M = int(np.prod(dims))
+    l, r = rs.randn(4, M), rs.randn(4, M)
+    P = ToeplitzPlan(dims, dtype=DT[tag], device=DEV)
+    P.set_column(torch.tensor(np.exp(-np.arange(M) / 5.0), dtype=DT[tag], device=DEV))
+    got = P.dqf(torch.tensor(l, dtype=DT[tag], device=DEV), torch.tensor(r, dtype=DT[tag], device=DEV))
+    want = zo.sym_toeplitz_dqf(l.T, r.T)
+    tol = 1e-12 if tag == "f64" else 2e-6
+    assert rel_err(_np(got), want) < tol
+    direct = sym_toeplitz_dqf(torch.tensor(l.T, dtype=DT[tag], device=DEV),
+                              torch.tensor(r.T, dtype=DT[tag], device=DEV))
+    assert rel_err(_np(direct), want) < tol

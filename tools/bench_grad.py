@@ -22,20 +22,27 @@ def t_ms(fn, reps=3):
     return a.elapsed_time(b) / reps
 
 
-for n, nvec in ((4096, 8), (65536, 8), (262144, 64)):
+for n, nvec in ((4096, 8), (65536, 8)):
     l = torch.randn(n, nvec, device="cuda")
     r = torch.randn(n, nvec, device="cuda")
     ms = t_ms(lambda: sym_toeplitz_dqf(l, r), reps=2 if n > 100000 else 5)
     fl = 4.0 * nvec * n * n     # 2 FMAs per (lag, k, vector)
     print(json.dumps({"kernel": "k_dqf", "n": n, "nvec": nvec, "ms": ms, "tflops": fl / ms / 1e9}), flush=True)
 
-for dims, B in (((64, 64), 4), ((128, 128), 4), ((32, 32, 16), 4)):
+for dims, B in (((64, 64), 4), ((1024, 1024), 32), ((256, 256, 128), 8)):
     P = ToeplitzPlan(dims, dtype=torch.float32, device="cuda")
     M, Mp = P.M, P.Mprime
     col = torch.exp(-torch.linspace(0, 3, M, device="cuda"))
     P.set_column(col)
     v = torch.randn(B, M, device="cuda")
     g = torch.randn(B, Mp, device="cuda")
-    ms = t_ms(lambda: P.column_grad(_lib.OP_RT, v, g))
-    fl = 2.0 * B * M * Mp
-    print(json.dumps({"kernel": "column_grad RT", "dims": dims, "B": B, "ms": ms, "tflops": fl / ms / 1e9}), flush=True)
+    ms = t_ms(lambda: P.column_grad(_lib.OP_RT, v, g), reps=2)
+    print(json.dumps({"kernel": "column_grad RT (fp64 cross spectrum on L_R)", "dims": dims, "B": B,
+                      "L_R": P.L_R, "ms": ms}), flush=True)
+    u = torch.randn(2 * B, M, device="cuda")
+    w = torch.randn(2 * B, M, device="cuda")
+    ms = t_ms(lambda: P.dqf(u, w), reps=2)
+    print(json.dumps({"kernel": "plan dqf (InvMatmul column grad, fp64 FFT on L_K)", "dims": dims, "nvec": 2 * B,
+                      "L_K": P.L_K, "ms": ms}), flush=True)
+    del v, g, u, w, P
+    torch.cuda.empty_cache()
