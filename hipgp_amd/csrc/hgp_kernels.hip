@@ -317,31 +317,45 @@ __global__ __launch_bounds__(UPD_THREADS) void k_rowdot_part(const T* __restrict
 }
 
 // out[b] = sum_g part[b*np + g]   (one wave per RHS, fixed tree)
+// One block of RED_THREADS per RHS sums that RHS's row of partials: every lane issues its
+// loads up front (np <= ~1k: one or two rounds), then a wave shuffle and a 4-entry LDS
+// combine.  A wave per RHS walking the row serially left these scalar kernels at ~15 us,
+// on the critical path between the column pass and the row-inverse pass of each chunk.
+constexpr int RED_THREADS = 256;
 template <typename T>
-__global__ void k_reduce_rows(const T* __restrict__ part, int np, int nrhs, T* __restrict__ out) {
-  const int b = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (b >= nrhs) return;
+__device__ __forceinline__ T block_row_sum(const T* __restrict__ row, int np) {
+  __shared__ T red[RED_THREADS / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   T s = 0;
-  for (int g = lane; g < np; g += 64) s += part[(int64_t)b * np + g];
+#pragma unroll 4
+  for (int g = threadIdx.x; g < np; g += RED_THREADS) s += row[g];
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-  if (lane == 0) out[b] = s;
+  if (lane == 0) red[w] = s;
+  __syncthreads();
+  T t = 0;
+#pragma unroll
+  for (int i = 0; i < RED_THREADS / 64; ++i) t += red[i];
+  return t;
+}
+
+template <typename T>
+__global__ __launch_bounds__(RED_THREADS) void k_reduce_rows(const T* __restrict__ part, int np, int nrhs,
+                                                             T* __restrict__ out) {
+  const int b = blockIdx.x;
+  const T s = block_row_sum(part + (int64_t)b * np, np);
+  if (threadIdx.x == 0) out[b] = s;
 }
 
 // per RHS: alpha = rs / sum(part)   (cg.py:66)
 template <typename T>
-__global__ void k_cg_alpha(const T* __restrict__ part, int np, int nrhs, const T* __restrict__ rs,
-                           T* __restrict__ alpha, const int* done) {
-  if (*done) return;
-  const int b = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (b >= nrhs) return;
-  T s = 0;
-  for (int g = lane; g < np; g += 64) s += part[(int64_t)b * np + g];
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-  if (lane == 0) alpha[b] = rs[b] / s;
+__global__ __launch_bounds__(RED_THREADS) void k_cg_alpha(const T* __restrict__ part, int np, int nrhs,
+                                                          const T* __restrict__ rs, T* __restrict__ alpha,
+                                                          const int* done) {
+  if (*done) return;   // block-uniform
+  const int b = blockIdx.x;
+  const T s = block_row_sum(part + (int64_t)b * np, np);
+  if (threadIdx.x == 0) alpha[b] = rs[b] / s;
 }
 
 // x += alpha p ; r -= alpha Ap ; partial r.r    (cg.py:67-69)
@@ -402,17 +416,12 @@ __global__ __launch_bounds__(1024) void k_cg_check(const T* __restrict__ part, i
 
 // zr = sum(part); beta = zr / rs; rs = zr   (cg.py:74 and next iteration's rs, cg.py:64)
 template <typename T>
-__global__ void k_cg_beta(const T* __restrict__ part, int np, int nrhs, T* __restrict__ rs, T* __restrict__ beta,
-                          const int* done) {
-  if (*done) return;
-  const int b = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (b >= nrhs) return;
-  T s = 0;
-  for (int g = lane; g < np; g += 64) s += part[(int64_t)b * np + g];
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-  if (lane == 0) {
+__global__ __launch_bounds__(RED_THREADS) void k_cg_beta(const T* __restrict__ part, int np, int nrhs,
+                                                         T* __restrict__ rs, T* __restrict__ beta, const int* done) {
+  if (*done) return;   // block-uniform
+  const int b = blockIdx.x;
+  const T s = block_row_sum(part + (int64_t)b * np, np);
+  if (threadIdx.x == 0) {
     beta[b] = s / rs[b];
     rs[b] = s;
   }
@@ -457,12 +466,12 @@ void rowdot_part(const void* a, const void* c, void* part, int64_t nrhs, int64_t
 }
 template <typename T>
 void reduce_rows(const void* part, int np, int nrhs, void* out, hipStream_t s) {
-  hipLaunchKernelGGL((k_reduce_rows<T>), dim3((unsigned)((nrhs + 3) / 4)), dim3(256), 0, s, (const T*)part, np, nrhs,
+  hipLaunchKernelGGL((k_reduce_rows<T>), dim3((unsigned)nrhs), dim3(RED_THREADS), 0, s, (const T*)part, np, nrhs,
                      (T*)out);
 }
 template <typename T>
 void cg_alpha(const void* part, int np, int nrhs, const void* rs, void* alpha, const int* done, hipStream_t s) {
-  hipLaunchKernelGGL((k_cg_alpha<T>), dim3((unsigned)((nrhs + 3) / 4)), dim3(256), 0, s, (const T*)part, np, nrhs,
+  hipLaunchKernelGGL((k_cg_alpha<T>), dim3((unsigned)nrhs), dim3(RED_THREADS), 0, s, (const T*)part, np, nrhs,
                      (const T*)rs, (T*)alpha, done);
 }
 template <typename T>
@@ -479,7 +488,7 @@ void cg_check(const void* part, int np, int nrhs, double tol, void* rnew, int* d
 }
 template <typename T>
 void cg_beta(const void* part, int np, int nrhs, void* rs, void* beta, const int* done, hipStream_t s) {
-  hipLaunchKernelGGL((k_cg_beta<T>), dim3((unsigned)((nrhs + 3) / 4)), dim3(256), 0, s, (const T*)part, np, nrhs,
+  hipLaunchKernelGGL((k_cg_beta<T>), dim3((unsigned)nrhs), dim3(RED_THREADS), 0, s, (const T*)part, np, nrhs,
                      (T*)rs, (T*)beta, done);
 }
 template <typename T>
