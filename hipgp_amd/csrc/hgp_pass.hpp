@@ -95,6 +95,10 @@ struct PassDesc {
   void* cg_p;
   const void* cg_coef;        // per-RHS alpha (EPI_XR) or beta (EPI_P)
   void* cg_part;              // EPI_XR: per-block partial sums of r.r  [q][row block]
+  // chained forward row pass (EPI_XR / EPI_P): the updated vector's rows (new r / new p) are
+  // transformed again in the same block and written as the next operator's column-major half
+  // spectra over the block's own segment of the intermediate (View{W, -, S0}: same geometry)
+  void* chain_out;
 };
 
 constexpr int LDS_CAP = 160 * 1024;

@@ -52,56 +52,21 @@ template <typename T, int H> struct RowTCfg {
   static constexpr int MINW = MINW_LDS < 1 ? 1 : (MINW_LDS > 4 ? 4 : MINW_LDS);
 };
 
-// Real row pairs -> column-major compact half spectra.
-//   in : View{x, q_stride (elements per RHS), r_stride (row pitch), 1, len = row length}
-//   out: View{W, q_stride (complex per RHS), r_stride = column pitch S0, 1, 0}
-//   Q RHS, Rn pairs per RHS (= ceil(nrows / 2)), grid = Q * ceil(Rn / C).
-template <typename T, int H>
-__global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) void k_row_fwd_t(const PassDesc d) {
+// The forward row transform of a block's row pairs after their real values are in va (Re = row
+// 2l, Im = row 2l+1, positions t + TT k < H, zero padded): twiddled odd half, both halves' FFTs,
+// Hermitian split, and the transposed half spectra out to W[c][row0 + row] (column pitch S0).
+// Needs the twiddle table staged in `tab`; uses the LDS area from `lds` (exchange images, tile).
+template <typename T, int H, int P>
+__device__ __forceinline__ void row_fwd_tail(C2<T> (&va)[P], C2<T> (&vb)[P],
+                                             C2<T>* lds, const C2<T>* tab, const C2<T>* __restrict__ twg, int t,
+                                             int l, int lbase, C2<T>* W, int64_t S0, int row0, int nrow_blk) {
   using Cfg = RowTCfg<T, H>;
-  constexpr int P = Cfg::P, TT = Cfg::TT, C = Cfg::C, PITCH = Cfg::PITCH;
-  if (d.done != nullptr && *d.done) return;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  C2<T>* lds = reinterpret_cast<C2<T>*>(smem_raw);
-  C2<T>* tab = lds + Cfg::AREA;
-  const C2<T>* __restrict__ twg = reinterpret_cast<const C2<T>*>(d.tw);
-  stage_tw<T, H>(tab, twg, threadIdx.x, Cfg::THREADS);
-  const int nrb = (d.Rn + C - 1) / C;
-  const int q = blockIdx.x / nrb;
-  const int rb = blockIdx.x - q * nrb;
-  // a pair's line spans whole waves at every H used here (TT >= 64): l is wave-uniform (scalar
-  // register, scalar row bases), t's known range folds the half-table sign tests
-  const int l = (TT % 64 == 0) ? __builtin_amdgcn_readfirstlane(threadIdx.x / TT) : threadIdx.x / TT;
-  const int t = threadIdx.x & (TT - 1);
-  const int lbase = l * H;
-  const int rp = rb * C + l;                       // this group's pair
-  const bool pvalid = (l < C) && (rp < d.Rn);
-  const int row_a = pvalid ? 2 * rp : 0;
-  const bool has2 = pvalid && (2 * rp + 1 < d.nrows);
-  const T* in_a = reinterpret_cast<const T*>(d.in.ptr) + (int64_t)q * d.in.q_stride + (int64_t)row_a * d.in.r_stride;
-  const T* in_b = has2 ? in_a + d.in.r_stride : in_a;
-  const int in_len = d.in.len;
-
-  C2<T> va[P], vb[P];
-  // raw buffer loads: past the row length (zero padding) and for absent rows they return 0
-  const BufRsrc ra = buf_rsrc(in_a, pvalid ? (uint32_t)in_len * (uint32_t)sizeof(T) : 0u);
-  const BufRsrc rb_ = buf_rsrc(in_b, has2 ? (uint32_t)in_len * (uint32_t)sizeof(T) : 0u);
-#pragma unroll
-  for (int k = 0; k < P; ++k) {
-    const uint32_t lo = (uint32_t)t * (uint32_t)sizeof(T), so = (uint32_t)(TT * k * (int)sizeof(T));
-    va[k] = mk<T>(buf_ld<T>(ra, lo, so), buf_ld<T>(rb_, lo, so));
-  }
-  __syncthreads();   // twiddle table staged
+  constexpr int TT = Cfg::TT, C = Cfg::C, PITCH = Cfg::PITCH;
+  static_assert(P == Cfg::P, "row_fwd_tail: P");
   const C2<T> wt0 = tw_at<T, H>(tab, t);
   #pragma unroll
   for (int k = 0; k < P; ++k) vb[k] = cmul<T>(va[k], tw_pos<T, H, TT>(tab, twg, wt0, t, k));
-
-  C2<T>* W = reinterpret_cast<C2<T>*>(d.out.ptr) + (int64_t)q * d.out.q_stride;
-  const int64_t S0 = d.out.r_stride;
   const BufRsrc rW = buf_rsrc(W, 0x7fffffffu);     // one RHS's slab: < 2 GiB (checked on the host)
-  const int row0 = 2 * rb * C;                     // first row of this block's tile
-  const int nrow_blk = d.nrows - row0 < 2 * C ? d.nrows - row0 : 2 * C;
-
   // both frequency halves' transforms, interleaved over the group's exchange image
   fft_line2<T, H, P, -1, 1, Cfg::WAVE>(va, vb, lds, lbase, t, tab);
   auto do_half = [&](auto half_c, C2<T>(&v)[P]) {
@@ -152,6 +117,52 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
   do_half(std::integral_constant<int, 1>{}, vb);
 }
 
+// Real row pairs -> column-major compact half spectra.
+//   in : View{x, q_stride (elements per RHS), r_stride (row pitch), 1, len = row length}
+//   out: View{W, q_stride (complex per RHS), r_stride = column pitch S0, 1, 0}
+//   Q RHS, Rn pairs per RHS (= ceil(nrows / 2)), grid = Q * ceil(Rn / C).
+template <typename T, int H>
+__global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) void k_row_fwd_t(const PassDesc d) {
+  using Cfg = RowTCfg<T, H>;
+  constexpr int P = Cfg::P, TT = Cfg::TT, C = Cfg::C, PITCH = Cfg::PITCH;
+  if (d.done != nullptr && *d.done) return;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  C2<T>* lds = reinterpret_cast<C2<T>*>(smem_raw);
+  C2<T>* tab = lds + Cfg::AREA;
+  const C2<T>* __restrict__ twg = reinterpret_cast<const C2<T>*>(d.tw);
+  stage_tw<T, H>(tab, twg, threadIdx.x, Cfg::THREADS);
+  const int nrb = (d.Rn + C - 1) / C;
+  const int q = blockIdx.x / nrb;
+  const int rb = blockIdx.x - q * nrb;
+  // a pair's line spans whole waves at every H used here (TT >= 64): l is wave-uniform (scalar
+  // register, scalar row bases), t's known range folds the half-table sign tests
+  const int l = (TT % 64 == 0) ? __builtin_amdgcn_readfirstlane(threadIdx.x / TT) : threadIdx.x / TT;
+  const int t = threadIdx.x & (TT - 1);
+  const int lbase = l * H;
+  const int rp = rb * C + l;                       // this group's pair
+  const bool pvalid = (l < C) && (rp < d.Rn);
+  const int row_a = pvalid ? 2 * rp : 0;
+  const bool has2 = pvalid && (2 * rp + 1 < d.nrows);
+  const T* in_a = reinterpret_cast<const T*>(d.in.ptr) + (int64_t)q * d.in.q_stride + (int64_t)row_a * d.in.r_stride;
+  const T* in_b = has2 ? in_a + d.in.r_stride : in_a;
+  const int in_len = d.in.len;
+
+  C2<T> va[P], vb[P];
+  // raw buffer loads: past the row length (zero padding) and for absent rows they return 0
+  const BufRsrc ra = buf_rsrc(in_a, pvalid ? (uint32_t)in_len * (uint32_t)sizeof(T) : 0u);
+  const BufRsrc rb_ = buf_rsrc(in_b, has2 ? (uint32_t)in_len * (uint32_t)sizeof(T) : 0u);
+#pragma unroll
+  for (int k = 0; k < P; ++k) {
+    const uint32_t lo = (uint32_t)t * (uint32_t)sizeof(T), so = (uint32_t)(TT * k * (int)sizeof(T));
+    va[k] = mk<T>(buf_ld<T>(ra, lo, so), buf_ld<T>(rb_, lo, so));
+  }
+  __syncthreads();   // twiddle table staged
+  C2<T>* W = reinterpret_cast<C2<T>*>(d.out.ptr) + (int64_t)q * d.out.q_stride;
+  const int row0 = 2 * rb * C;                     // first row of this block's tile
+  const int nrow_blk = d.nrows - row0 < 2 * C ? d.nrows - row0 : 2 * C;
+  row_fwd_tail<T, H>(va, vb, lds, tab, twg, t, l, lbase, W, d.out.r_stride, row0, nrow_blk);
+}
+
 // Column-major compact half spectra -> real row pairs (crop), optional fused dot.
 //   in : View{W, q_stride, r_stride = column pitch S0, 1, 0}
 //   out: View{y, q_stride (elements per RHS), r_stride (row pitch), 1, len = out row length}
@@ -160,10 +171,13 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
 // out_len), streamed with the row layout of the (nrhs, M) vectors:
 //   EPI_XR (y = A p):     x += a p;  r -= a y;  returns this thread's share of r.r  (cg.py:67-69)
 //   EPI_P  (y = C^-1 r):  p = y + b p                                                 (cg.py:75)
-// Four elements per thread are loaded before any is stored (the vectors never alias).
+// Four elements per thread are loaded before any is stored (the vectors never alias).  `keep`:
+// the updated value (new r / new p) replaces y in `ys` for the chained forward transform
+// (each element is read and rewritten by the same thread).
 template <typename T, int EPI, int THREADS>
-__device__ __forceinline__ T cg_epilogue(const T* __restrict__ ys, int nrow, int out_len, T* __restrict__ xg,
-                                         T* __restrict__ rg, T* __restrict__ pg, int64_t rpitch, T coef) {
+__device__ __forceinline__ T cg_epilogue(T* __restrict__ ys, int nrow, int out_len, T* __restrict__ xg,
+                                         T* __restrict__ rg, T* __restrict__ pg, int64_t rpitch, T coef,
+                                         bool keep) {
   const int nel = nrow * out_len;
   // the block's rows are one < 2 GiB window of each vector: raw buffers, 32-bit lane offsets
   const BufRsrc rp = buf_rsrc(pg, 0x7fffffffu), rx = buf_rsrc(xg, 0x7fffffffu), rr = buf_rsrc(rg, 0x7fffffffu);
@@ -193,8 +207,11 @@ __device__ __forceinline__ T cg_epilogue(const T* __restrict__ ys, int nrow, int
           const T rn = rv[u] - coef * yv[u];
           buf_st<T>(rn, rr, g[u]);
           s += rn * rn;
+          if (keep) ys[e0 + u * THREADS] = rn;
         } else {
-          buf_st<T>(yv[u] + coef * pv[u], rp, g[u]);
+          const T pn = yv[u] + coef * pv[u];
+          buf_st<T>(pn, rp, g[u]);
+          if (keep) ys[e0 + u * THREADS] = pn;
         }
       }
     }
@@ -202,7 +219,8 @@ __device__ __forceinline__ T cg_epilogue(const T* __restrict__ ys, int nrow, int
   return s;
 }
 
-template <typename T, int H, int EPI = EPI_OUT>
+// CH (EPI_XR / EPI_P only): chained forward transform of the updated vector into d.chain_out.
+template <typename T, int H, int EPI = EPI_OUT, bool CH = false>
 __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) void k_row_inv_t(const PassDesc d) {
   using Cfg = RowTCfg<T, H>;
   constexpr int P = Cfg::P, TT = Cfg::TT, C = Cfg::C, PITCH = Cfg::PITCH;
@@ -327,11 +345,14 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
     T* pg = reinterpret_cast<T*>(d.cg_p) + g0;
     T* xg = EPI == EPI_XR ? reinterpret_cast<T*>(d.cg_x) + g0 : pg;
     T* rg = EPI == EPI_XR ? reinterpret_cast<T*>(d.cg_r) + g0 : pg;
-    T s = cg_epilogue<T, EPI, Cfg::THREADS>(ys, nrow_blk, out_len, xg, rg, pg, d.out.r_stride, coef);
+    constexpr bool chain = CH;
+    T s = cg_epilogue<T, EPI, Cfg::THREADS>(ys, nrow_blk, out_len, xg, rg, pg, d.out.r_stride, coef, chain);
     if constexpr (EPI == EPI_XR) {   // deterministic block sum of r.r -> partial [q][rb]
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-      T* red = reinterpret_cast<T*>(tab);   // twiddles are no longer read
+      // past the staged rows (2C x out_len <= C x H values < the exchange area): the twiddle
+      // table stays intact for the chained transform
+      T* red = ys + 2 * C * out_len;
       if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
       __syncthreads();
       if (threadIdx.x == 0) {
@@ -340,6 +361,22 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
         reinterpret_cast<T*>(d.cg_part)[(int64_t)q * nrb + rb] = tot;
       }
     }
+    if constexpr (!chain) return;
+    // Chained forward row pass of the updated vector (the next operator's first pass): the
+    // block's rows are complete in `ys`, so they are transformed here instead of being read
+    // back from HBM by a k_row_fwd_t launch.  The half spectra go over this block's own row
+    // segment of the intermediate, whose tile was read in full at the top of this kernel.
+    __syncthreads();   // updated rows staged
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+      const int p = t + TT * k;
+      const T a = (pvalid && p < out_len) ? ys[(2 * l) * out_len + p] : (T)0;
+      const T b = (has2 && p < out_len) ? ys[(2 * l + 1) * out_len + p] : (T)0;
+      va[k] = mk<T>(a, b);
+    }
+    __syncthreads();   // rows read before the exchange images overlay them
+    row_fwd_tail<T, H>(va, vb, lds, tab, twg, t, l, lbase, reinterpret_cast<C2<T>*>(d.chain_out) + (int64_t)q * d.in.q_stride,
+                       S0, row0, nrow_blk);
     return;
   }
   T* out_a = reinterpret_cast<T*>(d.out.ptr) + (int64_t)q * d.out.q_stride + (int64_t)(pvalid ? 2 * rp : 0) * d.out.r_stride;
