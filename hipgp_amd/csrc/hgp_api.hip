@@ -99,8 +99,8 @@ struct hgp_plan {
   int nstreams = 2;
   // 2-D PCG chaining: the last run_op left the forward row spectra of the vector the next
   // operator consumes (new r after K, new p after C^-1) in each chunk's ws1 slot
-  // Opt-in (HGP_CHAIN=1): measured slower at C2 (PCG 18.9 -> 20.3 ms) -- the chained kernels
-  // spill at the row kernels' 128-VGPR bound and lose the row/column overlap of the two streams
+  // Opt-in (HGP_CHAIN=1): measured slower at C2 (PCG 18.4 -> 20.2 ms, with one stream or two):
+  // the chained kernels spill at the row kernels' 128-VGPR bound
   bool chain = false;
   bool chain_resident = false;
   hipStream_t side[3] = {nullptr, nullptr, nullptr};
