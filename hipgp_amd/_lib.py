@@ -27,7 +27,7 @@ EXPORTS = (
     "hgp_toeplitz_apply_pass", "hgp_op_pass_count", "hgp_pcg_rnorm2", "hgp_kuf_grid",
     "hgp_kuf_semi_mc", "hgp_kuf_semi_sqexp", "hgp_knn_doubly_diag", "hgp_meanfield_stats",
     "hgp_block_stats", "hgp_sym_toeplitz_dqf", "hgp_plan_column_grad",
-    "hgp_plan_dqf",
+    "hgp_plan_dqf", "hgp_pcg_local_flag", "hgp_pcg_set_done", "hgp_pcg_iters",
 )
 KERN_SQEXP, KERN_MATERN12, KERN_MATERN32, KERN_MATERN52, KERN_GNEITING = 0, 1, 2, 3, 4
 
@@ -75,6 +75,9 @@ def lib():
         "hgp_sym_toeplitz_dqf": (i32, [i32, vp, vp, i64, i64, vp, vp]),
         "hgp_plan_column_grad": (i32, [vp, i32, vp, vp, i64, vp]),
         "hgp_plan_dqf": (i32, [vp, vp, vp, i64, vp]),
+        "hgp_pcg_local_flag": (i32, [vp, dbl, vp]),
+        "hgp_pcg_set_done": (i32, [vp, vp]),
+        "hgp_pcg_iters": (i32, [vp, pi32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -65,6 +65,19 @@ struct DevBuf {
   }
 };
 
+// hgp_rowdot's partial-sum scratch (one per host thread and device, never freed: a few KB-MB)
+struct RowdotScratch {
+  int device = -1;
+  DevBuf buf;
+  hipEvent_t ev = nullptr;
+  hipStream_t last = nullptr;
+  bool used = false;
+  RowdotScratch() = default;
+  RowdotScratch(RowdotScratch&& o) noexcept : device(o.device), ev(o.ev), last(o.last), used(o.used) {
+    buf.ptr = o.buf.ptr; buf.bytes = o.buf.bytes; o.buf.ptr = nullptr; o.buf.bytes = 0; o.ev = nullptr;
+  }
+};
+
 }  // namespace
 
 struct hgp_plan {
@@ -889,6 +902,40 @@ int hgp_pcg_rnorm2(hgp_plan* plan, void* out) {
   return 0;
 }
 
+int hgp_pcg_local_flag(hgp_plan* plan, double tol, int* flag) {
+  HGP_TRY(check_plan(plan));
+  if (!plan->cg_active) return fail(HGP_E_STATE, "hgp_pcg_begin has not been called");
+  if (flag == nullptr) return fail(HGP_E_ARG, "null flag");
+  HGP_TRY(use_device(plan));
+  const void* rnew = reinterpret_cast<const char*>(plan->scal.ptr) + 3 * plan->cg_nrhs * plan->esz;
+  if (plan->dtype == HGP_F64) cg_local_flag<double>(rnew, (int)plan->cg_nrhs, tol, flag, plan->stream);
+  else cg_local_flag<float>(rnew, (int)plan->cg_nrhs, tol, flag, plan->stream);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+int hgp_pcg_iters(hgp_plan* plan, int* iters) {
+  HGP_TRY(check_plan(plan));
+  if (!plan->cg_active) return fail(HGP_E_STATE, "hgp_pcg_begin has not been called");
+  if (iters == nullptr) return fail(HGP_E_ARG, "null iters");
+  HGP_TRY(use_device(plan));
+  int h[2] = {0, 0};
+  HIP_TRY(hipMemcpyAsync(h, plan->flags.ptr, sizeof(h), hipMemcpyDeviceToHost, plan->stream));
+  HIP_TRY(hipStreamSynchronize(plan->stream));
+  *iters = h[1];
+  return 0;
+}
+
+int hgp_pcg_set_done(hgp_plan* plan, const int* flag) {
+  HGP_TRY(check_plan(plan));
+  if (!plan->cg_active) return fail(HGP_E_STATE, "hgp_pcg_begin has not been called");
+  if (flag == nullptr) return fail(HGP_E_ARG, "null flag");
+  HGP_TRY(use_device(plan));
+  cg_set_done(reinterpret_cast<int*>(plan->flags.ptr), flag, plan->stream);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
 int hgp_get_spectrum(hgp_plan* plan, int which, void* out) {
   HGP_TRY(check_plan(plan));
   if (!plan->have_spec) return fail(HGP_E_STATE, "hgp_plan_set_column has not been called");
@@ -908,15 +955,36 @@ int hgp_get_spectrum(hgp_plan* plan, int which, void* out) {
 int hgp_rowdot(int dtype, const void* a, const void* c, void* out, int64_t nrhs, int64_t M, void* hip_stream) {
   if (nrhs <= 0 || M <= 0) return 0;
   if (a == nullptr || c == nullptr || out == nullptr) return fail(HGP_E_ARG, "null pointer");
+  if (dtype != HGP_F32 && dtype != HGP_F64) return fail(HGP_E_ARG, "dtype must be HGP_F32 or HGP_F64");
   hipStream_t s = reinterpret_cast<hipStream_t>(hip_stream);
   const int np = update_np(M);
-  void* part = nullptr;
   const size_t es = dtype == HGP_F64 ? 8 : 4;
-  HIP_TRY(hipMallocAsync(&part, (size_t)(nrhs * np) * es, s));
+  // partial sums in a per-thread, per-device scratch that persists across calls: a call on
+  // another stream first waits for the previous user's event, growth waits for it on the host
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  // (heap-held and never destroyed: no hipFree runs during process teardown)
+  static thread_local std::vector<RowdotScratch>* pool = new std::vector<RowdotScratch>();
+  RowdotScratch* sc = nullptr;
+  for (auto& e : *pool)
+    if (e.device == dev) sc = &e;
+  if (sc == nullptr) {
+    pool->emplace_back();
+    sc = &pool->back();
+    sc->device = dev;
+    HIP_TRY(hipEventCreateWithFlags(&sc->ev, hipEventDisableTiming));
+  }
+  const size_t need = (size_t)(nrhs * np) * es;
+  if (sc->used && need > sc->buf.bytes) HIP_TRY(hipEventSynchronize(sc->ev));
+  HGP_TRY(sc->buf.ensure(need));
+  if (sc->used && sc->last != s) HIP_TRY(hipStreamWaitEvent(s, sc->ev, 0));
+  void* part = sc->buf.ptr;
   if (dtype == HGP_F64) { rowdot_part<double>(a, c, part, nrhs, M, np, s); reduce_rows<double>(part, np, (int)nrhs, out, s); }
   else { rowdot_part<float>(a, c, part, nrhs, M, np, s); reduce_rows<float>(part, np, (int)nrhs, out, s); }
-  HIP_TRY(hipFreeAsync(part, s));
   HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(sc->ev, s));
+  sc->last = s;
+  sc->used = true;
   return 0;
 }
 

@@ -41,6 +41,57 @@ template <typename T> __device__ __forceinline__ C2<T> cmulc(C2<T> a, C2<T> b) {
 }
 template <typename T> __device__ __forceinline__ C2<T> cscale(C2<T> a, T s) { return mk<T>(a.x * s, a.y * s); }
 
+// Packed fp32 complex arithmetic.  A wave64 v_fma_f32 / v_add_f32 occupies the SIMD for 4 cycles
+// on gfx950 and v_pk_fma_f32 / v_pk_add_f32 does both halves of a register pair in about the
+// same time (tools/valu_rate.hip: 69 vs 124 TFLOP/s), and the FFT passes are VALU-bound, so the
+// fp32 (re, im) pair is computed as one 2-vector: a complex add is one v_pk_add_f32, a complex
+// product three packed instructions (the broadcasts fold into op_sel) instead of four.
+#ifndef HGP_PK
+#define HGP_PK 1
+#endif
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2v pv(C2<float> a) { return __builtin_bit_cast(f2v, a); }
+__device__ __forceinline__ C2<float> vp(f2v a) { return __builtin_bit_cast(C2<float>, a); }
+__device__ __forceinline__ f2v pv_lo(f2v a) { return __builtin_shufflevector(a, a, 0, 0); }
+__device__ __forceinline__ f2v pv_hi(f2v a) { return __builtin_shufflevector(a, a, 1, 1); }
+__device__ __forceinline__ f2v pv_swap(f2v a) { return __builtin_shufflevector(a, a, 1, 0); }
+#if HGP_PK
+template <> __device__ __forceinline__ C2<float> cadd<float>(C2<float> a, C2<float> b) { return vp(pv(a) + pv(b)); }
+template <> __device__ __forceinline__ C2<float> csub<float>(C2<float> a, C2<float> b) { return vp(pv(a) - pv(b)); }
+template <> __device__ __forceinline__ C2<float> cmul<float>(C2<float> a, C2<float> b) {
+  const f2v av = pv(a), bv = pv(b);
+  return vp(pv_lo(av) * bv + pv_hi(av) * (pv_swap(bv) * f2v{-1.f, 1.f}));   // (ax bx - ay by, ax by + ay bx)
+}
+template <> __device__ __forceinline__ C2<float> cmulc<float>(C2<float> a, C2<float> b) {
+  const f2v av = pv(a), bv = pv(b);
+  return vp(pv_lo(bv) * av + pv_hi(bv) * (pv_swap(av) * f2v{1.f, -1.f}));   // (ax bx + ay by, ay bx - ax by)
+}
+template <> __device__ __forceinline__ C2<float> cscale<float>(C2<float> a, float s) { return vp(pv(a) * s); }
+#endif
+
+// Two real rows packed as Z = a + i b, transformed: their spectra from Z at k and Zp = Z at -k,
+// A = (Z + conj Zp) / 2, B = (Z - conj Zp) / 2i (exact halvings, same rounding either form).
+template <typename T>
+__device__ __forceinline__ void herm_split(C2<T> z, C2<T> zp, C2<T>& A, C2<T>& B) {
+  if constexpr (HGP_PK && std::is_same<T, float>::value) {
+    const f2v Z = pv(z), P = pv(zp);
+    A = vp(__builtin_elementwise_fma(P, f2v{1.f, -1.f}, Z) * 0.5f);
+    B = vp(pv_swap(__builtin_elementwise_fma(P, f2v{-1.f, 1.f}, Z)) * f2v{0.5f, -0.5f});
+  } else {
+    const T hf = (T)0.5;
+    A = mk<T>(hf * (z.x + zp.x), hf * (z.y - zp.y));
+    B = mk<T>(hf * (z.y + zp.y), -hf * (z.x - zp.x));
+  }
+}
+// the inverse: Z = A + i B
+template <typename T>
+__device__ __forceinline__ C2<T> herm_join(C2<T> A, C2<T> B) {
+  if constexpr (HGP_PK && std::is_same<T, float>::value)
+    return vp(__builtin_elementwise_fma(pv_swap(pv(B)), f2v{-1.f, 1.f}, pv(A)));
+  else
+    return mk<T>(A.x - B.y, A.y + B.x);
+}
+
 // Raw buffer access (gfx9 resource word 3 = 0x00020000, stride 0): a wave-uniform base in
 // scalar registers plus a 32-bit lane byte offset, so no 64-bit address is formed per access;
 // loads at offsets >= `bytes` return 0 and stores there are dropped (used for zero padding,
@@ -96,11 +147,40 @@ template <int H, int P> struct Stages {
 
 // multiply by exp(DIR * 2*pi*i*Q/16), DIR = -1 forward / +1 inverse; Q a compile-time
 // constant after unrolling (the switch folds).
+// packed: v * w for a compile-time constant w = (c, s): lo(v) (c, s) + hi(v) (-s, c), two
+// packed instructions (the broadcasts are op_sel)
+__device__ __forceinline__ C2<float> pk_mulk(C2<float> v, float c, float s) {
+  const f2v a = pv(v);
+  return vp(__builtin_elementwise_fma(pv_hi(a), f2v{-s, c}, pv_lo(a) * f2v{c, s}));
+}
+// packed: v * (+-i) = (-+y, +-x): the swap is op_sel, the signs one constant product
+__device__ __forceinline__ C2<float> pk_muli(C2<float> v, float sg) { return vp(pv_swap(pv(v)) * f2v{-sg, sg}); }
+
 template <typename T, int DIR>
 __device__ __forceinline__ C2<T> rot16(C2<T> v, int Q) {
   const T c8 = (T)0.70710678118654752440, c1 = (T)0.92387953251128675613, s1 = (T)0.38268343236508977173;
   Q &= 15;
   if (DIR > 0) Q = (16 - Q) & 15;           // inverse: exp(+i th) = forward rotation by -Q
+  if constexpr (HGP_PK && std::is_same<T, float>::value) {
+    switch (Q) {                            // forward angle th = 2 pi Q / 16: multiply by (cos th, -sin th)
+      case 0: return v;
+      case 4: return pk_muli(v, -1.f);
+      case 8: return vp(-pv(v));
+      case 12: return pk_muli(v, 1.f);
+      case 2: return pk_mulk(v, c8, -c8);
+      case 6: return pk_mulk(v, -c8, -c8);
+      case 10: return pk_mulk(v, -c8, c8);
+      case 14: return pk_mulk(v, c8, c8);
+      case 1: return pk_mulk(v, c1, -s1);
+      case 3: return pk_mulk(v, s1, -c1);
+      case 5: return pk_mulk(v, -s1, -c1);
+      case 7: return pk_mulk(v, -c1, -s1);
+      case 9: return pk_mulk(v, -c1, s1);
+      case 11: return pk_mulk(v, -s1, c1);
+      case 13: return pk_mulk(v, s1, c1);
+      default: return pk_mulk(v, c1, s1);   // 15
+    }
+  }
   switch (Q) {                              // forward: multiply by (cos th, -sin th), th=2pi Q/16
     case 0: return v;
     case 4: return mk<T>(v.y, -v.x);
@@ -130,6 +210,16 @@ __device__ __forceinline__ void dft(C2<T>* v) {
     C2<T> a = v[0], b = v[1];
     v[0] = cadd<T>(a, b);
     v[1] = csub<T>(a, b);
+  } else if constexpr (R == 4 && HGP_PK && std::is_same<T, float>::value) {
+    // packed: v1 / v3 = d02 +- (-+i) d13 as one fma each (x (+-1, -+1) is exact, so the fma
+    // rounds exactly like the add), the swap of d13 folds into op_sel
+    const f2v s02 = pv(v[0]) + pv(v[2]), d02 = pv(v[0]) - pv(v[2]);
+    const f2v s13 = pv(v[1]) + pv(v[3]), d13 = pv(v[1]) - pv(v[3]);
+    const f2v k = (DIR < 0) ? f2v{1.f, -1.f} : f2v{-1.f, 1.f};   // fwd: (y, -x); inv: (-y, x)
+    v[0] = vp(s02 + s13);
+    v[2] = vp(s02 - s13);
+    v[1] = vp(__builtin_elementwise_fma(pv_swap(d13), k, d02));
+    v[3] = vp(__builtin_elementwise_fma(pv_swap(d13), -k, d02));
   } else if constexpr (R == 4) {
     C2<T> s02 = cadd<T>(v[0], v[2]), d02 = csub<T>(v[0], v[2]);
     C2<T> s13 = cadd<T>(v[1], v[3]), d13 = csub<T>(v[1], v[3]);

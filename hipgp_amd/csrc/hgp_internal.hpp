@@ -89,5 +89,7 @@ template <typename T> void cg_check(const void* part, int np, int nrhs, double t
 template <typename T> void cg_beta(const void* part, int np, int nrhs, void* rs, void* beta, const int* done, hipStream_t s);
 template <typename T> void cg_update_p(void* p, const void* z, const void* beta, int64_t nrhs, int64_t M, const int* done,
                                        hipStream_t s);
+template <typename T> void cg_local_flag(const void* rnew, int nrhs, double tol, int* flag, hipStream_t s);
+void cg_set_done(int* done, const int* flag, hipStream_t s);
 
 }  // namespace hgp

@@ -497,6 +497,32 @@ void cg_update_p(void* p, const void* z, const void* beta, int64_t nrhs, int64_t
   hipLaunchKernelGGL((k_cg_update_p<T>), grid, dim3(UPD_THREADS), 0, s, (T*)p, (const T*)z, (const T*)beta, M, done);
 }
 
+// All-rank break rule without a host round trip (hgp_pcg_local_flag / hgp_pcg_set_done):
+// flag = 1 when every sqrt(r.r) of this rank's RHS is below tol (cg.py:70, NaN = not converged)
+template <typename T>
+__global__ __launch_bounds__(256) void k_cg_local_flag(const T* __restrict__ rnew, int nrhs, double tol, int* flag) {
+  __shared__ int any_not;
+  if (threadIdx.x == 0) any_not = 0;
+  __syncthreads();
+  int mine = 0;
+  for (int b = threadIdx.x; b < nrhs; b += blockDim.x)
+    if (!(sqrt(rnew[b]) < (T)tol)) mine = 1;
+  if (mine) atomicOr(&any_not, 1);
+  __syncthreads();
+  if (threadIdx.x == 0) *flag = any_not ? 0 : 1;
+}
+template <typename T>
+void cg_local_flag(const void* rnew, int nrhs, double tol, int* flag, hipStream_t s) {
+  hipLaunchKernelGGL((k_cg_local_flag<T>), dim3(1), dim3(256), 0, s, (const T*)rnew, nrhs, tol, flag);
+}
+// the plan's done flag := the (all-reduced) flag; later kernels of the solve are no-ops
+__global__ void k_cg_set_done(int* done, const int* flag) {
+  if (threadIdx.x == 0 && *flag != 0) *done = 1;
+}
+void cg_set_done(int* done, const int* flag, hipStream_t s) {
+  hipLaunchKernelGGL(k_cg_set_done, dim3(1), dim3(64), 0, s, done, flag);
+}
+
 #define HGP_INST(T)                                                                                            \
   template void cg_init<T>(const void*, void*, void*, int64_t, hipStream_t);                                 \
   template void vcopy<T>(const void*, void*, int64_t, const int*, hipStream_t);                              \
@@ -508,7 +534,8 @@ void cg_update_p(void* p, const void* z, const void* beta, int64_t nrhs, int64_t
                                 const int*, hipStream_t);                                                    \
   template void cg_check<T>(const void*, int, int, double, void*, int*, int*, hipStream_t);                  \
   template void cg_beta<T>(const void*, int, int, void*, void*, const int*, hipStream_t);                    \
-  template void cg_update_p<T>(void*, const void*, const void*, int64_t, int64_t, const int*, hipStream_t);
+  template void cg_update_p<T>(void*, const void*, const void*, int64_t, int64_t, const int*, hipStream_t); \
+  template void cg_local_flag<T>(const void*, int, double, int*, hipStream_t);
 HGP_INST(float)
 HGP_INST(double)
 #undef HGP_INST

@@ -315,7 +315,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
     C2<T> B = in_c2[c];
     if (!has2) B = mk<T>(0, 0);
     if (cj) { A.y = -A.y; B.y = -B.y; }
-    return mk<T>(A.x - B.y, A.y + B.x);
+    return herm_join<T>(A, B);
   };
   // second half of an input longer than H (only the fp64 setup grids): x[p + H], or 0
   auto load_hi = [&](int p) -> C2<T> {
@@ -396,9 +396,10 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
           const bool store = (half == 0) ? (p <= H / 2) : (p < H / 2);
           if (valid && store) {
             const int c = compact_col<H>(half, p);
-            const T hf = (T)0.5;
-            out_c[c] = mk<T>(hf * (v[k].x + zp.x), hf * (v[k].y - zp.y));               // (Z + conj Zp)/2
-            if (has2) out_c2[c] = mk<T>(hf * (v[k].y + zp.y), -hf * (v[k].x - zp.x));  // (Z - conj Zp)/2i
+            C2<T> A, B;
+            herm_split<T>(v[k], zp, A, B);
+            out_c[c] = A;
+            if (has2) out_c2[c] = B;
           }
         }
       } else if (valid) {

@@ -82,9 +82,7 @@ __device__ __forceinline__ void row_fwd_tail(C2<T> (&va)[P], C2<T> (&vb)[P],
       const int p = t + TT * k;
       const int pp = (half == 0) ? ((H - p) & (H - 1)) : (H - 1 - p);
       const C2<T> zp = lds[lds_phys(lbase + pp)];
-      const T hf = (T)0.5;
-      A[k] = mk<T>(hf * (v[k].x + zp.x), hf * (v[k].y - zp.y));    // (Z + conj Zp)/2
-      B[k] = mk<T>(hf * (v[k].y + zp.y), -hf * (v[k].x - zp.x));   // (Z - conj Zp)/2i
+      herm_split<T>(v[k], zp, A[k], B[k]);
     }
     __syncthreads();   // every group done with its exchange image: the tile overlays them
     // tile[col][row]: col = compact column - first column of the half, row = 2l + {0,1}
@@ -297,7 +295,7 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
       C2<T> B = lds[c * PITCH + 2 * li + 1];
       if (!has2) B = mk<T>(0, 0);
       if (cj) { A.y = -A.y; B.y = -B.y; }
-      v[k] = mk<T>(A.x - B.y, A.y + B.x);
+      v[k] = herm_join<T>(A, B);
     }
   };
   using H0 = std::integral_constant<int, 0>;

@@ -5,11 +5,12 @@ observations split into contiguous shards, one per rank, and each rank runs set-
 for its own rows with NO collective inside the solve.  Two places couple ranks:
 
 * the all-RHS break rule of `cg.py:70` — `ToeplitzPlan.pcg_allranks` applies it exactly with one
-  all-reduce(MIN) of an int flag per iteration (only when `exact_break=True`; with the usual
-  fp32 / tol 1e-8 it never fires and ranks run `maxiter` steps on their own);
+  all-reduce(MIN) of an int flag per iteration, on the device with RCCL (only when
+  `exact_break` is on: the default for fp64; with fp32 / tol 1e-8 it never fires and ranks run
+  `maxiter` steps on their own);
 * the natural-gradient statistics (`hipgp.py:234-266`): sum_n a_n, -sum_n ivar (kn.m - y) kn and
   sum_n ivar kn^2 (mean-field) or the per-block grams sum_n ivar kn_blk kn_blk^T (block family)
-  — one all-reduce(SUM) of a packed buffer per minibatch, after which every rank holds identical
+  — all-reduced (SUM, in place) once per minibatch, after which every rank holds identical
   theta gradients.
 
 Backend: "nccl" (= RCCL over xGMI on ROCm) on GPUs, "gloo" for the CPU tests.
@@ -32,29 +33,45 @@ def rhs_shard(n, world_size, rank):
     return slice(start, start + base + (1 if rank < extra else 0))
 
 
+def _allreduce_(t, group):
+    """In-place SUM all-reduce; gloo reduces CUDA tensors through a host copy."""
+    if dist.get_backend(group) == "gloo" and t.is_cuda:
+        host = t.cpu()
+        dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
+        t.copy_(host)
+    else:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return t
+
+
 def allreduce_stats(stats, group=None):
-    """Sum the mean-field batch statistics of all ranks in ONE all-reduce of a packed buffer."""
+    """Sum the batch statistics of all ranks: lam_sum ((M',) mean-field or (nblk, bs, bs) block
+    grams) and dm_sum (M',) are reduced in place (no packed copy of the M'-sized vectors), the
+    two scalars (sum a_n, n) in one small buffer."""
     ws = dist.get_world_size(group) if dist.is_initialized() else 1
     if ws == 1:
         return stats
-    lam, dm = stats["lam_sum"], stats["dm_sum"]
-    buf = torch.cat([lam.reshape(-1), dm.reshape(-1),
-                     torch.stack([torch.as_tensor(stats["an_sum"], dtype=lam.dtype, device=lam.device),
-                                  torch.as_tensor(float(stats["n"]), dtype=lam.dtype, device=lam.device)])])
-    if dist.get_backend(group) == "gloo" and buf.is_cuda:
-        host = buf.cpu()
-        dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
-        buf = host.to(lam.device)
-    else:
-        dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
-    k, kd = lam.numel(), dm.numel()     # lam_sum: (M',) mean-field or (nblk, bs, bs) block gram
-    return {"lam_sum": buf[:k].reshape(lam.shape), "dm_sum": buf[k:k + kd], "an_sum": buf[k + kd],
-            "n": int(round(float(buf[k + kd + 1])))}
+    lam, dm = stats["lam_sum"].contiguous(), stats["dm_sum"].contiguous()
+    _allreduce_(lam, group)
+    _allreduce_(dm, group)
+    small = torch.stack([torch.as_tensor(stats["an_sum"], dtype=lam.dtype, device=lam.device).reshape(()),
+                         torch.as_tensor(float(stats["n"]), dtype=lam.dtype, device=lam.device)])
+    _allreduce_(small, group)
+    return {"lam_sum": lam, "dm_sum": dm, "an_sum": small[0], "n": int(round(float(small[1])))}
 
 
-def sharded_compute_kn(model, Knm_local, maxiter_cg=20, tol=1e-8, exact_break=False, group=None, Kmm=None):
+def sharded_compute_kn(model, Knm_local, maxiter_cg=10, tol=1e-8, exact_break=None, group=None, Kmm=None):
     """kn = R^T K^{-1} Knm^T for this rank's rows (`hipgp.py:117-146`).  exact_break applies
-    the all-RHS break rule across ranks (see module docstring)."""
+    the all-RHS break rule across ranks (see module docstring); default: on for fp64 (where
+    tol = 1e-8 can be met) and off for fp32 (where it never is at these sizes).  A rank whose
+    shard is empty returns a (0, M') kn and still joins the break rule's all-reduces."""
+    if exact_break is None:
+        exact_break = Knm_local.dtype == torch.float64
+    if Knm_local.shape[0] == 0:
+        if exact_break:
+            from hipgp_amd.plan import pcg_idle_rank
+            pcg_idle_rank(maxiter_cg, Knm_local.device, group)
+        return Knm_local.new_zeros((0, model.Mprime))
     if Kmm is None:
         Kmm = model.toeplitz()
     if exact_break:
@@ -65,14 +82,18 @@ def sharded_compute_kn(model, Knm_local, maxiter_cg=20, tol=1e-8, exact_break=Fa
     return Kmm._matmul_by_RT(d0)
 
 
-def sharded_elbo_and_grad(model, xbatch, ybatch, noise_std_batch=None, maxiter_cg=20, tol=1e-8,
-                          exact_break=False, group=None, compute_kn=None, integrated_obs=False,
+def sharded_elbo_and_grad(model, xbatch, ybatch, noise_std_batch=None, maxiter_cg=10, tol=1e-8,
+                          exact_break=None, group=None, compute_kn=None, integrated_obs=False,
                           semi_integrated_estimator="analytic", semi_integrated_samps=10):
-    """`MeanFieldToeplitzGP.elbo_and_grad` with the minibatch sharded by rows over the ranks
-    of `group`; every rank passes the SAME full minibatch and gets the same ELBO and grads.
-    `compute_kn(model, Knm_local)` may be injected (tests run the host logic on CPU).
+    """`elbo_and_grad` (mean-field or block family) with the minibatch sharded by rows over the
+    ranks of `group`; every rank passes the SAME full minibatch and gets the same ELBO and theta
+    grads.  `compute_kn(model, Knm_local)` may be injected (tests run the host logic on CPU).
     Line-integral observations ("mc-biased") draw the reference's one torch.rand(1) offset per
-    rank: ranks seeded alike draw the same offset, as the single-process reference does."""
+    rank: ranks seeded alike draw the same offset, as the single-process reference does.
+
+    Hyper-parameter learning (learn_kernel / learn_noise): the returned ELBO's value is the
+    global one and its graph holds this rank's share of sum_n a_n / bsz; after backward(),
+    `allreduce_hyper_grads(model)` sums the shares (as the single process would get them)."""
     ws = dist.get_world_size(group) if dist.is_initialized() else 1
     rk = dist.get_rank(group) if dist.is_initialized() else 0
     sl = rhs_shard(xbatch.shape[0], ws, rk)
@@ -85,4 +106,23 @@ def sharded_elbo_and_grad(model, xbatch, ybatch, noise_std_batch=None, maxiter_c
         kn = compute_kn(model, Knm)
     nsd = None if noise_std_batch is None else noise_std_batch[sl]
     stats = allreduce_stats(model.batch_stats(kn, ybatch[sl], Knn_diag, nsd), group=group)
-    return model.apply_stats(stats, xbatch.shape[0])
+    elbo = model.apply_stats(stats, xbatch.shape[0])
+    if model.hyper_grad_needed(nsd):
+        n_local = sl.stop - sl.start
+        if n_local > 0:
+            share = model.autograd_elbo(xbatch[sl], ybatch[sl], nsd, Knm, Knn_diag, kn, nsum=n_local,
+                                        bsz=xbatch.shape[0])
+            elbo = elbo.detach() + (share - share.detach())
+    return elbo
+
+
+def allreduce_hyper_grads(model, group=None):
+    """Sum the kernel / noise hyper-parameter gradients over the ranks after backward() of
+    `sharded_elbo_and_grad`'s ELBO (a rank with no observations contributes zeros)."""
+    if not (dist.is_initialized() and dist.get_world_size(group) > 1):
+        return
+    for p in (model.log_sig2, model.log_ell, model.log_noise2):
+        if not p.requires_grad:
+            continue
+        g = p.grad if p.grad is not None else torch.zeros_like(p)
+        p.grad = _allreduce_(g.detach().clone(), group)

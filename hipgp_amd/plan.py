@@ -136,25 +136,40 @@ class ToeplitzPlan:
         return out
 
     # -- PCG ---------------------------------------------------------------------------------
-    def pcg(self, b, maxiter, tol, precond=True, out=None, return_iters=False):
-        """Batched PCG with the conj_grad2 recurrence (`cg.py:44-80`), row layout (nrhs, M)."""
-        b = self._vec(b, "b", self.M)
+    def _rhs(self, b, layout):
+        """b as the solver takes it: (nrhs, M) rows (conj_grad2) or (M, L) columns (conj_grad)."""
+        if layout == _lib.LAYOUT_ROWS:
+            b = self._vec(b, "b", self.M)
+            return b, b.shape[0]
+        _lib.require_device_tensor(b, "b")
+        if b.dtype != self.dtype or b.device != self.device:
+            raise TypeError(f"b is {b.dtype} on {b.device}, plan is {self.dtype} on {self.device}")
+        if b.dim() != 2 or b.shape[0] != self.M:
+            raise ValueError(f"b must be (M={self.M}, L) in column layout, got {tuple(b.shape)}")
+        return b.contiguous(), b.shape[1]
+
+    def pcg(self, b, maxiter, tol, precond=True, out=None, return_iters=False, layout=_lib.LAYOUT_ROWS):
+        """Batched PCG: conj_grad2's recurrence (`cg.py:44-80`) on rows b (nrhs, M), or, with
+        layout=LAYOUT_COLS, conj_grad's (`cg.py:5-41`) on columns b (M, L) (the library
+        transposes on the device)."""
+        b, nrhs = self._rhs(b, layout)
         x = torch.empty_like(b) if out is None else out
         self._bind_stream()
         iters = ctypes.c_int(0)
         check(lib().hgp_pcg_solve(self._h, ctypes.c_void_p(b.data_ptr()), ctypes.c_void_p(x.data_ptr()),
-                                  b.shape[0], int(maxiter), float(tol), int(bool(precond)),
-                                  _lib.LAYOUT_ROWS, ctypes.byref(iters) if return_iters else None))
+                                  nrhs, int(maxiter), float(tol), int(bool(precond)),
+                                  int(layout), ctypes.byref(iters) if return_iters else None))
         return (x, iters.value) if return_iters else x
 
-    def pcg_steps(self, b, maxiter, tol, precond=True, callback=None):
+    def pcg_steps(self, b, maxiter, tol, precond=True, callback=None, layout=_lib.LAYOUT_ROWS):
         """Stepwise PCG for the callback form (`cg.py:77-78`): callback(n, x) after every
-        iteration that did not meet the break test; returns x (updated in place)."""
-        b = self._vec(b, "b", self.M)
+        iteration that did not meet the break test; returns x (updated in place; in the
+        caller's layout after every step)."""
+        b, nrhs = self._rhs(b, layout)
         x = torch.empty_like(b)
         self._bind_stream()
         check(lib().hgp_pcg_begin(self._h, ctypes.c_void_p(b.data_ptr()), ctypes.c_void_p(x.data_ptr()),
-                                  b.shape[0], int(bool(precond)), _lib.LAYOUT_ROWS))
+                                  nrhs, int(bool(precond)), int(layout)))
         conv = ctypes.c_int(0)
         for n in range(int(maxiter)):
             check(lib().hgp_pcg_step(self._h, float(tol), ctypes.byref(conv)))
@@ -168,17 +183,33 @@ class ToeplitzPlan:
         """PCG on this rank's right-hand sides with the reference's break rule applied over
         ALL ranks' RHS (`cg.py:69-71`): each step runs without a local break, then one
         all-reduce(MIN) of "every sqrt(r.r) < tol here" decides for everybody.  Returns
-        (x, iterations)."""
+        (x, iterations).
+
+        RCCL ("nccl"): the flag never leaves the device -- hgp_pcg_local_flag, an all-reduce on
+        the stream order, hgp_pcg_set_done -- so the host queues `maxiter` steps without a
+        synchronisation and the steps after the break are no-ops on the device.  gloo (CPU
+        tests): the flag goes through the host each iteration.  A rank with no RHS (a short
+        last minibatch) joins the same all-reduces (`pcg_idle_rank`)."""
         import torch.distributed as dist
+        if b.shape[0] == 0:
+            return torch.empty_like(b), pcg_idle_rank(maxiter, self.device, group)
         b = self._vec(b, "b", self.M)
         x = torch.empty_like(b)
         self._bind_stream()
         check(lib().hgp_pcg_begin(self._h, ctypes.c_void_p(b.data_ptr()), ctypes.c_void_p(x.data_ptr()),
                                   b.shape[0], int(bool(precond)), _lib.LAYOUT_ROWS))
+        if dist.get_backend(group) != "gloo":
+            flag = torch.empty(1, dtype=torch.int32, device=self.device)
+            for _ in range(int(maxiter)):
+                check(lib().hgp_pcg_step(self._h, -1.0, None))
+                check(lib().hgp_pcg_local_flag(self._h, float(tol), ctypes.c_void_p(flag.data_ptr())))
+                dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+                check(lib().hgp_pcg_set_done(self._h, ctypes.c_void_p(flag.data_ptr())))
+            it = ctypes.c_int(0)
+            check(lib().hgp_pcg_iters(self._h, ctypes.byref(it)))
+            return x, it.value
         rn = torch.empty(b.shape[0], dtype=self.dtype, device=self.device)
-        # the flag travels on the device for RCCL ("nccl"), on the host for gloo
-        fdev = "cpu" if dist.get_backend(group) == "gloo" else self.device
-        flag = torch.empty(1, dtype=torch.int32, device=fdev)
+        flag = torch.empty(1, dtype=torch.int32)
         it = 0
         for it in range(1, int(maxiter) + 1):
             check(lib().hgp_pcg_step(self._h, -1.0, None))
@@ -201,6 +232,22 @@ class ToeplitzPlan:
                     lib().hgp_plan_destroy(h)
             except Exception:
                 pass
+
+
+def pcg_idle_rank(maxiter, device, group=None):
+    """The all-reduces of `ToeplitzPlan.pcg_allranks` for a rank that owns no right-hand side:
+    it votes "converged" (MIN identity) every iteration and follows the reduced flag, so the
+    other ranks never wait on it.  Returns the iteration count the group stopped at."""
+    import torch.distributed as dist
+    gloo = dist.get_backend(group) == "gloo"
+    flag = torch.ones(1, dtype=torch.int32, device="cpu" if gloo else device)
+    it = 0
+    for it in range(1, int(maxiter) + 1):
+        flag.fill_(1)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+        if gloo and int(flag.item()):
+            break
+    return it
 
 
 def sym_toeplitz_dqf(left_vectors, right_vectors):

@@ -15,8 +15,13 @@ Line-integral observations come from the fused kernels of 
 The block-diagonal family's statistics (per-block grams, kn^T S kn) are the fused kernel
 hgp_block_stats.
 
-Not built here (OUT of the hot path): the full-rank variational family,
-kernel-hyper-parameter learning through the solve (row f4), `batch_solve`'s dense M'xM' system.
+Kernel / noise hyper-parameter learning: with learn_kernel / learn_noise the
+ELBO returned by `elbo_and_grad` carries the autograd graph through Knm, Knn and kn (InvMatmul's
+backward PCG + hgp_plan_dqf, the R^T column gradient hgp_plan_column_grad), as the reference's
+fit loop needs it (`svi_gp.py:317-326`).
+
+Not built here (OUT of the hot path): the full-rank variational family and
+`batch_solve`'s dense M'xM' system.
 """
 import numpy as np
 import torch
@@ -244,7 +249,37 @@ class ToeplitzInducingGP(SviGP):
                                          semi_integrated_samps=semi_integrated_samps)
         kn = self.compute_kn(Knm, maxiter_cg=maxiter_cg, Kmm=Kmm)
         stats = self.batch_stats(kn, ybatch, Knn_diag, noise_std_batch)
-        return self.apply_stats(stats, xbatch.shape[0])
+        elbo = self.apply_stats(stats, xbatch.shape[0])
+        if self.hyper_grad_needed(noise_std_batch):
+            # learn_kernel / learn_noise: the fit loop back-propagates the returned ELBO
+            # (`svi_gp.py:317-326`), so it carries the graph to log_sig2 / log_ell / log_noise2
+            # through Knm, Knn and kn (InvMatmul.backward + the R^T column gradient) as in
+            # `hipgp.py:214-227`, with the variational parameters held fixed (`:216-217`)
+            elbo = self.autograd_elbo(xbatch, ybatch, noise_std_batch, Knm, Knn_diag, kn)
+        return elbo
+
+    def hyper_grad_needed(self, noise_std_batch=None):
+        """True when the ELBO must carry an autograd graph to the kernel / noise parameters."""
+        if not torch.is_grad_enabled():
+            return False
+        kern = self.learn_kernel and (self.log_sig2.requires_grad or self.log_ell.requires_grad)
+        noise = noise_std_batch is None and self.log_noise2.requires_grad
+        return bool(kern or noise)
+
+    def autograd_elbo(self, xbatch, ybatch, noise_std_batch, Knm, Knn_diag, kn, nsum=None, bsz=None):
+        """mean_n a_n - KL/N with autograd through Knm, Knn_diag, kn and the noise terms
+        (`hipgp.py:214-227`); qm, qS fixed.  With nsum/bsz (a shard of a minibatch of bsz rows)
+        the shard's share sum_n a_n / bsz is returned instead (no KL term)."""
+        with torch.no_grad():
+            qm, qS = self.standard_variational_params()
+            qm, qS = qm.detach(), qS.detach()
+        an = self.compute_batch_an(xbatch, ybatch, noise_std_batch, qm=qm, qS=qS, Knm=Knm,
+                                   Knn_diag=Knn_diag, kn=kn)
+        if bsz is not None:
+            # a_n may be the reference's (n, n) broadcast (per-observation noise): its mean
+            # equals the mean of the per-row values, so mean * n is the shard's sum
+            return torch.mean(an) * nsum / bsz
+        return torch.mean(an) - self.get_kl_to_prior(qm, qS) / self.N
 
     def predict(self, x, integrated_obs=False, semi_integrated_estimator="analytic",
                 semi_integrated_samps=10, maxiter_cg=50, Kmm=None):
@@ -313,6 +348,9 @@ class MeanFieldToeplitzGP(ToeplitzInducingGP):
            an_sum  = sum_n a_n
            lam_sum = sum_n ivar_n kn_n^2            (M',)   `hipgp.py:241`
            dm_sum  = -sum_n ivar_n (kn_n.m - y_n) kn_n   (M',)   `hipgp.py:234-236`"""
+        if kn.shape[0] == 0:    # an empty shard of a minibatch (hipgp_amd.dist)
+            z = kn.new_zeros(kn.shape[1])
+            return {"an_sum": kn.new_zeros(()), "lam_sum": z, "dm_sum": z.clone(), "n": 0}
         with torch.no_grad():
             qm, qS = self.standard_variational_params()
             ivar, log_sd = self.noise_terms(noise_std_batch)
@@ -517,6 +555,9 @@ class BlockToeplitzGP(ToeplitzInducingGP):
            an_sum  = sum_n a_n                                         `hipgp.py:370-414`
            lam_sum = sum_n ivar_n kn_blk kn_blk^T   (num_blocks, bs, bs)  `hipgp.py:252-256`
            dm_sum  = -sum_n ivar_n (kn_n.m - y_n) kn_n   (M',)          `hipgp.py:234-236`"""
+        if kn.shape[0] == 0:    # an empty shard of a minibatch (hipgp_amd.dist)
+            G = kn.new_zeros((self.num_blocks, self.block_size, self.block_size))
+            return {"an_sum": kn.new_zeros(()), "lam_sum": G, "dm_sum": kn.new_zeros(kn.shape[1]), "n": 0}
         with torch.no_grad():
             qm, qS = self.standard_variational_params()
             qm, qS = qm.detach(), qS.detach()

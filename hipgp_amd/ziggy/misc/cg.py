@@ -11,6 +11,29 @@ import torch
 from hipgp_amd.plan import rowdot
 
 
+class ColumnOp:
+    """x (M, L) -> op(x^T)^T for a libhipgp plan: the column-layout operator lambdas that
+    `gram_solve` hands `conj_grad` (`toeplitz_expanded.py:46-49`), as an object `conj_grad`
+    recognises, so that the whole column-layout solve runs as hgp_pcg_solve(LAYOUT_COLS)."""
+
+    def __init__(self, plan, op):
+        self.plan, self.op = plan, op
+
+    def __call__(self, x):
+        return self.plan.apply(self.op, x.t().contiguous()).t()
+
+
+def _cols_fastpath(A_mul, precond):
+    from hipgp_amd import _lib
+    if not isinstance(A_mul, ColumnOp) or A_mul.op != _lib.OP_K:
+        return None
+    if precond is None:
+        return A_mul.plan, False
+    if isinstance(precond, ColumnOp) and precond.plan is A_mul.plan and precond.op == _lib.OP_CINV:
+        return A_mul.plan, True
+    return None
+
+
 def _toeplitz_fastpath(A_mul, precond):
     owner = getattr(A_mul, "__self__", None)
     fn = getattr(A_mul, "__func__", None)
@@ -61,7 +84,16 @@ def conj_grad2(A_mul, b, precond=None, maxiter=20, tol=1e-10, callback=None):
 
 
 def conj_grad(A_mul, b, precond=None, maxiter=20, tol=1e-10, callback=None):
-    """Column layout: b (M, L), dim=0 dots (`cg.py:5-41`); same recurrence per column."""
+    """Column layout: b (M, L), dim=0 dots (`cg.py:5-41`); same recurrence per column.
+    ColumnOp operators of one plan (K, and C^-1 as the preconditioner) run as one fused
+    hgp_pcg_solve in LAYOUT_COLS; any other callables run the generic recurrence."""
+    from hipgp_amd import _lib
+    fp = _cols_fastpath(A_mul, precond)
+    if fp is not None:
+        plan, use_p = fp
+        if callback is None:
+            return plan.pcg(b, maxiter, tol, precond=use_p, layout=_lib.LAYOUT_COLS)
+        return plan.pcg_steps(b, maxiter, tol, precond=use_p, callback=callback, layout=_lib.LAYOUT_COLS)
     At = lambda y: A_mul(y.t()).t()
     Pt = None if precond is None else (lambda y: precond(y.t()).t())
     cb = None if callback is None else (lambda n, x: callback(n, x.t()))

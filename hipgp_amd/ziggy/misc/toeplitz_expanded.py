@@ -2,9 +2,9 @@
 
 ToeplitzMatmul is the older twin of ToeplitzTensor: NO nugget on the column
 (`toeplitz_expanded.py:242-250`), multiply types "gram" | "RTv" | "Rv" | "circ_inv"
-(`:139-189`).  gram_solve runs conj_grad's column-layout recurrence (`cg.py:5-41`) — per
-column it is the same arithmetic as the row layout, so the solve runs in row layout on the
-(bsz, M) input and the callback sees the (M, bsz) view the reference passes.
+(`:139-189`).  gram_solve runs conj_grad's column-layout recurrence (`cg.py:5-41`) on vec^T (M, bsz) as the
+reference does; its K / C^-1 operators are ColumnOp objects, so conj_grad runs the whole solve as
+hgp_pcg_solve(LAYOUT_COLS) and the callback sees the (M, bsz) iterate.
 """
 import numpy as np
 import torch
@@ -12,6 +12,7 @@ from torch import nn
 
 from hipgp_amd import _lib
 from hipgp_amd.plan import ToeplitzPlan
+from hipgp_amd.ziggy.misc.cg import ColumnOp, conj_grad
 
 _OPS = {"gram": _lib.OP_K, "RTv": _lib.OP_RT, "Rv": _lib.OP_R, "circ_inv": _lib.OP_CINV}
 
@@ -24,15 +25,13 @@ def gram_solve(xgrids, kernel_fun, vec, K_matmul=None, maxiter=20, do_precond=Tr
         K_matmul = ToeplitzMatmul(xgrids, kernel_fun, batch_shape=vec.shape[:-1])
     else:
         K_matmul.set_batch_shape(vec.shape[:-1])
-    plan = K_matmul._plan
-    if callback is None:
-        d = plan.pcg(vec, maxiter, tol, precond=do_precond)
-    else:
-        d = plan.pcg_steps(vec, maxiter, tol, precond=do_precond,
-                           callback=lambda n, x: callback(n, x.t()))
+    Kmul = ColumnOp(K_matmul._plan, _lib.OP_K)
+    precond = ColumnOp(K_matmul._plan, _lib.OP_CINV) if do_precond else None
+    # column layout as the reference (`:46-53`): one fused hgp_pcg_solve(LAYOUT_COLS)
+    d = conj_grad(Kmul, vec.t(), precond=precond, maxiter=maxiter, tol=tol, callback=callback)  # (M, bsz)
     if mult_RT:
-        return K_matmul(d, multiply_type="RTv")
-    return d
+        return K_matmul(d.t(), multiply_type="RTv")
+    return d.t()
 
 
 class ToeplitzMatmul(nn.Module):

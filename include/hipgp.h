@@ -100,6 +100,17 @@ int hgp_pcg_step(hgp_plan* plan, double tol, int* converged);
  * step that met the test (the break precedes only the z/p update). */
 int hgp_pcg_rnorm2(hgp_plan* plan, void* out);
 
+/* Device-side form of the same all-rank break rule (no host round trip per iteration):
+ * hgp_pcg_local_flag writes *flag (device int) = 1 when every sqrt(r.r) of the plan's RHS is
+ * below tol after the last step(tol = -1); the caller all-reduces it (MIN, e.g. RCCL on the
+ * same stream order) and hgp_pcg_set_done(flag) raises the plan's done flag when the reduced
+ * value is 1, so every later step of the solve is a no-op on the device. */
+int hgp_pcg_local_flag(hgp_plan* plan, double tol, int* flag);
+int hgp_pcg_set_done(hgp_plan* plan, const int* flag);
+/* Iterations the current solve has executed whose break test did not stop it, plus the one
+ * that did (host int; synchronises the plan's stream). */
+int hgp_pcg_iters(hgp_plan* plan, int* iters);
+
 /* The clamped spectrum D (which=HGP_SPEC_D), sqrt(D) or 1/D on the full expanded grid
  * (device, M' reals) — the real parts of ToeplitzTensor.D / D_sqrt / Di
  * (toeplitz_tensor.py:28-31). */

@@ -1,0 +1,101 @@
+"""The BASELINE configs C3 (2048^2) and C4 (4096^2) on the GPU: PCG (`_solve`, `compute_kn`)
+and the mean-field ELBO / natural gradient at full grid size in fp32, against the fp64 plan
+of the same problem, plus residual checks.  At these sizes the rows are longer than one wave's
+line (16-pair row blocks, the fused PCG epilogues k_row_inv_t<float, 2048 | 4096, EPI_XR | EPI_P>
+with the alpha / beta mid-pass), the 4096^2 fp32 twiddles are two-level LDS tables, and the RHS
+run in several workspace chunks over the two streams (the 1 GiB budget: 4 RHS per chunk at
+4096^2 fp32, 2 in fp64).  Nugget 0.1 keeps the problems well conditioned, so fp32 and fp64
+agree to ~1e-4 (a difference of the implementations, not of the chaos of a clamped solve)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _tt(m, dtype, jitter=0.1):
+    import ziggy.kernels as zk
+    from ziggy.misc.toeplitz_tensor import ToeplitzTensor
+    k = zk.Matern(nu=1.5, dtype=dtype)
+    grids = [torch.linspace(-1, 1, m, device=DEV, dtype=dtype) for _ in range(2)]
+    return ToeplitzTensor(grids, lambda x, y: k.forward(x, y, params=(1., .1)), jitter_val=jitter)
+
+
+@pytest.mark.parametrize("m,B", [(2048, 16), (4096, 10)], ids=["C3_2048x2048_B16", "C4_4096x4096_B10"])
+def test_pcg_compute_kn_fp32_vs_fp64(m, B):
+    g = torch.Generator(device=DEV).manual_seed(21)
+    b64 = torch.randn(B, m * m, device=DEV, generator=g, dtype=torch.float64)
+    out = {}
+    for dt in (torch.float64, torch.float32):
+        T = _tt(m, dt)
+        b = b64.to(dt)
+        x = T._solve(b, do_precond=True, maxiter=20, tol=1e-8)
+        res = (T._matmul_by_K(x).double() - b64).norm(dim=1) / b64.norm(dim=1)
+        kn = None
+        if m == 2048 or dt == torch.float32:      # fp64 R^T rows of H = 8192 exceed one CU's LDS
+            kn = T._matmul_by_RT(T.inv_matmul(b, do_precond=True, maxiter=20, tol=1e-8))
+            assert kn.shape == (B, (2 * m - 2) ** 2)
+            # the whitening identity R (R^T d) = K d on the same solve
+            d = T.inv_matmul(b[:2], do_precond=True, maxiter=20, tol=1e-8)
+            Kd = T._matmul_by_K(d)
+            rr = T._matmul_by_R(T._matmul_by_RT(d))
+            assert float((rr - Kd).abs().max() / Kd.abs().max()) < (1e-10 if dt == torch.float64 else 1e-4)
+        out[dt] = (x.double(), float(res.max()), kn)
+        del T
+        torch.cuda.empty_cache()
+    x64, r64, kn64 = out[torch.float64]
+    x32, r32, kn32 = out[torch.float32]
+    assert r64 < 0.05, r64                      # 20 preconditioned iterations have converged well
+    assert abs(r32 - r64) < 1e-3, (r32, r64)
+    rel = float(((x32 - x64).norm(dim=1) / x64.norm(dim=1)).max())
+    assert rel < 1e-3, rel
+    if kn64 is not None:
+        rel_kn = float(((kn32.double() - kn64).norm(dim=1) / kn64.norm(dim=1)).max())
+        assert rel_kn < 1e-3, rel_kn
+
+
+def test_pcg_break_rule_C3():
+    """The all-RHS break rule at 2048^2 (fp64, a tolerance met after a few iterations): the
+    fused 2-D iteration stops at the same iteration as a stepwise run with a callback."""
+    T = _tt(2048, torch.float64)
+    g = torch.Generator(device=DEV).manual_seed(22)
+    b = torch.randn(3, 2048 * 2048, device=DEV, generator=g, dtype=torch.float64)
+    tol = 1e-4 * float(b.norm(dim=1).min())
+    x, iters = T._plan.pcg(b, 50, tol, precond=True, return_iters=True)
+    calls = []
+    x2 = T._plan.pcg_steps(b, 50, tol, precond=True, callback=lambda n, xx: calls.append(n))
+    assert 1 < iters < 50 and len(calls) == iters - 1
+    assert torch.equal(x, x2)
+    r = (T._matmul_by_K(x) - b).norm(dim=1)
+    assert float(r.max()) < tol * 1.01
+
+
+def test_meanfield_elbo_C3():
+    """Mean-field `elbo_and_grad` at the C3 grid (2048^2, M' = 4094^2) with 16 observations:
+    the fp32 model's ELBO and natural gradient against the fp64 model's."""
+    import ziggy.hipgp as hg
+    import ziggy.kernels as zk
+    res = {}
+    rs = np.random.RandomState(5)
+    x = rs.rand(16, 2) * 1.8 - .9
+    y = rs.randn(16, 1)
+    for dt in (torch.float64, torch.float32):
+        k = zk.Matern(nu=1.5, dtype=dt)
+        grids = [torch.linspace(-1, 1, 2048, dtype=dt) for _ in range(2)]
+        mod = hg.MeanFieldToeplitzGP(k, grids, num_obs=100000, sig2_init=1., ell_init=.1, noise2_init=.05,
+                                     dtype=dt, jitter_val=0.1)
+        torch.manual_seed(3)
+        with torch.no_grad():
+            mod.global_theta1.copy_(torch.randn(mod.Mprime, 1, dtype=torch.float64).to(dt) * .01)
+        mod = mod.cuda_params(0)
+        elbo = mod.elbo_and_grad(torch.tensor(x, dtype=dt, device=DEV), torch.tensor(y, dtype=dt, device=DEV),
+                                 maxiter_cg=20)
+        res[dt] = (float(elbo), mod.global_theta1.grad.double(), mod.global_theta2.grad.double())
+        del mod
+        torch.cuda.empty_cache()
+    e64, g1_64, g2_64 = res[torch.float64]
+    e32, g1_32, g2_32 = res[torch.float32]
+    assert abs(e32 - e64) < 1e-4 * abs(e64), (e32, e64)
+    for a, b in ((g1_32, g1_64), (g2_32, g2_64)):
+        assert float((a - b).norm() / b.norm()) < 1e-4

@@ -68,7 +68,7 @@ def test_rhs_shard_partition():
             assert idx == list(range(n))
 
 
-def _dist_worker(rank, world_size, port, out):
+def _dist_worker(rank, world_size, port, out, nobs=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch.distributed as dist
@@ -79,10 +79,13 @@ def _dist_worker(rank, world_size, port, out):
         mod = _model(fx)
         kn_full = torch.tensor(fx["kn"])
         x = torch.tensor(fx["xobs"])
+        y = torch.tensor(fx["yobs"])
+        if nobs is not None:     # a short minibatch: fewer rows than ranks, some shards empty
+            kn_full, x, y = kn_full[:nobs], x[:nobs], y[:nobs]
         # inject kn for this rank's rows (the device solve is exercised by the GPU tests)
         sl = hdist.rhs_shard(x.shape[0], world_size, rank)
         fake_kn = lambda model, Knm_local: kn_full[sl]
-        elbo = hdist.sharded_elbo_and_grad(mod, x, torch.tensor(fx["yobs"]), compute_kn=fake_kn)
+        elbo = hdist.sharded_elbo_and_grad(mod, x, y, compute_kn=fake_kn)
         out[rank] = (float(elbo), mod.global_theta1.grad.numpy().copy(), mod.global_theta2.grad.numpy().copy())
     finally:
         dist.destroy_process_group()
@@ -106,3 +109,41 @@ def test_sharded_natgrad_gloo(world_size):
     # every rank holds bit-identical gradients
     for r in range(1, world_size):
         assert np.array_equal(out[0][1], out[r][1]) and np.array_equal(out[0][2], out[r][2])
+
+
+def _dist_worker_short(rank, world_size, port, out):
+    _dist_worker(rank, world_size, port, out, nobs=2)
+
+
+def test_sharded_natgrad_empty_shard_gloo():
+    """3 ranks, a minibatch of 2 observations: one rank's shard is empty; it contributes zero
+    statistics and joins the all-reduces (no hang), and every rank gets the single-process
+    ELBO / natural gradient of those 2 observations."""
+    fx = load("G5", "f64")
+    mod = _model(fx)
+    kn = torch.tensor(fx["kn"])[:2]
+    stats = mod.batch_stats(kn, torch.tensor(fx["yobs"])[:2], torch.tensor(fx["Knn_diag"])[:2])
+    elbo_ref = float(mod.apply_stats(stats, 2))
+    g1_ref = mod.global_theta1.grad.numpy().copy()
+    empty = mod.batch_stats(kn[:0], torch.tensor(fx["yobs"])[:0], torch.tensor(fx["Knn_diag"])[:0])
+    assert empty["n"] == 0 and float(empty["lam_sum"].abs().sum()) == 0.0
+    mgr = mp.Manager()
+    out = mgr.dict()
+    port = 29500 + os.getpid() % 1000 + 7
+    mp.spawn(_dist_worker_short, args=(3, port, out), nprocs=3, join=True)
+    assert len(out) == 3
+    for r in range(3):
+        elbo, g1, _ = out[r]
+        assert abs(elbo - elbo_ref) < 1e-12 * abs(elbo_ref)
+        assert rel_err(g1, g1_ref) < 1e-12
+
+
+def test_hyper_grad_needed_flags():
+    fx = load("G5", "f64")
+    mod = _model(fx)                       # learn_kernel=False, learn_noise default False
+    assert not mod.hyper_grad_needed()
+    mod.log_noise2.requires_grad_(True)
+    assert mod.hyper_grad_needed()         # noise2 drives ivar when no per-observation noise
+    assert not mod.hyper_grad_needed(torch.ones(3, 1, dtype=torch.float64))
+    with torch.no_grad():
+        assert not mod.hyper_grad_needed()
