@@ -107,15 +107,10 @@ struct hgp_plan {
   void* cg_x = nullptr;
   bool cg_active = false;
   int64_t ws_budget = (int64_t)1 << 30;
+  bool ws_explicit = false;               // HGP_WS_MB given: the byte budget alone sets the chunks
   // 2-D operators run their RHS chunks on `nstreams` streams (the plan's own + side streams),
   // so one chunk's compute-heavy column pass overlaps another's memory-heavy row passes
   int nstreams = 2;
-  // 2-D PCG chaining: the last run_op left the forward row spectra of the vector the next
-  // operator consumes (new r after K, new p after C^-1) in each chunk's ws1 slot
-  // Opt-in (HGP_CHAIN=1): measured slower at C2 (PCG 18.4 -> 20.2 ms, with one stream or two):
-  // the chained kernels spill at the row kernels' 128-VGPR bound
-  bool chain = false;
-  bool chain_resident = false;
   hipStream_t side[3] = {nullptr, nullptr, nullptr};
   hipEvent_t ev_fork = nullptr, ev_join[3] = {nullptr, nullptr, nullptr};
 
@@ -228,9 +223,7 @@ using MidFn = std::function<void(int64_t, int, hipStream_t)>;
 template <typename T>
 int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void* dotv, void* partial,
            const int* done, int only_pass = -1, void* spart = nullptr, const RowEpi* epi = nullptr,
-           const MidFn* mid = nullptr, bool use_resident = false, bool want_chain = false) {
-  const bool resident = P->chain_resident;
-  P->chain_resident = false;   // any operator call overwrites the slots
+           const MidFn* mid = nullptr) {
   const OpGeom g = op_geom(P, op);
   const int d = P->d;
   const int conv_mode = g.spec_kind == SPEC_REAL ? PASS_CONV : PASS_CONVC;
@@ -256,13 +249,15 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
   if (B1 + B2 > 0) {
     const int64_t per = (B1 + B2) * (int64_t)cs;
     Qc = std::max<int64_t>(1, std::min<int64_t>((nrhs + NS - 1) / NS, P->ws_budget / (per * NS)));
+    // Infinity-Cache-resident chunks: where 8 RHS of a 2-D intermediate fit in ~72 MiB, each
+    // stream works on 8 RHS at a time, so the intermediate a column pass writes is still in the
+    // 256 MiB Infinity Cache when the row-inverse pass reads it (C2: row inverse 4.2 -> 5.0 TB/s,
+    // K matvec +4-6 %, tools/gpu_env_ab.sh).  Larger grids keep the byte budget (fewer RHS per
+    // chunk there cost more in launch tails than the cache gains: C3 / C4 measured slower).
+    if (d == 2 && !P->ws_explicit && per * 8 <= ((int64_t)72 << 20)) Qc = std::min<int64_t>(Qc, 8);
     HGP_TRY(P->ws1.ensure((size_t)(B1 * Qc * NS) * cs));
     if (B2) HGP_TRY(P->ws2.ensure((size_t)(B2 * Qc) * cs));
   }
-  // chaining needs every chunk in a slot of its own (the slot's spectra outlive the call)
-  const bool can_chain = d == 2 && only_pass < 0 && P->chain && (nrhs + Qc - 1) / Qc <= NS;
-  const bool skip_fwd = use_resident && resident && can_chain;
-  const bool do_chain = want_chain && can_chain && epi != nullptr;
   hipStream_t streams[4] = {P->stream, nullptr, nullptr, nullptr};
   if (NS > 1) {
     HGP_TRY(ensure_side_streams(P, NS));
@@ -321,8 +316,7 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
       A.in = View{(void*)xi, g.in_M, g.in[1], 1, (int)g.in[1]};
       A.out = View{w1, B1, S0, 1, 0};
       A.tw = g.tw[1].ptr; A.Q = qn; A.Rn = (int)((g.in[0] + 1) / 2); A.nrows = (int)g.in[0]; A.done = done;
-      if (skip_fwd) ++pass_no;   // w1 already holds x's row spectra (chained by the previous op)
-      else HGP_TRY(run_rowt(0, A, EPI_OUT));
+      HGP_TRY(run_rowt(0, A, EPI_OUT));
       // B: CONV along axis 0 = contiguous lines (q, c1), in place; spectrum [c1][k0]
       PassDesc Bd = base_desc();
       Bd.in = View{w1, B1, S0, 1, (int)g.in[0]};
@@ -350,7 +344,6 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
         Cd.cg_p = reinterpret_cast<T*>(epi->p) + q0 * g.out_M;
         Cd.cg_coef = reinterpret_cast<const T*>(epi->coef) + q0;
         Cd.cg_part = epi->part ? reinterpret_cast<T*>(epi->part) + q0 * nrb : nullptr;
-        if (do_chain) Cd.chain_out = w1;
       }
       HGP_TRY(run_rowt(1, Cd, epi_mode));
     } else {
@@ -396,7 +389,6 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
     HIP_TRY(hipEventRecord(P->ev_join[i - 1], streams[i]));
     HIP_TRY(hipStreamWaitEvent(P->stream, P->ev_join[i - 1], 0));
   }
-  P->chain_resident = do_chain;
   return 0;
 }
 
@@ -677,19 +669,14 @@ int pcg_step_t(hgp_plan* P, double tol) {
       cg_alpha<T>(part_s + q0 * nps, nps, qn, rs + q0, alpha + q0, done, cs);
     };
     const RowEpi exr{EPI_XR, P->r.ptr, P->cg_x, P->p.ptr, alpha, P->part_u.ptr};
-    // with a preconditioner, the K op's row-inverse also transforms the new r for C^-1 and the
-    // C^-1 op's transforms the new p for the next K (run_op: "chaining")
-    const bool chain = P->cg_precond != 0;
-    HGP_TRY(run_op<T>(P, HGP_OP_K, P->p.ptr, P->Ap.ptr, nrhs, nullptr, nullptr, done, -1, part_s, &exr, &mid_alpha,
-                      chain, chain));
+    HGP_TRY(run_op<T>(P, HGP_OP_K, P->p.ptr, P->Ap.ptr, nrhs, nullptr, nullptr, done, -1, part_s, &exr, &mid_alpha));
     cg_check<T>(P->part_u.ptr, npx, (int)nrhs, tol, rnew, done, iters, s);
     if (P->cg_precond) {
       const MidFn mid_beta = [&](int64_t q0, int qn, hipStream_t cs) {
         cg_beta<T>(part_s + q0 * nps, nps, qn, rs + q0, beta + q0, done, cs);
       };
       const RowEpi ep{EPI_P, P->r.ptr, P->cg_x, P->p.ptr, beta, nullptr};
-      HGP_TRY(run_op<T>(P, HGP_OP_CINV, P->r.ptr, P->Ap.ptr, nrhs, nullptr, nullptr, done, -1, part_s, &ep, &mid_beta,
-                        true, true));
+      HGP_TRY(run_op<T>(P, HGP_OP_CINV, P->r.ptr, P->Ap.ptr, nrhs, nullptr, nullptr, done, -1, part_s, &ep, &mid_beta));
     } else {
       cg_beta<T>(P->part_u.ptr, npx, (int)nrhs, rs, beta, done, s);
       cg_update_p<T>(P->p.ptr, P->r.ptr, beta, nrhs, M, done, s);
@@ -775,11 +762,9 @@ int hgp_plan_create(int device, int ndim, const int64_t* m, int dtype, int64_t m
     P->prodLR *= P->LR[a];
   }
   const char* wb = std::getenv("HGP_WS_MB");
-  if (wb) P->ws_budget = (int64_t)std::atoll(wb) << 20;
+  if (wb) { P->ws_budget = (int64_t)std::atoll(wb) << 20; P->ws_explicit = true; }
   const char* ns = std::getenv("HGP_STREAMS");
   if (ns) P->nstreams = std::max(1, std::min(4, std::atoi(ns)));
-  const char* ch = std::getenv("HGP_CHAIN");
-  if (ch) P->chain = std::atoi(ch) != 0;
   int rc = 0;
   for (int a = 0; a < d && rc == 0; ++a) {
     if (dtype == HGP_F64) {

@@ -41,55 +41,19 @@ template <typename T> __device__ __forceinline__ C2<T> cmulc(C2<T> a, C2<T> b) {
 }
 template <typename T> __device__ __forceinline__ C2<T> cscale(C2<T> a, T s) { return mk<T>(a.x * s, a.y * s); }
 
-// Packed fp32 complex arithmetic.  A wave64 v_fma_f32 / v_add_f32 occupies the SIMD for 4 cycles
-// on gfx950 and v_pk_fma_f32 / v_pk_add_f32 does both halves of a register pair in about the
-// same time (tools/valu_rate.hip: 69 vs 124 TFLOP/s), and the FFT passes are VALU-bound, so the
-// fp32 (re, im) pair is computed as one 2-vector: a complex add is one v_pk_add_f32, a complex
-// product three packed instructions (the broadcasts fold into op_sel) instead of four.
-#ifndef HGP_PK
-#define HGP_PK 1
-#endif
-typedef float f2v __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ f2v pv(C2<float> a) { return __builtin_bit_cast(f2v, a); }
-__device__ __forceinline__ C2<float> vp(f2v a) { return __builtin_bit_cast(C2<float>, a); }
-__device__ __forceinline__ f2v pv_lo(f2v a) { return __builtin_shufflevector(a, a, 0, 0); }
-__device__ __forceinline__ f2v pv_hi(f2v a) { return __builtin_shufflevector(a, a, 1, 1); }
-__device__ __forceinline__ f2v pv_swap(f2v a) { return __builtin_shufflevector(a, a, 1, 0); }
-#if HGP_PK
-template <> __device__ __forceinline__ C2<float> cadd<float>(C2<float> a, C2<float> b) { return vp(pv(a) + pv(b)); }
-template <> __device__ __forceinline__ C2<float> csub<float>(C2<float> a, C2<float> b) { return vp(pv(a) - pv(b)); }
-template <> __device__ __forceinline__ C2<float> cmul<float>(C2<float> a, C2<float> b) {
-  const f2v av = pv(a), bv = pv(b);
-  return vp(pv_lo(av) * bv + pv_hi(av) * (pv_swap(bv) * f2v{-1.f, 1.f}));   // (ax bx - ay by, ax by + ay bx)
-}
-template <> __device__ __forceinline__ C2<float> cmulc<float>(C2<float> a, C2<float> b) {
-  const f2v av = pv(a), bv = pv(b);
-  return vp(pv_lo(bv) * av + pv_hi(bv) * (pv_swap(av) * f2v{1.f, -1.f}));   // (ax bx + ay by, ay bx - ax by)
-}
-template <> __device__ __forceinline__ C2<float> cscale<float>(C2<float> a, float s) { return vp(pv(a) * s); }
-#endif
 
 // Two real rows packed as Z = a + i b, transformed: their spectra from Z at k and Zp = Z at -k,
 // A = (Z + conj Zp) / 2, B = (Z - conj Zp) / 2i (exact halvings, same rounding either form).
 template <typename T>
 __device__ __forceinline__ void herm_split(C2<T> z, C2<T> zp, C2<T>& A, C2<T>& B) {
-  if constexpr (HGP_PK && std::is_same<T, float>::value) {
-    const f2v Z = pv(z), P = pv(zp);
-    A = vp(__builtin_elementwise_fma(P, f2v{1.f, -1.f}, Z) * 0.5f);
-    B = vp(pv_swap(__builtin_elementwise_fma(P, f2v{-1.f, 1.f}, Z)) * f2v{0.5f, -0.5f});
-  } else {
-    const T hf = (T)0.5;
-    A = mk<T>(hf * (z.x + zp.x), hf * (z.y - zp.y));
-    B = mk<T>(hf * (z.y + zp.y), -hf * (z.x - zp.x));
-  }
+  const T hf = (T)0.5;
+  A = mk<T>(hf * (z.x + zp.x), hf * (z.y - zp.y));
+  B = mk<T>(hf * (z.y + zp.y), -hf * (z.x - zp.x));
 }
 // the inverse: Z = A + i B
 template <typename T>
 __device__ __forceinline__ C2<T> herm_join(C2<T> A, C2<T> B) {
-  if constexpr (HGP_PK && std::is_same<T, float>::value)
-    return vp(__builtin_elementwise_fma(pv_swap(pv(B)), f2v{-1.f, 1.f}, pv(A)));
-  else
-    return mk<T>(A.x - B.y, A.y + B.x);
+  return mk<T>(A.x - B.y, A.y + B.x);
 }
 
 // Raw buffer access (gfx9 resource word 3 = 0x00020000, stride 0): a wave-uniform base in
@@ -147,40 +111,11 @@ template <int H, int P> struct Stages {
 
 // multiply by exp(DIR * 2*pi*i*Q/16), DIR = -1 forward / +1 inverse; Q a compile-time
 // constant after unrolling (the switch folds).
-// packed: v * w for a compile-time constant w = (c, s): lo(v) (c, s) + hi(v) (-s, c), two
-// packed instructions (the broadcasts are op_sel)
-__device__ __forceinline__ C2<float> pk_mulk(C2<float> v, float c, float s) {
-  const f2v a = pv(v);
-  return vp(__builtin_elementwise_fma(pv_hi(a), f2v{-s, c}, pv_lo(a) * f2v{c, s}));
-}
-// packed: v * (+-i) = (-+y, +-x): the swap is op_sel, the signs one constant product
-__device__ __forceinline__ C2<float> pk_muli(C2<float> v, float sg) { return vp(pv_swap(pv(v)) * f2v{-sg, sg}); }
-
 template <typename T, int DIR>
 __device__ __forceinline__ C2<T> rot16(C2<T> v, int Q) {
   const T c8 = (T)0.70710678118654752440, c1 = (T)0.92387953251128675613, s1 = (T)0.38268343236508977173;
   Q &= 15;
   if (DIR > 0) Q = (16 - Q) & 15;           // inverse: exp(+i th) = forward rotation by -Q
-  if constexpr (HGP_PK && std::is_same<T, float>::value) {
-    switch (Q) {                            // forward angle th = 2 pi Q / 16: multiply by (cos th, -sin th)
-      case 0: return v;
-      case 4: return pk_muli(v, -1.f);
-      case 8: return vp(-pv(v));
-      case 12: return pk_muli(v, 1.f);
-      case 2: return pk_mulk(v, c8, -c8);
-      case 6: return pk_mulk(v, -c8, -c8);
-      case 10: return pk_mulk(v, -c8, c8);
-      case 14: return pk_mulk(v, c8, c8);
-      case 1: return pk_mulk(v, c1, -s1);
-      case 3: return pk_mulk(v, s1, -c1);
-      case 5: return pk_mulk(v, -s1, -c1);
-      case 7: return pk_mulk(v, -c1, -s1);
-      case 9: return pk_mulk(v, -c1, s1);
-      case 11: return pk_mulk(v, -s1, c1);
-      case 13: return pk_mulk(v, s1, c1);
-      default: return pk_mulk(v, c1, s1);   // 15
-    }
-  }
   switch (Q) {                              // forward: multiply by (cos th, -sin th), th=2pi Q/16
     case 0: return v;
     case 4: return mk<T>(v.y, -v.x);
@@ -210,16 +145,6 @@ __device__ __forceinline__ void dft(C2<T>* v) {
     C2<T> a = v[0], b = v[1];
     v[0] = cadd<T>(a, b);
     v[1] = csub<T>(a, b);
-  } else if constexpr (R == 4 && HGP_PK && std::is_same<T, float>::value) {
-    // packed: v1 / v3 = d02 +- (-+i) d13 as one fma each (x (+-1, -+1) is exact, so the fma
-    // rounds exactly like the add), the swap of d13 folds into op_sel
-    const f2v s02 = pv(v[0]) + pv(v[2]), d02 = pv(v[0]) - pv(v[2]);
-    const f2v s13 = pv(v[1]) + pv(v[3]), d13 = pv(v[1]) - pv(v[3]);
-    const f2v k = (DIR < 0) ? f2v{1.f, -1.f} : f2v{-1.f, 1.f};   // fwd: (y, -x); inv: (-y, x)
-    v[0] = vp(s02 + s13);
-    v[2] = vp(s02 - s13);
-    v[1] = vp(__builtin_elementwise_fma(pv_swap(d13), k, d02));
-    v[3] = vp(__builtin_elementwise_fma(pv_swap(d13), -k, d02));
   } else if constexpr (R == 4) {
     C2<T> s02 = cadd<T>(v[0], v[2]), d02 = csub<T>(v[0], v[2]);
     C2<T> s13 = cadd<T>(v[1], v[3]), d13 = csub<T>(v[1], v[3]);
@@ -276,24 +201,12 @@ __device__ __forceinline__ void xsync() {
 #ifndef HGP_TW_FULL_MAX
 #define HGP_TW_FULL_MAX (16 * 1024)   // largest half table (bytes) kept whole in LDS
 #endif
-//  * stage-1 power table (HGP_TW_T1, after the above): the second Stockham stage needs, per
-//    thread, the powers w^r (r < R1) of one twiddle w = W_H^{kk H/(NS1 R1)}, kk < NS1 (NS1, R1 =
-//    the first two radices).  There are only NS1 x R1 such values: they are tabulated once per
-//    block ([kk][r], pitch R1 + 1: the NS1 rows a wave reads start in distinct banks) and read
-//    with R1 - 1 LDS loads instead of one load and R1 - 2 complex products per butterfly.
-#ifndef HGP_TW_T1
-#define HGP_TW_T1 0   // measured slower (C2 column pass 0.149 -> 0.155 ms): LDS-bound, not VALU-bound
-#endif
 template <typename T, int H> struct TwTab {
   static constexpr bool TWO = H * (int)sizeof(C2<T>) > HGP_TW_FULL_MAX;
   static constexpr int LG = [] { int l = 0; while ((1 << l) < H) ++l; return l; }();
   static constexpr int S = TWO ? (1 << ((LG + 1) / 2)) : H;
   static constexpr int ENTRIES = TWO ? S + H / S : H;
-  using St = Stages<H, (H < PMax<T>::v ? H : PMax<T>::v)>;
-  static constexpr bool T1 = HGP_TW_T1 && St::count() >= 2 && St::radix(1) > 2;
-  static constexpr int T1_NS = St::radix(0), T1_R = T1 ? St::radix(1) : 0, T1_PITCH = T1_R + 1;
-  static constexpr int T1_ENTRIES = T1 ? T1_NS * T1_PITCH : 0;
-  static constexpr int BYTES = (ENTRIES + T1_ENTRIES) * (int)sizeof(C2<T>);
+  static constexpr int BYTES = ENTRIES * (int)sizeof(C2<T>);
 };
 
 // copy the table layout above from the global W_L^q array (all threads of the block)
@@ -303,16 +216,6 @@ __device__ __forceinline__ void stage_tw(C2<T>* tab, const C2<T>* __restrict__ t
   for (int q = tid; q < TW::ENTRIES; q += nthreads) {
     if constexpr (TW::TWO) tab[q] = q < TW::S ? twg[q] : twg[(q - TW::S) * TW::S];
     else tab[q] = twg[q];
-  }
-  if constexpr (TW::T1) {
-    constexpr int STEP = 2 * (H / (TW::T1_NS * TW::T1_R));      // W_H^e = W_L^{2e}
-    for (int e = tid; e < TW::T1_ENTRIES; e += nthreads) {
-      const int kk = e / TW::T1_PITCH, r = e - kk * TW::T1_PITCH;
-      const int q = STEP * kk * r;                               // < 2H: kk, r < 16
-      C2<T> w = twg[q & (H - 1)];
-      if (q & H) { w.x = -w.x; w.y = -w.y; }
-      tab[TW::ENTRIES + e] = w;
-    }
   }
 }
 
@@ -325,24 +228,6 @@ __device__ __forceinline__ C2<T> tw_at(const C2<T>* __restrict__ tab, int q) {
   else w = tab[qq];
   if (q & H) { w.x = -w.x; w.y = -w.y; }
   return w;
-}
-
-// W_L^{t + TT k} at a thread's positions (t < TT, t + TT k < H): the lane's W_L^t (one LDS
-// lookup, `wt`) times the wave-uniform W_L^{TT k}, read from the global half table `twg` by
-// scalar loads -- one LDS access per thread instead of one per point (the column pass is
-// bound by LDS traffic more than by VALU; ~1 ulp more rounding, so fp32 only: the fp64 plans
-// reproduce the reference's break iteration at tol 1e-10 and keep the exact table values).
-#ifndef HGP_POS_TW
-#define HGP_POS_TW 0   // measured slower: the scalar loads share lgkmcnt with the LDS exchanges
-#endif
-template <typename T, int H, int TT>
-__device__ __forceinline__ C2<T> tw_pos(const C2<T>* tab, const C2<T>* __restrict__ twg, C2<T> wt, int t, int k) {
-  if constexpr (HGP_POS_TW && std::is_same<T, float>::value) {   // fp64 keeps exact lookups
-    if (k == 0) return wt;
-    return cmul<T>(wt, twg[TT * k]);
-  } else {
-    return tw_at<T, H>(tab, t + TT * k);
-  }
 }
 
 // LDS address of logical element e (padding breaks the power-of-two strides of the
@@ -381,18 +266,12 @@ __device__ __forceinline__ void fft_stage(C2<T> (&v)[P], C2<T>* lds, int base, i
         // w^r with w = W_H^{kk*H/(NS*R)}: one LDS lookup, powers by binary powering
         // (at most 4 products deep, ~4 ulp) -- few LDS reads and few live registers.
         C2<T> wp[R];
-        if constexpr (TwTab<T, H>::T1 && S == 1) {
-          const C2<T>* t1 = tab + TwTab<T, H>::ENTRIES + kk * TwTab<T, H>::T1_PITCH;
+        wp[1] = tw_at<T, H>(tab, (2 * (H / (NS * R))) * kk);
 #pragma unroll
-          for (int r = 1; r < R; ++r) wp[r] = t1[r];
-        } else {
-          wp[1] = tw_at<T, H>(tab, (2 * (H / (NS * R))) * kk);
-#pragma unroll
-          for (int r = 2; r < R; ++r) {
-            const int hi = (r & (r - 1)) == 0 ? r / 2 : (1 << (31 - __builtin_clz(r)));   // r = hi + lo
-            const int lo = r - hi;
-            wp[r] = cmul<T>(wp[hi], wp[lo]);
-          }
+        for (int r = 2; r < R; ++r) {
+          const int hi = (r & (r - 1)) == 0 ? r / 2 : (1 << (31 - __builtin_clz(r)));   // r = hi + lo
+          const int lo = r - hi;
+          wp[r] = cmul<T>(wp[hi], wp[lo]);
         }
 #pragma unroll
         for (int r = 1; r < R; ++r) a[b][r] = (DIR < 0) ? cmul<T>(a[b][r], wp[r]) : cmulc<T>(a[b][r], wp[r]);
@@ -458,18 +337,12 @@ __device__ __forceinline__ void fft_bfly(const C2<T> (&v)[P], C2<T> (&a)[P], int
       const int j = t + b * TT;
       const int kk = j & (NS - 1);
       C2<T> wp[R];
-      if constexpr (TwTab<T, H>::T1 && S == 1) {   // stage-1 powers from the block's table
-        const C2<T>* t1 = tab + TwTab<T, H>::ENTRIES + kk * TwTab<T, H>::T1_PITCH;
+      wp[1] = tw_at<T, H>(tab, (2 * (H / (NS * R))) * kk);
 #pragma unroll
-        for (int r = 1; r < R; ++r) wp[r] = t1[r];
-      } else {
-        wp[1] = tw_at<T, H>(tab, (2 * (H / (NS * R))) * kk);
-#pragma unroll
-        for (int r = 2; r < R; ++r) {
-          const int hi = (r & (r - 1)) == 0 ? r / 2 : (1 << (31 - __builtin_clz(r)));
-          const int lo = r - hi;
-          wp[r] = cmul<T>(wp[hi], wp[lo]);
-        }
+      for (int r = 2; r < R; ++r) {
+        const int hi = (r & (r - 1)) == 0 ? r / 2 : (1 << (31 - __builtin_clz(r)));   // r = hi + lo
+        const int lo = r - hi;
+        wp[r] = cmul<T>(wp[hi], wp[lo]);
       }
 #pragma unroll
       for (int r = 1; r < R; ++r)
@@ -479,67 +352,11 @@ __device__ __forceinline__ void fft_bfly(const C2<T> (&v)[P], C2<T> (&a)[P], int
   }
 }
 
-// The exchange before the last stage of the one-wave 1024-point fp32 transform (radices
-// 16, 16, 4; TT = 64 threads) needs no LDS.  Thread t = (row rho = t>>4, column c = t&15)
-// reads positions t + 64k; stage 1 (NS = 16, one radix-16 butterfly per thread) wrote output
-// r' of thread t' to 256 (t'>>4) + 16 r' + (t'&15).  So destination (lane (rho, c), register
-// k = 4 al + be) <- source (lane (al, c), register 4 be + rho): the lane-row bits (lane bits
-// 4, 5) trade places with the register's low bits, and the register's two 2-bit fields swap.
-// v_permlane16_swap exchanges lane bit 4 with the pairing of two registers (odd rows of the
-// first <-> even rows of the second), v_permlane32_swap lane bit 5 (upper half <-> lower
-// half); the field swap is a renaming.  32 cross-lane moves instead of 16 LDS writes + 16
-// reads and their round-trip latency.
-template <typename T, int H, int P, int S>
-struct PermlaneXchg {
-  using St = Stages<H, P>;
-#ifdef HGP_PERMLANE_XCHG
-  static constexpr bool enabled = true;
-#else
-  static constexpr bool enabled = false;   // measured slower than the LDS exchange
-#endif
-  static constexpr bool value = enabled && std::is_same<T, float>::value && H == 1024 && P == 16 && St::count() == 3 &&
-                                S == 1 && St::radix(1) == 16 && St::ns(1) == 16 && St::radix(2) == 4;
-};
-
-__device__ __forceinline__ void pl16_swap(float& a, float& b) {
-  auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
-  a = __uint_as_float(r[0]);
-  b = __uint_as_float(r[1]);
-}
-__device__ __forceinline__ void pl32_swap(float& a, float& b) {
-  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
-  a = __uint_as_float(r[0]);
-  b = __uint_as_float(r[1]);
-}
-
-template <int P>
-__device__ __forceinline__ void fft_xchg_permlane(C2<float> (&a)[P], C2<float> (&v)[P]) {
-#pragma unroll
-  for (int r = 0; r < 16; r += 2) {          // lane bit 4 <-> register bit 0
-    pl16_swap(a[r].x, a[r + 1].x);
-    pl16_swap(a[r].y, a[r + 1].y);
-  }
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {             // lane bit 5 <-> register bit 1
-    if (r & 2) continue;
-    pl32_swap(a[r].x, a[r + 2].x);
-    pl32_swap(a[r].y, a[r + 2].y);
-  }
-#pragma unroll
-  for (int al = 0; al < 4; ++al)
-#pragma unroll
-    for (int be = 0; be < 4; ++be) v[4 * al + be] = a[4 * be + al];
-}
-
 // exchange after stage S: write a (stage-S outputs), read this thread's stage-(S+1) inputs
 template <typename T, int H, int P, int STRIDE, bool WAVE, int S>
 __device__ __forceinline__ void fft_xchg(C2<T> (&a)[P], C2<T> (&v)[P], C2<T>* lds, int base, int t) {
   using St = Stages<H, P>;
   constexpr int R = St::radix(S), NS = St::ns(S), TT = H / P, NB = P / R;
-  if constexpr (PermlaneXchg<T, H, P, S>::value && STRIDE == 1 && WAVE) {
-    fft_xchg_permlane<P>(a, v);
-    return;
-  }
   const int idxD = (t / NS) * NS * R + (t & (NS - 1));
   const int wb = base + idxD * STRIDE;
   const int pwb = lds_phys(wb);
@@ -552,19 +369,8 @@ __device__ __forceinline__ void fft_xchg(C2<T> (&a)[P], C2<T> (&v)[P], C2<T>* ld
   xsync<WAVE>();
   const int rb = base + t * STRIDE;
   const int prb = lds_phys(rb);
-#ifdef HGP_LDS_NOREAD2
-  // one ds_read_b64 per value (2 LDS cycles) instead of the ds_read2_b64 pairs (8 cycles) the
-  // load/store optimiser forms from a shared base: every read gets its own address register
-#pragma unroll
-  for (int k = 0; k < P; ++k) {
-    int a = lds_at(prb, rb, TT * k * STRIDE, false);
-    asm volatile("" : "+v"(a));
-    v[k] = lds[a];
-  }
-#else
 #pragma unroll
   for (int k = 0; k < P; ++k) v[k] = lds[lds_at(prb, rb, TT * k * STRIDE, false)];
-#endif
 }
 
 // last stage's outputs back to natural register order

@@ -95,10 +95,6 @@ struct PassDesc {
   void* cg_p;
   const void* cg_coef;        // per-RHS alpha (EPI_XR) or beta (EPI_P)
   void* cg_part;              // EPI_XR: per-block partial sums of r.r  [q][row block]
-  // chained forward row pass (EPI_XR / EPI_P): the updated vector's rows (new r / new p) are
-  // transformed again in the same block and written as the next operator's column-major half
-  // spectra over the block's own segment of the intermediate (View{W, -, S0}: same geometry)
-  void* chain_out;
 };
 
 constexpr int LDS_CAP = 160 * 1024;
@@ -356,7 +352,6 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
     const int in_len = d.in.len;
     const int lim = in_len - 1;
     const bool fold = CAN_FOLD && in_len > H;
-    const C2<T> wt = tw_at<T, H>(tab, t);
 #pragma unroll
     for (int k = 0; k < P; ++k) {
       const int p = t + TT * k;
@@ -372,7 +367,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
         if (fold) c = load_hi(p);
       }
       va[k] = cadd<T>(a, c);
-      vb[k] = cmul<T>(csub<T>(a, c), tw_pos<T, H, TT>(tab, twg, wt, t, k));
+      vb[k] = cmul<T>(csub<T>(a, c), tw_at<T, H>(tab, p));
     }
   }
 
@@ -417,10 +412,6 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
       // the line's real spectrum, loaded after the forward transforms (no registers held across
       // them); L2-resident: every line of a block shares it (RHS-fastest map, XCD-grouped)
       T sre1[P];
-#ifdef HGP_EXP_NOSPEC   // timing experiment only (wrong results): no spectrum loads
-#pragma unroll
-      for (int k = 0; k < P; ++k) { sre[k] = (T)1; sre1[k] = (T)1; }
-#else
       if constexpr (BUF) {
         const BufRsrc rspec = buf_rsrc(sb, 0x7fffffffu);
 #pragma unroll
@@ -435,7 +426,6 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
           sre1[k] = sb[so + (H + TT * k) * sp];
         }
       }
-#endif
       if (d.spart != nullptr) {   // uniform: spectral dot sum_k S_k |X_k|^2 of this line
 #pragma unroll
         for (int k = 0; k < P; ++k) {
@@ -488,11 +478,10 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
     // registers or scratch) from the loads at the top of the kernel
     asm volatile("" : "+v"(t));
     if constexpr (LAY == LAY_STRIDED) asm volatile("" : "+v"(lc));
-    const C2<T> wt = tw_at<T, H>(tab, t);
 #pragma unroll
     for (int k = 0; k < P; ++k) {
       const int p = t + TT * k;
-      const C2<T> wo = cmulc<T>(vb[k], tw_pos<T, H, TT>(tab, twg, wt, t, k));
+      const C2<T> wo = cmulc<T>(vb[k], tw_at<T, H>(tab, p));
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
         const C2<T> y = hh == 0 ? cadd<T>(va[k], wo) : csub<T>(va[k], wo);
@@ -531,130 +520,6 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
           reinterpret_cast<T*>(d.spart)[(int64_t)q * d.Rn + r] = w * s;
         }
       }
-    }
-  }
-}
-
-// ------------------------------------------------------------------------------------------
-// Wave-split convolution along contiguous complex lines (the 2-D column pass on the
-// transposed intermediate, hgp_api.hip): y = crop(IFFT_L(S . FFT_L(pad x))) per line.
-// The two frequency halves of a line run in two different thread groups (one wavefront each
-// at H = 1024): each group loads the line, forms its half's input (x or x W_L^p), runs the
-// forward FFT, the spectrum product and the inverse FFT with wave-local exchanges only, and
-// the odd group adds the even group's result after ONE block barrier (y = ye + conj(W) yo).
-// Half the registers of a one-group-per-line kernel (no second half held), so twice the
-// waves per SIMD hide the memory and LDS latency; the spectrum of the half is prefetched
-// with the data.  NOT dispatched by the library: the one-group-per-line k_pass<CONTIG, CONV>
-// measured faster (its two halves share the exchange image and the line loads); kept only
-// for the side-by-side timing in tools/passbench.hip.
-// ------------------------------------------------------------------------------------------
-template <typename T, int H> struct ConvCfg {
-  static constexpr int P = (H < PMax<T>::v) ? H : PMax<T>::v;
-  static constexpr int TT = H / P;                     // threads per half-line group
-#ifndef HGP_CONV_LINES
-  static constexpr int C0 = 4;
-#else
-  static constexpr int C0 = HGP_CONV_LINES;
-#endif
-  static constexpr int ex_elems(int c) { return 2 * c * H + (2 * c * H) / 16; }
-  static constexpr int lds_bytes_for(int c) { return ex_elems(c) * (int)sizeof(C2<T>) + TwTab<T, H>::BYTES; }
-  static constexpr int c_lines() {
-    int c = C0 * 64 / TT;            // C0 lines per block at one wave per half-line
-    if (c < 1) c = 1;
-    while (c > 1 && (2 * c * TT > 1024 || lds_bytes_for(c) > LDS_CAP / 2)) c >>= 1;
-    return c;
-  }
-  static constexpr int C = c_lines();
-  static constexpr int THREADS = 2 * C * TT;
-  static constexpr int LDS = lds_bytes_for(C);
-  static constexpr bool WAVE = TT <= 64;
-#ifndef HGP_MINW_CONV
-  static constexpr int MINW = 4;
-#else
-  static constexpr int MINW = HGP_MINW_CONV;
-#endif
-};
-
-template <typename T, int H, bool CPLX_SPEC>
-__global__ __launch_bounds__((ConvCfg<T, H>::THREADS), (ConvCfg<T, H>::MINW)) void k_conv_ws(const PassDesc d) {
-  using Cfg = ConvCfg<T, H>;
-  constexpr int P = Cfg::P, TT = Cfg::TT, C = Cfg::C;
-  if (d.done != nullptr && *d.done) return;                          // uniform: before any barrier
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  C2<T>* lds = reinterpret_cast<C2<T>*>(smem_raw);
-  C2<T>* tab = lds + Cfg::ex_elems(C);
-  {
-    const C2<T>* __restrict__ twg = reinterpret_cast<const C2<T>*>(d.tw);
-    stage_tw<T, H>(tab, twg, threadIdx.x, Cfg::THREADS);
-  }
-  const int g = threadIdx.x / TT;          // group: line l = g/2, half = g%2
-  const int t = threadIdx.x - g * TT;
-  const int l = g >> 1;
-  const int half = g & 1;
-  const int gbase = g * H;                 // this group's exchange image (logical, lds_phys pads)
-  const int64_t line = (int64_t)blockIdx.x * C + l;
-  int q = (int)(line / d.Rn);
-  int r = (int)(line - (int64_t)q * d.Rn);
-  const bool valid = q < d.Q;
-  if (!valid) { q = 0; r = 0; }
-  const C2<T>* in_c = reinterpret_cast<const C2<T>*>(d.in.ptr) + (int64_t)q * d.in.q_stride + (int64_t)r * d.in.r_stride;
-  C2<T>* out_c = reinterpret_cast<C2<T>*>(d.out.ptr) + (int64_t)q * d.out.q_stride + (int64_t)r * d.out.r_stride;
-  const int in_len = d.in.len;
-
-  // prefetch: this half's spectrum (real or complex) and the line (x[p], p < H; in_len <= H)
-  T sre[P];
-  C2<T> scx[P];
-  const int sp = (int)d.spec_p;
-  if constexpr (!CPLX_SPEC) {
-    const T* sb = reinterpret_cast<const T*>(d.spec) + (int64_t)r * d.spec_r;
-#pragma unroll
-    for (int k = 0; k < P; ++k) sre[k] = sb[(half * H + t + TT * k) * sp];
-  } else {
-    const C2<T>* sb = reinterpret_cast<const C2<T>*>(d.spec) + (int64_t)r * d.spec_r;
-#pragma unroll
-    for (int k = 0; k < P; ++k) scx[k] = sb[(half * H + t + TT * k) * sp];
-  }
-  C2<T> v[P];
-#pragma unroll
-  for (int k = 0; k < P; ++k) {
-    const int p = t + TT * k;
-    C2<T> a = in_c[p < in_len ? p : in_len - 1];
-    if (p >= in_len) a = mk<T>(0, 0);
-    v[k] = a;
-  }
-  __syncthreads();   // twiddle table staged
-  if (half) {
-#pragma unroll
-    for (int k = 0; k < P; ++k) v[k] = cmul<T>(v[k], tw_at<T, H>(tab, t + TT * k));
-  }
-  fft_line<T, H, P, -1, 1, Cfg::WAVE>(v, lds, gbase, t, tab);
-  if constexpr (!CPLX_SPEC) {
-#pragma unroll
-    for (int k = 0; k < P; ++k) v[k] = mk<T>(v[k].x * sre[k], v[k].y * sre[k]);
-  } else {
-#pragma unroll
-    for (int k = 0; k < P; ++k) v[k] = d.spec_kind == SPEC_CPLX ? cmul<T>(v[k], scx[k]) : cmulc<T>(v[k], scx[k]);
-  }
-  fft_line<T, H, P, +1, 1, Cfg::WAVE>(v, lds, gbase, t, tab);
-  // combine: the even group parks ye in its image, the odd group adds conj(W_L^p) yo
-  xsync<Cfg::WAVE>();
-  if (!half) {
-#pragma unroll
-    for (int k = 0; k < P; ++k) lds[lds_phys(gbase + t + TT * k)] = v[k];
-  }
-  __syncthreads();
-  if (half && valid) {
-    const int out_len = d.out.len;
-    const int ebase = gbase - H;
-    int tt = t;
-    asm volatile("" : "+v"(tt));
-#pragma unroll
-    for (int k = 0; k < P; ++k) {
-      const int p = tt + TT * k;
-      const C2<T> ye = lds[lds_phys(ebase + p)];
-      const C2<T> wo = cmulc<T>(v[k], tw_at<T, H>(tab, p));
-      if (p < out_len) out_c[p] = cadd<T>(ye, wo);
-      if (p + H < out_len) out_c[p + H] = csub<T>(ye, wo);
     }
   }
 }

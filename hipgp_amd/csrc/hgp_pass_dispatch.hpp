@@ -66,24 +66,18 @@ static PassGeom geom_h(int lay) {
     default: break;                                                                                  \
   }
 
-template <typename T, int H, int EPI, bool CH>
-static hipError_t launch_rowt_inv_c(const PassDesc& d, int64_t nb, hipStream_t s) {
+template <typename T, int H, int EPI>
+static hipError_t launch_rowt_inv(const PassDesc& d, int64_t nb, hipStream_t s) {
   using Cfg = RowTCfg<T, H>;
   static bool attr_set = false;   // opt in to > 64 KB dynamic LDS once per instance
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_row_inv_t<T, H, EPI, CH>,
+    hipError_t e = hipFuncSetAttribute((const void*)k_row_inv_t<T, H, EPI>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  hipLaunchKernelGGL((k_row_inv_t<T, H, EPI, CH>), dim3((unsigned)nb), dim3(Cfg::THREADS), Cfg::LDS, s, d);
+  hipLaunchKernelGGL((k_row_inv_t<T, H, EPI>), dim3((unsigned)nb), dim3(Cfg::THREADS), Cfg::LDS, s, d);
   return hipGetLastError();
-}
-template <typename T, int H, int EPI>
-static hipError_t launch_rowt_inv(const PassDesc& d, int64_t nb, hipStream_t s) {
-  if constexpr (EPI != EPI_OUT)
-    if (d.chain_out != nullptr) return launch_rowt_inv_c<T, H, EPI, true>(d, nb, s);
-  return launch_rowt_inv_c<T, H, EPI, false>(d, nb, s);
 }
 
 template <typename T, int H>

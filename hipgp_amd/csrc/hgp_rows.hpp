@@ -63,9 +63,8 @@ __device__ __forceinline__ void row_fwd_tail(C2<T> (&va)[P], C2<T> (&vb)[P],
   using Cfg = RowTCfg<T, H>;
   constexpr int TT = Cfg::TT, C = Cfg::C, PITCH = Cfg::PITCH;
   static_assert(P == Cfg::P, "row_fwd_tail: P");
-  const C2<T> wt0 = tw_at<T, H>(tab, t);
-  #pragma unroll
-  for (int k = 0; k < P; ++k) vb[k] = cmul<T>(va[k], tw_pos<T, H, TT>(tab, twg, wt0, t, k));
+#pragma unroll
+  for (int k = 0; k < P; ++k) vb[k] = cmul<T>(va[k], tw_at<T, H>(tab, t + TT * k));
   const BufRsrc rW = buf_rsrc(W, 0x7fffffffu);     // one RHS's slab: < 2 GiB (checked on the host)
   // both frequency halves' transforms, interleaved over the group's exchange image
   fft_line2<T, H, P, -1, 1, Cfg::WAVE>(va, vb, lds, lbase, t, tab);
@@ -122,7 +121,7 @@ __device__ __forceinline__ void row_fwd_tail(C2<T> (&va)[P], C2<T> (&vb)[P],
 template <typename T, int H>
 __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) void k_row_fwd_t(const PassDesc d) {
   using Cfg = RowTCfg<T, H>;
-  constexpr int P = Cfg::P, TT = Cfg::TT, C = Cfg::C, PITCH = Cfg::PITCH;
+  constexpr int P = Cfg::P, TT = Cfg::TT, C = Cfg::C;
   if (d.done != nullptr && *d.done) return;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   C2<T>* lds = reinterpret_cast<C2<T>*>(smem_raw);
@@ -169,13 +168,10 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
 // out_len), streamed with the row layout of the (nrhs, M) vectors:
 //   EPI_XR (y = A p):     x += a p;  r -= a y;  returns this thread's share of r.r  (cg.py:67-69)
 //   EPI_P  (y = C^-1 r):  p = y + b p                                                 (cg.py:75)
-// Four elements per thread are loaded before any is stored (the vectors never alias).  `keep`:
-// the updated value (new r / new p) replaces y in `ys` for the chained forward transform
-// (each element is read and rewritten by the same thread).
+// Four elements per thread are loaded before any is stored (the vectors never alias).
 template <typename T, int EPI, int THREADS>
-__device__ __forceinline__ T cg_epilogue(T* __restrict__ ys, int nrow, int out_len, T* __restrict__ xg,
-                                         T* __restrict__ rg, T* __restrict__ pg, int64_t rpitch, T coef,
-                                         bool keep) {
+__device__ __forceinline__ T cg_epilogue(const T* __restrict__ ys, int nrow, int out_len, T* __restrict__ xg,
+                                         T* __restrict__ rg, T* __restrict__ pg, int64_t rpitch, T coef) {
   const int nel = nrow * out_len;
   // the block's rows are one < 2 GiB window of each vector: raw buffers, 32-bit lane offsets
   const BufRsrc rp = buf_rsrc(pg, 0x7fffffffu), rx = buf_rsrc(xg, 0x7fffffffu), rr = buf_rsrc(rg, 0x7fffffffu);
@@ -205,11 +201,8 @@ __device__ __forceinline__ T cg_epilogue(T* __restrict__ ys, int nrow, int out_l
           const T rn = rv[u] - coef * yv[u];
           buf_st<T>(rn, rr, g[u]);
           s += rn * rn;
-          if (keep) ys[e0 + u * THREADS] = rn;
         } else {
-          const T pn = yv[u] + coef * pv[u];
-          buf_st<T>(pn, rp, g[u]);
-          if (keep) ys[e0 + u * THREADS] = pn;
+          buf_st<T>(yv[u] + coef * pv[u], rp, g[u]);
         }
       }
     }
@@ -217,8 +210,7 @@ __device__ __forceinline__ T cg_epilogue(T* __restrict__ ys, int nrow, int out_l
   return s;
 }
 
-// CH (EPI_XR / EPI_P only): chained forward transform of the updated vector into d.chain_out.
-template <typename T, int H, int EPI = EPI_OUT, bool CH = false>
+template <typename T, int H, int EPI = EPI_OUT>
 __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) void k_row_inv_t(const PassDesc d) {
   using Cfg = RowTCfg<T, H>;
   constexpr int P = Cfg::P, TT = Cfg::TT, C = Cfg::C, PITCH = Cfg::PITCH;
@@ -322,11 +314,10 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
     __syncthreads();   // every group is done with its exchange image
     int tt = t;
     asm volatile("" : "+v"(tt));
-    const C2<T> wtc = tw_at<T, H>(tab, tt);
 #pragma unroll
     for (int k = 0; k < P; ++k) {
       const int p = tt + TT * k;
-      const C2<T> wo = cmulc<T>(vb[k], tw_pos<T, H, TT>(tab, twg, wtc, tt, k));
+      const C2<T> wo = cmulc<T>(vb[k], tw_at<T, H>(tab, p));
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
         const C2<T> y = hh == 0 ? cadd<T>(va[k], wo) : csub<T>(va[k], wo);
@@ -343,14 +334,11 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
     T* pg = reinterpret_cast<T*>(d.cg_p) + g0;
     T* xg = EPI == EPI_XR ? reinterpret_cast<T*>(d.cg_x) + g0 : pg;
     T* rg = EPI == EPI_XR ? reinterpret_cast<T*>(d.cg_r) + g0 : pg;
-    constexpr bool chain = CH;
-    T s = cg_epilogue<T, EPI, Cfg::THREADS>(ys, nrow_blk, out_len, xg, rg, pg, d.out.r_stride, coef, chain);
+    T s = cg_epilogue<T, EPI, Cfg::THREADS>(ys, nrow_blk, out_len, xg, rg, pg, d.out.r_stride, coef);
     if constexpr (EPI == EPI_XR) {   // deterministic block sum of r.r -> partial [q][rb]
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-      // past the staged rows (2C x out_len <= C x H values < the exchange area): the twiddle
-      // table stays intact for the chained transform
-      T* red = ys + 2 * C * out_len;
+      T* red = ys + 2 * C * out_len;   // past the staged rows (2C x out_len <= C x H values)
       if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
       __syncthreads();
       if (threadIdx.x == 0) {
@@ -359,28 +347,10 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
         reinterpret_cast<T*>(d.cg_part)[(int64_t)q * nrb + rb] = tot;
       }
     }
-    if constexpr (!chain) return;
-    // Chained forward row pass of the updated vector (the next operator's first pass): the
-    // block's rows are complete in `ys`, so they are transformed here instead of being read
-    // back from HBM by a k_row_fwd_t launch.  The half spectra go over this block's own row
-    // segment of the intermediate, whose tile was read in full at the top of this kernel.
-    __syncthreads();   // updated rows staged
-#pragma unroll
-    for (int k = 0; k < P; ++k) {
-      const int p = t + TT * k;
-      const T a = (pvalid && p < out_len) ? ys[(2 * l) * out_len + p] : (T)0;
-      const T b = (has2 && p < out_len) ? ys[(2 * l + 1) * out_len + p] : (T)0;
-      va[k] = mk<T>(a, b);
-    }
-    __syncthreads();   // rows read before the exchange images overlay them
-    row_fwd_tail<T, H>(va, vb, lds, tab, twg, t, l, lbase, reinterpret_cast<C2<T>*>(d.chain_out) + (int64_t)q * d.in.q_stride,
-                       S0, row0, nrow_blk);
     return;
   }
   T* out_a = reinterpret_cast<T*>(d.out.ptr) + (int64_t)q * d.out.q_stride + (int64_t)(pvalid ? 2 * rp : 0) * d.out.r_stride;
   T* out_b = out_a + d.out.r_stride;
-  const BufRsrc roa = buf_rsrc(out_a, pvalid ? (uint32_t)out_len * (uint32_t)sizeof(T) : 0u);
-  const BufRsrc rob = buf_rsrc(out_b, has2 ? (uint32_t)out_len * (uint32_t)sizeof(T) : 0u);
   const T* dot_a = nullptr;
   const T* dot_b = nullptr;
   if (d.partial != nullptr) {
@@ -390,26 +360,15 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
   T dsum = 0;
   int tt = t;
   asm volatile("" : "+v"(tt));
-  const C2<T> wtc = tw_at<T, H>(tab, tt);
 #pragma unroll
   for (int k = 0; k < P; ++k) {
     const int p = tt + TT * k;
-    const C2<T> wo = cmulc<T>(vb[k], tw_pos<T, H, TT>(tab, twg, wtc, tt, k));
+    const C2<T> wo = cmulc<T>(vb[k], tw_at<T, H>(tab, p));
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
       const C2<T> y = hh == 0 ? cadd<T>(va[k], wo) : csub<T>(va[k], wo);
       const int pp = p + hh * H;
-#ifndef HGP_ROWINV_BUFFER_OUT
-      if (false) {   // plain global stores measured ~4 % faster here than buffer stores
-#else
-      if (dot_a == nullptr) {   // uniform: buffer stores, the ranges crop and drop absent rows
-#endif
-        if (hh * H < out_len) {
-          const uint32_t lo = (uint32_t)t * (uint32_t)sizeof(T), so = (uint32_t)((pp - t) * (int)sizeof(T));
-          buf_st<T>(y.x, roa, lo, so);
-          buf_st<T>(y.y, rob, lo, so);
-        }
-      } else if (pvalid && pp < out_len) {
+      if (pvalid && pp < out_len) {
         out_a[pp] = y.x;
         if (dot_a != nullptr) dsum += y.x * dot_a[pp];
         if (has2) {

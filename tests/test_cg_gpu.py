@@ -131,8 +131,9 @@ def test_pcg_cols_layout_equals_rows(dims, dtype):
         assert torch.equal(xc.t(), xr) and torch.equal(xc2, xc)
         assert ir == ic
     # early break in column layout: the iteration count matches the row layout's
-    xr, ir = P.pcg(b, 200, 1e-3 * float(b.norm(dim=1).min()), precond=True, return_iters=True)
-    xc, ic = P.pcg(b.t().contiguous(), 200, 1e-3 * float(b.norm(dim=1).min()), precond=True, return_iters=True,
+    rtol = 1e-3 if dtype == torch.float64 else 3e-2     # fp32 stalls near its rounding floor
+    xr, ir = P.pcg(b, 200, rtol * float(b.norm(dim=1).min()), precond=True, return_iters=True)
+    xc, ic = P.pcg(b.t().contiguous(), 200, rtol * float(b.norm(dim=1).min()), precond=True, return_iters=True,
                    layout=_lib.LAYOUT_COLS)
     assert ir == ic < 200 and torch.equal(xc.t(), xr)
 

@@ -262,35 +262,3 @@ def test_large_grid_fp32_vs_fp64(m):
     for name, a, b, tol in zip(("K", "Cinv", "RT"), outs[torch.float32], outs[torch.float64], (2e-5, 2e-3, 1e-4)):
         err = float((a - b).abs().max() / b.abs().max())
         assert err < tol, (name, err)
-
-
-# ---- chained 2-D PCG row passes (opt-in HGP_CHAIN=1, hgp_api.hip run_op) ----------------------
-@pytest.mark.parametrize("dims,dtype,B", [((1024, 1024), torch.float32, 32), ((33, 40), torch.float64, 5),
-                                          ((65, 64), torch.float32, 3)], ids=["C2_f32", "ragged_f64", "odd_rows_f32"])
-def test_pcg_chained_matches_unchained(dims, dtype, B, monkeypatch):
-    """The chained row-inverse kernel transforms exactly the values it stores, with the code of
-    k_row_fwd_t compiled into another kernel (FMA contraction may differ), so the chained PCG
-    agrees with the default one to rounding amplified over 20 iterations; when chaining must
-    fall back (more chunks than streams) the result is bit-identical.  Odd row counts leave a
-    half-empty last pair; B = 5 splits 3 + 2 over the two streams."""
-    from hipgp_amd.plan import ToeplitzPlan
-    grids = [np.linspace(-1, 1, m) for m in dims]
-    col = zo.toeplitz_column(grids, lambda x, y: zo.kernel_eval("matern", x, y, (1., .05), nu=1.5), 1e-2)
-    g = torch.Generator(device=DEV).manual_seed(5)
-    b = torch.randn(B, int(np.prod(dims)), device=DEV, generator=g, dtype=torch.float64).to(dtype)
-    out = {}
-    for chain, ws_mb in (("0", None), ("1", None), ("1", "1")):
-        monkeypatch.setenv("HGP_CHAIN", chain)
-        if ws_mb is None:
-            monkeypatch.delenv("HGP_WS_MB", raising=False)
-        else:   # tiny workspace: more chunks than streams, chaining must fall back
-            monkeypatch.setenv("HGP_WS_MB", ws_mb)
-        P = ToeplitzPlan(dims, dtype, DEV)
-        P.set_column(torch.tensor(col, device=DEV, dtype=dtype))
-        out[(chain, ws_mb)] = P.pcg(b, 20, 1e-12, precond=True).clone()
-    ref = out[("0", None)]
-    assert torch.isfinite(ref).all()
-    tol = 1e-4 if dtype == torch.float32 else 1e-11
-    rel = float(((out[("1", None)] - ref).norm(dim=1) / ref.norm(dim=1)).max())
-    assert rel < tol, rel
-    assert torch.equal(out[("1", "1")], ref)

@@ -40,6 +40,28 @@ def kernel(kind, nu, dtype):
     return zk.SqExp(dtype=dtype) if kind == "sqexp" else zk.Matern(nu=nu, dtype=dtype)
 
 
+HBM_PEAK = 8.0e12
+
+
+def byte_model(dims, maxiter):
+    """SURVEY §8(d) pruned-pass algorithmic bytes per RHS (fp32): B_K, B_RT, compute_kn."""
+    d = len(dims)
+    M = int(np.prod(dims))
+    n = [2 * m - 2 for m in dims]
+    Mp = int(np.prod(n))
+    h = dims[-1]                          # n_last / 2 + 1 = m_last
+    if d == 1:
+        bk, brt = 8 * M, 4 * M + 4 * Mp
+    elif d == 2:
+        bk = 8 * M + 32 * dims[0] * h
+        brt = 4 * M + 16 * dims[0] * h + 16 * n[0] * h + 4 * Mp
+    else:
+        bk = 8 * M + 32 * dims[0] * dims[1] * h + 32 * dims[0] * n[1] * h
+        brt = 4 * M + 16 * dims[0] * dims[1] * h + 16 * dims[0] * n[1] * h + 32 * n[0] * n[1] * h + 4 * Mp
+    kn = maxiter * (2 * bk + 44 * M) + bk + brt
+    return bk, brt, kn
+
+
 def timed(fn, reps=3):
     fn()
     torch.cuda.synchronize()
@@ -108,6 +130,11 @@ def run(name, dev):
         out["speedup_compute_kn_vs_reference_cpu"] = ref["compute_kn_s_per_rhs"] / out["compute_kn_s_per_rhs"]
     else:
         out["speedup_compute_kn_vs_reference_cpu"] = ref["compute_kn_s"] / t_kn
+    bk, brt, bkn = byte_model(dims, maxiter)
+    out["kmatvec_hbm_frac"] = B * bk / t_op / HBM_PEAK
+    out["compute_kn_model_s"] = B * bkn / HBM_PEAK
+    out["compute_kn_hbm_frac"] = B * bkn / t_kn / HBM_PEAK
+    out["ws_mb"] = os.environ.get("HGP_WS_MB", "default")
     out["peak_mem_gb"] = torch.cuda.max_memory_allocated(dev) / 1e9
     return out
 

@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--dims", default="256,256,128")
     ap.add_argument("--rhs", type=int, default=25)
     ap.add_argument("--op", default="K", choices=["K", "CINV", "RT", "R"])
+    ap.add_argument("--op-only", type=int, default=0, help="only run the op this many times (PMC passes)")
     a = ap.parse_args()
     from hipgp_amd import _lib
     import ziggy.kernels as zk
@@ -48,6 +49,12 @@ def main():
         e.synchronize()
         return s.elapsed_time(e) / reps
 
+    if a.op_only:
+        for _ in range(a.op_only):
+            plan.apply(op, x, out=y)
+        torch.cuda.synchronize()
+        print(json.dumps({"dims": dims, "rhs": a.rhs, "op": a.op, "ops": a.op_only}))
+        return
     op_ms = tm(lambda: plan.apply(op, x, out=y))
     npass = _lib.lib().hgp_op_pass_count(plan._h)
     passes = []

@@ -1,0 +1,37 @@
+"""Summarise tools/prof_cfg.sh: per-kernel rocprofv3 stats (from the timing run) and HBM bytes per
+batched operator from the FETCH_SIZE / WRITE_SIZE passes (FETCH_SIZE x2: gfx950 counts half of
+wide streaming reads, MI355X_MICROARCH.md §HBM), against the SURVEY §8(d) algorithmic bytes."""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+root, nops, shape, rhs = sys.argv[1], int(sys.argv[2]), [int(v) for v in sys.argv[3].split(",")], int(sys.argv[4])
+OP_KERNELS = ("k_row_fwd_t", "k_row_inv_t", "k_pass<float")
+stats = glob.glob(os.path.join(root, "stats", "**", "*kernel_stats.csv"), recursive=True)
+if stats:
+    with open(stats[0]) as fh:
+        rows = list(csv.DictReader(fh))
+    print("kernel stats (timing run):")
+    for r in rows[:12]:
+        print(f"  {r['Name'][:70]:70s} calls {r['Calls']:>5} avg_us {float(r['AverageNs']) / 1e3:9.1f} pct {float(r['Percentage']):5.1f}")
+tot = collections.defaultdict(float)
+for c in ("FETCH_SIZE", "WRITE_SIZE"):
+    for f in glob.glob(os.path.join(root, c, "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if any(k in row.get("Kernel_Name", "") for k in OP_KERNELS):
+                    tot[c] += float(row["Counter_Value"])
+d = len(shape)
+M = 1
+for m in shape:
+    M *= m
+h = shape[-1]
+bk = 8 * M + (32 * shape[0] * h if d == 2 else 32 * shape[0] * shape[1] * h + 32 * shape[0] * (2 * shape[1] - 2) * h)
+traffic = (2 * tot["FETCH_SIZE"] + tot["WRITE_SIZE"]) * 1024 / nops
+res = {"shape": shape, "rhs": rhs, "ops": nops, "fetch_kb_per_op_raw": tot["FETCH_SIZE"] / nops,
+       "write_kb_per_op": tot["WRITE_SIZE"] / nops, "traffic_bytes_per_op": traffic,
+       "algorithmic_bytes_per_op": rhs * bk, "traffic_over_algorithmic": traffic / (rhs * bk)}
+print(json.dumps(res))

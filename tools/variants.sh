@@ -1,8 +1,8 @@
 #!/bin/bash
 # Compile-time variants of libhipgp for tuning: build here (BUILD=1), time on the GPU box.
-#   VARS="a: n:-DHGP_LDS_NOREAD2"  (name:flags, space separated; flags use ',' for spaces)
+#   VARS="a: s8:-DHGP_ROWT_PAIRS=4"  (name:flags, space separated; flags use "," for spaces)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-VARS=${VARS:-"a: n:-DHGP_LDS_NOREAD2"}
+VARS=${VARS:-"a:"}
 if [ -n "$BUILD" ]; then
   for v in $VARS; do
     k=${v%%:*}; f=${v#*:}; f=${f//,/ }
