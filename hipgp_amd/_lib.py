@@ -18,6 +18,7 @@ HGP_F32, HGP_F64 = 0, 1
 OP_K, OP_CINV, OP_RT, OP_R = 0, 1, 2, 3
 SPEC_D, SPEC_DSQRT, SPEC_DI = 0, 1, 2
 LAYOUT_ROWS, LAYOUT_COLS = 0, 1
+SLAB_FWD, SLAB_CONV, SLAB_INV = 0, 1, 2
 
 # every symbol include/hipgp.h declares (tests check the library exports all of them)
 EXPORTS = (
@@ -28,6 +29,7 @@ EXPORTS = (
     "hgp_kuf_semi_mc", "hgp_kuf_semi_sqexp", "hgp_knn_doubly_diag", "hgp_meanfield_stats",
     "hgp_block_stats", "hgp_sym_toeplitz_dqf", "hgp_plan_column_grad",
     "hgp_plan_dqf", "hgp_pcg_local_flag", "hgp_pcg_set_done", "hgp_pcg_iters",
+    "hgp_slab_info", "hgp_slab_pass",
 )
 KERN_SQEXP, KERN_MATERN12, KERN_MATERN32, KERN_MATERN52, KERN_GNEITING = 0, 1, 2, 3, 4
 
@@ -78,6 +80,8 @@ def lib():
         "hgp_pcg_local_flag": (i32, [vp, dbl, vp]),
         "hgp_pcg_set_done": (i32, [vp, vp]),
         "hgp_pcg_iters": (i32, [vp, pi32]),
+        "hgp_slab_info": (i32, [vp, i32, pi64, pi64]),
+        "hgp_slab_pass": (i32, [vp, i32, i32, vp, vp, i64, i64, i64, i64]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

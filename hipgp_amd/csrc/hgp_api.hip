@@ -575,6 +575,113 @@ int set_column_t(hgp_plan* P, const void* column, double jitter, double clamp_mi
   return 0;
 }
 
+// ---- grid-block (slab) sharding along axis 0 (hipgp_amd/slab.py) ----------------------------
+// The op's pass sequence split at its axis-0 convolution.  Exchange layout E (plan dtype, complex):
+//   E[g][q][i][c]  g < NG: d = 2 the compact column of axis 1 (NG = L1/2 + 1, inner = 1);
+//                          d = 3 the axis-1 frequency k1 (NG = L1, inner = compact stride of axis 2)
+//                  q < nrhs, i: the axis-0 row (the rank's rows, or whole lines in CONV)
+// so the groups a rank owns after the all-to-all are one contiguous block.
+struct SlabGeom { int64_t NG, inner; };
+SlabGeom slab_geom(const hgp_plan* P, int op) {
+  const OpGeom g = op_geom(P, op);
+  if (P->d == 2) return SlabGeom{g.L[1] / 2 + 1, 1};
+  return SlabGeom{g.L[1], compact_stride(g.L[2])};
+}
+
+template <typename T>
+int slab_pass_t(hgp_plan* P, int op, int stage, const void* in, void* out, int64_t nrhs, int64_t nrows, int64_t g0,
+                int64_t ng) {
+  const OpGeom g = op_geom(P, op);
+  const int d = P->d;
+  const SlabGeom sg = slab_geom(P, op);
+  const int conv_mode = g.spec_kind == SPEC_REAL ? PASS_CONV : PASS_CONVC;
+  hipStream_t st = P->stream;
+  const size_t cs = sizeof(C2<T>);
+  auto rowt = [&](int inv, PassDesc& D, int64_t H) -> int {
+    hipError_t e = launch_rowt<T>((int)H, inv, EPI_OUT, D, st);
+    if (e == hipErrorNotSupported)
+      return fail(HGP_E_UNSUPPORTED, "row transform of H = " + std::to_string(H) + " points does not fit one CU's LDS");
+    if (e != hipSuccess) return fail(HGP_E_HIP, std::string("slab row pass: ") + hipGetErrorString(e));
+    return 0;
+  };
+  const int64_t rows_len = stage == HGP_SLAB_FWD ? g.in[0] : g.out[0];
+  if (stage != HGP_SLAB_CONV && (nrows < 1 || nrows > rows_len))
+    return fail(HGP_E_ARG, "nrows must be in [1, " + std::to_string(rows_len) + "]");
+  if (stage == HGP_SLAB_CONV && (g0 < 0 || ng < 1 || g0 + ng > sg.NG))
+    return fail(HGP_E_ARG, "groups [g0, g0 + ng) must lie in [0, " + std::to_string(sg.NG) + ")");
+  if (d == 2) {
+    const int64_t H1 = g.L[1] / 2;
+    if (stage == HGP_SLAB_FWD || stage == HGP_SLAB_INV) {
+      // the row kernels address one RHS's columns with 32-bit byte offsets from its base
+      if (sg.NG * nrhs * nrows * (int64_t)cs >= ((int64_t)1 << 31))
+        return fail(HGP_E_UNSUPPORTED, "slab too large: NG * nrhs * nrows complex values exceed 2 GiB");
+      PassDesc D = base_desc();
+      D.tw = g.tw[1].ptr; D.Q = (int)nrhs; D.Rn = (int)((nrows + 1) / 2); D.nrows = (int)nrows;
+      if (stage == HGP_SLAB_FWD) {
+        D.in = View{const_cast<void*>(in), nrows * g.in[1], g.in[1], 1, (int)g.in[1]};
+        D.out = View{out, nrows, nrhs * nrows, 1, 0};
+        return rowt(0, D, H1);
+      }
+      D.in = View{const_cast<void*>(in), nrows, nrhs * nrows, 1, 0};
+      D.out = View{out, nrows * g.out[1], g.out[1], 1, (int)g.out[1]};
+      return rowt(1, D, H1);
+    }
+    if (stage != HGP_SLAB_CONV) return fail(HGP_E_ARG, "bad slab stage");
+    const int64_t P0 = std::max(g.in[0], g.out[0]);
+    PassDesc Bd = base_desc();
+    Bd.in = View{const_cast<void*>(in), P0, nrhs * P0, 1, (int)g.in[0]};
+    Bd.out = View{out, P0, nrhs * P0, 1, (int)g.out[0]};
+    const size_t se = g.spec_kind == SPEC_REAL ? sizeof(T) : cs;
+    Bd.spec = static_cast<const char*>(g.spec) + (size_t)(g0 * g.L[0]) * se;
+    Bd.spec_kind = g.spec_kind; Bd.spec_i = 0; Bd.spec_p = 1; Bd.spec_r = g.L[0];
+    Bd.tw = g.tw[0].ptr; Bd.Q = (int)nrhs; Bd.Rn = (int)ng; Bd.In = 1;
+    return launch<T>((int)(g.L[0] / 2), conv_mode, LAY_CONTIG, Bd, nrhs * ng, st);
+  }
+  // d = 3
+  const int64_t Sl = sg.inner, L1 = g.L[1], H2 = g.L[2] / 2;
+  if (stage == HGP_SLAB_FWD || stage == HGP_SLAB_INV) {
+    const int64_t r1 = stage == HGP_SLAB_FWD ? g.in[1] : g.out[1];
+    const int64_t wsz = nrhs * nrows * r1 * Sl;
+    if (L1 * nrhs * nrows * Sl >= ((int64_t)1 << 31) || wsz >= ((int64_t)1 << 31))
+      return fail(HGP_E_UNSUPPORTED, "slab too large for 32-bit element offsets");
+    HGP_TRY(P->ws1.ensure((size_t)wsz * cs));
+    C2<T>* w1 = reinterpret_cast<C2<T>*>(P->ws1.ptr);
+    if (stage == HGP_SLAB_FWD) {
+      PassDesc P1 = base_desc();   // axis 2: real row pairs -> w1 [q][i][i1][c2]
+      P1.in = View{const_cast<void*>(in), nrows * g.in[1] * g.in[2], g.in[2], 1, (int)g.in[2]};
+      P1.out = View{w1, nrows * r1 * Sl, Sl, 1, 0};
+      P1.tw = g.tw[2].ptr; P1.Q = (int)nrhs; P1.Rn = (int)((nrows * r1 + 1) / 2); P1.nrows = (int)(nrows * r1);
+      HGP_TRY(launch<T>((int)H2, PASS_FWD, LAY_RP, P1, nrhs * P1.Rn, st));
+      PassDesc P2 = base_desc();   // axis 1 (strided): w1 -> E [k1][q][i][c2]
+      P2.in = View{w1, nrows * r1 * Sl, r1 * Sl, Sl, (int)r1};
+      P2.out = View{out, nrows * Sl, Sl, nrhs * nrows * Sl, (int)L1};
+      P2.tw = g.tw[1].ptr; P2.Q = (int)nrhs; P2.Rn = (int)nrows; P2.In = (int)(H2 + 1);
+      return launch<T>((int)(L1 / 2), PASS_FWD, LAY_STRIDED, P2, 0, st);
+    }
+    PassDesc P4 = base_desc();     // axis 1 inverse (strided): E [k1][q][o][c2] -> w1 [q][o][o1][c2]
+    P4.in = View{const_cast<void*>(in), nrows * Sl, Sl, nrhs * nrows * Sl, (int)L1};
+    P4.out = View{w1, nrows * r1 * Sl, r1 * Sl, Sl, (int)r1};
+    P4.tw = g.tw[1].ptr; P4.Q = (int)nrhs; P4.Rn = (int)nrows; P4.In = (int)(H2 + 1);
+    HGP_TRY(launch<T>((int)(L1 / 2), PASS_INV, LAY_STRIDED, P4, 0, st));
+    PassDesc P5 = base_desc();     // axis 2 inverse: w1 -> real rows (crop)
+    P5.in = View{w1, nrows * r1 * Sl, Sl, 1, (int)g.L[2]};
+    P5.out = View{out, nrows * r1 * g.out[2], g.out[2], 1, (int)g.out[2]};
+    P5.tw = g.tw[2].ptr; P5.Q = (int)nrhs; P5.Rn = (int)((nrows * r1 + 1) / 2); P5.nrows = (int)(nrows * r1);
+    return launch<T>((int)H2, PASS_INV, LAY_RP, P5, nrhs * P5.Rn, st);
+  }
+  if (stage != HGP_SLAB_CONV) return fail(HGP_E_ARG, "bad slab stage");
+  const int64_t P0 = std::max(g.in[0], g.out[0]);
+  if (ng * nrhs * P0 * Sl >= ((int64_t)1 << 31)) return fail(HGP_E_UNSUPPORTED, "slab too large for 32-bit element offsets");
+  PassDesc P3 = base_desc();       // axis 0 conv (strided over i), lines (k1, c2) of each RHS
+  P3.in = View{const_cast<void*>(in), P0 * Sl, nrhs * P0 * Sl, Sl, (int)g.in[0]};
+  P3.out = View{out, P0 * Sl, nrhs * P0 * Sl, Sl, (int)g.out[0]};
+  const size_t se = g.spec_kind == SPEC_REAL ? sizeof(T) : cs;
+  P3.spec = static_cast<const char*>(g.spec) + (size_t)(g0 * Sl) * se;
+  P3.spec_kind = g.spec_kind; P3.spec_i = 1; P3.spec_r = Sl; P3.spec_p = L1 * Sl;
+  P3.tw = g.tw[0].ptr; P3.Q = (int)nrhs; P3.Rn = (int)ng; P3.In = (int)(H2 + 1);
+  return launch<T>((int)(g.L[0] / 2), conv_mode, LAY_STRIDED, P3, 0, st);
+}
+
 // ---- PCG -------------------------------------------------------------------------------------
 int rn_last(const hgp_plan* P) {
   if (P->d == 1) return 1;
@@ -1179,6 +1286,30 @@ int hgp_plan_dqf(hgp_plan* plan, const void* left, const void* right, int64_t nv
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(plan->stream));
   return 0;
+}
+
+int hgp_slab_info(const hgp_plan* plan, int op, int64_t* ngroups, int64_t* inner) {
+  HGP_TRY(check_plan(plan));
+  if (op < HGP_OP_K || op > HGP_OP_R) return fail(HGP_E_ARG, "bad op");
+  if (plan->d < 2) return fail(HGP_E_UNSUPPORTED, "slab sharding needs a 2-D or 3-D grid");
+  const SlabGeom g = slab_geom(plan, op);
+  if (ngroups) *ngroups = g.NG;
+  if (inner) *inner = g.inner;
+  return 0;
+}
+
+int hgp_slab_pass(hgp_plan* plan, int op, int stage, const void* in, void* out, int64_t nrhs, int64_t nrows,
+                  int64_t g0, int64_t ng) {
+  HGP_TRY(check_plan(plan));
+  if (!plan->have_spec) return fail(HGP_E_STATE, "hgp_plan_set_column has not been called");
+  if (op < HGP_OP_K || op > HGP_OP_R) return fail(HGP_E_ARG, "bad op");
+  if (plan->d < 2) return fail(HGP_E_UNSUPPORTED, "slab sharding needs a 2-D or 3-D grid");
+  if (stage < HGP_SLAB_FWD || stage > HGP_SLAB_INV) return fail(HGP_E_ARG, "bad slab stage");
+  if (nrhs < 0 || (nrhs > 0 && (in == nullptr || out == nullptr))) return fail(HGP_E_ARG, "bad in/out/nrhs");
+  if (stage != HGP_SLAB_CONV && in == out) return fail(HGP_E_ARG, "in and out must not alias (row stages)");
+  if (nrhs == 0) return 0;
+  HGP_TRY(use_device(plan));
+  return DISPATCH(plan, slab_pass_t, plan, op, stage, in, out, nrhs, nrows, g0, ng);
 }
 
 int hgp_plan_info(const hgp_plan* plan, int64_t* M, int64_t* Mprime, int64_t* L_K, int64_t* L_R) {

@@ -111,6 +111,24 @@ int hgp_pcg_set_done(hgp_plan* plan, const int* flag);
  * that did (host int; synchronises the plan's stream). */
 int hgp_pcg_iters(hgp_plan* plan, int* iters);
 
+/* Grid-block (slab) sharding along axis 0 (row e2: a 2-D / 3-D grid's axis-0 rows split over
+ * ranks; hipgp_amd/slab.py drives it).  Each op is its pass sequence split at the axis-0
+ * convolution, which needs whole axis-0 lines and so runs between two all-to-all transposes.
+ * Exchange layout E (plan dtype, interleaved complex): E[g][q][i][c]
+ *   d = 2: g < NG = L1/2 + 1 compact axis-1 columns, inner = 1;
+ *   d = 3: g < NG = L1 axis-1 frequencies, c < inner = the compact half-spectrum pitch of axis 2;
+ *   q < nrhs; i = axis-0 row (a rank's rows in FWD / INV, whole lines in CONV).
+ * stage HGP_SLAB_FWD : x (nrhs, nrows, rest of the input row) real -> E over this rank's nrows
+ *                      input rows (all NG groups)                 toeplitz_tensor.py:79,94,109,122
+ * stage HGP_SLAB_CONV: E lines [ng][nrhs][P0][inner], P0 = max(in0, out0) rows per line, groups
+ *                      [g0, g0 + ng) of the op's spectrum; in place allowed  (:80-82 etc.)
+ * stage HGP_SLAB_INV : E over this rank's nrows output rows -> y (nrhs, nrows, rest) real, crop
+ * Partial dot products / PCG scalars are the caller's (all-reduced over ranks). */
+enum { HGP_SLAB_FWD = 0, HGP_SLAB_CONV = 1, HGP_SLAB_INV = 2 };
+int hgp_slab_info(const hgp_plan* plan, int op, int64_t* ngroups, int64_t* inner);
+int hgp_slab_pass(hgp_plan* plan, int op, int stage, const void* in, void* out, int64_t nrhs,
+                  int64_t nrows, int64_t g0, int64_t ng);
+
 /* The clamped spectrum D (which=HGP_SPEC_D), sqrt(D) or 1/D on the full expanded grid
  * (device, M' reals) — the real parts of ToeplitzTensor.D / D_sqrt / Di
  * (toeplitz_tensor.py:28-31). */

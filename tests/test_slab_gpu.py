@@ -1,0 +1,89 @@
+"""Grid-block (slab) sharding (row e2) on the GPU: a same-device rehearsal -- 2 processes on
+cuda:0, gloo for the all-to-all transposes and the CG dot all-reduces (RCCL on a multi-GPU
+node) -- of SlabToeplitz on libhipgp's hgp_slab_pass stages.  The gathered K, C^-1, R^T, R and
+the slab PCG / compute_kn agree with the single-rank plan to rounding (fp64 1e-11 on the ops;
+fp32 within FFT rounding); the slab PCG runs the conj_grad2 recurrence with all-reduced
+dots, the single-rank plan the fused device PCG."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from oracle import ziggy_oracle as zo
+
+pytestmark = pytest.mark.gpu
+
+CASES = {"2d_f64": ((64, 48), torch.float64), "2d_C2_f32": ((1024, 1024), torch.float32),
+         "3d_f64": ((16, 12, 10), torch.float64), "3d_f32": ((128, 96, 64), torch.float32),
+         "2d_odd_f64": ((33, 40), torch.float64)}
+
+
+def _column(dims):
+    grids = [np.linspace(-1, 1, m) for m in dims]
+    return zo.toeplitz_column(grids, lambda x, y: zo.kernel_eval("matern", x, y, (1., .1), nu=1.5), 0.05)
+
+
+def _worker(rank, ws, port, case, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        torch.cuda.set_device(0)
+        from hipgp_amd import _lib
+        from hipgp_amd.slab import slab_toeplitz
+        dims, dt = CASES[case]
+        col = torch.tensor(_column(dims), device="cuda", dtype=dt)
+        S = slab_toeplitz(dims, col, dtype=dt, device="cuda")
+        M = int(np.prod(dims))
+        Mp = int(np.prod([2 * m - 2 for m in dims]))
+        g = torch.Generator(device="cuda").manual_seed(9)
+        v = torch.randn(3, M, device="cuda", generator=g, dtype=torch.float64).to(dt)
+        w = torch.randn(3, Mp, device="cuda", generator=g, dtype=torch.float64).to(dt)
+        res = {}
+        for name, op, x, grid in (("K", _lib.OP_K, v, "m"), ("Cinv", _lib.OP_CINV, v, "m"),
+                                  ("RT", _lib.OP_RT, v, "m"), ("R", _lib.OP_R, w, "n")):
+            res[name] = S.apply(op, S.scatter_rows(x, grid)).double().cpu().numpy()
+        x, it = S.pcg(S.scatter_rows(v), maxiter=10, tol=1e-30)
+        res["pcg"] = x.double().cpu().numpy()
+        res["kn"] = S.compute_kn(S.scatter_rows(v), maxiter=10, tol=1e-30).double().cpu().numpy()
+        torch.cuda.synchronize()
+        out[rank] = res
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_slab_two_ranks_same_device(case):
+    from hipgp_amd import _lib
+    from hipgp_amd.plan import ToeplitzPlan
+    dims, dt = CASES[case]
+    mgr = mp.Manager()
+    out = mgr.dict()
+    port = 29650 + os.getpid() % 100 + len(case)
+    mp.spawn(_worker, args=(2, port, case, out), nprocs=2, join=True)
+    assert len(out) == 2
+    P = ToeplitzPlan(dims, dt, "cuda")
+    P.set_column(torch.tensor(_column(dims), device="cuda", dtype=dt))
+    M = int(np.prod(dims))
+    Mp = int(np.prod([2 * m - 2 for m in dims]))
+    g = torch.Generator(device="cuda").manual_seed(9)
+    v = torch.randn(3, M, device="cuda", generator=g, dtype=torch.float64).to(dt)
+    w = torch.randn(3, Mp, device="cuda", generator=g, dtype=torch.float64).to(dt)
+    gat = lambda k: np.concatenate([out[0][k], out[1][k]], axis=1)
+    tol_op = 1e-11 if dt == torch.float64 else 2e-5
+    for name, op, x in (("K", _lib.OP_K, v), ("Cinv", _lib.OP_CINV, v), ("RT", _lib.OP_RT, v), ("R", _lib.OP_R, w)):
+        ref = P.apply(op, x).double().cpu().numpy()
+        got = gat(name)
+        assert got.shape == ref.shape, name
+        err = float(np.max(np.abs(got - ref)) / np.max(np.abs(ref)))
+        assert err < tol_op, (name, err)
+    xr = P.pcg(v, 10, 1e-30, precond=True).double().cpu().numpy()
+    tol_pcg = 1e-9 if dt == torch.float64 else 1e-4
+    err = float(np.linalg.norm(gat("pcg") - xr) / np.linalg.norm(xr))
+    assert err < tol_pcg, err
+    kn = P.apply(_lib.OP_RT, P.pcg(v, 10, 1e-30, precond=True)).double().cpu().numpy()
+    err = float(np.linalg.norm(gat("kn") - kn) / np.linalg.norm(kn))
+    assert err < tol_pcg, err
