@@ -262,3 +262,30 @@ def test_large_grid_fp32_vs_fp64(m):
     for name, a, b, tol in zip(("K", "Cinv", "RT"), outs[torch.float32], outs[torch.float64], (2e-5, 2e-3, 1e-4)):
         err = float((a - b).abs().max() / b.abs().max())
         assert err < tol, (name, err)
+
+
+@pytest.mark.parametrize("dims,dtype", [((1025, 8), torch.float64), ((2048, 8), torch.float64), ((4096, 8), torch.float64),
+                                        ((8, 2048), torch.float64), ((600, 600), torch.float64),
+                                        ((2048, 2048), torch.float32), ((1024, 1024), torch.float32)],
+                         ids=["1025x8_f64", "2048x8_f64", "4096x8_f64", "8x2048_f64", "600x600_f64", "C3_f32", "C2_f32"])
+def test_long_lines_accuracy_and_repeatability(dims, dtype):
+    """Contiguous-line passes with lines of several waves (axis-0 columns of 2048 / 4096 points,
+    fp64 setup DCTs along long rows): fp64 ops at fp64 accuracy against the oracle, and every op
+    bitwise identical from run to run (a race once showed as 1e-8 run-to-run noise in fp64)."""
+    from hipgp_amd import _lib
+    from hipgp_amd.plan import ToeplitzPlan
+    grids = [np.linspace(-1, 1, m) for m in dims]
+    col = zo.toeplitz_column(grids, lambda x, y: zo.kernel_eval("matern", x, y, (1., .1), nu=1.5), 0.1)
+    P = ToeplitzPlan(dims, dtype, DEV)
+    P.set_column(torch.tensor(col, device=DEV, dtype=dtype))
+    v = np.random.RandomState(0).randn(4, int(np.prod(dims)))
+    vt = torch.tensor(v, device=DEV, dtype=dtype)
+    for op in (_lib.OP_K, _lib.OP_CINV, _lib.OP_RT):
+        ys = [P.apply(op, vt) for _ in range(4)]
+        for y in ys[1:]:
+            assert torch.equal(y, ys[0]), op
+    if dtype == torch.float64 and np.prod(dims) < 5e6:
+        T = zo.ToeplitzOracle(col, dims)
+        assert rel_err(P.spectrum(_lib.SPEC_D).cpu().numpy(), T.D) < 1e-12
+        for op, ref in ((_lib.OP_K, T.matmul_K(v)), (_lib.OP_RT, T.matmul_RT(v))):
+            assert rel_err(_np(P.apply(op, vt)), ref) < 1e-11, op
