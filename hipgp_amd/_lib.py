@@ -29,7 +29,7 @@ EXPORTS = (
     "hgp_kuf_semi_mc", "hgp_kuf_semi_sqexp", "hgp_knn_doubly_diag", "hgp_meanfield_stats",
     "hgp_block_stats", "hgp_sym_toeplitz_dqf", "hgp_plan_column_grad",
     "hgp_plan_dqf", "hgp_pcg_local_flag", "hgp_pcg_set_done", "hgp_pcg_iters",
-    "hgp_slab_info", "hgp_slab_pass",
+    "hgp_slab_info", "hgp_slab_pass", "hgp_plan_mem", "hgp_plan_trim",
 )
 KERN_SQEXP, KERN_MATERN12, KERN_MATERN32, KERN_MATERN52, KERN_GNEITING = 0, 1, 2, 3, 4
 
@@ -81,6 +81,8 @@ def lib():
         "hgp_pcg_set_done": (i32, [vp, vp]),
         "hgp_pcg_iters": (i32, [vp, pi32]),
         "hgp_slab_info": (i32, [vp, i32, pi64, pi64]),
+        "hgp_plan_mem": (i32, [vp, pi64, pi64]),
+        "hgp_plan_trim": (i32, [vp]),
         "hgp_slab_pass": (i32, [vp, i32, i32, vp, vp, i64, i64, i64, i64]),
     }
     for name, (res, args) in sig.items():

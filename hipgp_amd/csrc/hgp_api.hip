@@ -231,16 +231,21 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
   const int64_t Sl = compact_stride(g.L[d - 1]);
   // per-RHS workspace (complex elements)
   int64_t B1 = 0, B2 = 0;
-  // 2-D: column-major intermediate W[q][c][i0], c < H1 + 1, column pitch S0 (hgp_rows.hpp)
+  // 2-D: column-major intermediate W[q][c][i0], c < H1 + 1, column pitch S0 (hgp_rows.hpp);
+  // rows whose row-pair kernels do not fit one CU's LDS (fp64 H >= 8192) take the generic
+  // sequence instead: row pairs -> row-major [q][i0][c] -> strided axis-0 conv -> row pairs
+  const bool gen2 = d == 2 && !rowt_fits<T>((int)(g.L[1] / 2));
   const int64_t S0 = (d == 2) ? round_up(std::max(g.in[0], g.out[0]), 16) : 0;
-  if (d == 2) B1 = (g.L[1] / 2 + 1) * S0;
+  if (d == 2) B1 = gen2 ? std::max(g.in[0], g.out[0]) * Sl : (g.L[1] / 2 + 1) * S0;
+  if (gen2 && (spart != nullptr || epi != nullptr || mid != nullptr))
+    return fail(HGP_E_ARG, "internal: the generic 2-D sequence has no fused PCG epilogue");
   if (d == 3) {
     B1 = std::max(g.in[0] * g.in[1], g.out[0] * g.out[1]) * Sl;
     B2 = std::max(g.in[0], g.out[0]) * g.L[1] * Sl;
   }
   // the 2-D row passes address one RHS's intermediate slab (and the contiguous pass one line)
   // with 32-bit byte offsets from a scalar base (raw buffer accesses, hgp_rows.hpp)
-  if (d == 2 && B1 * (int64_t)cs >= ((int64_t)1 << 31))
+  if (d == 2 && !gen2 && B1 * (int64_t)cs >= ((int64_t)1 << 31))
     return fail(HGP_E_UNSUPPORTED, "2-D grid too large: one right-hand side's intermediate exceeds 2 GiB");
   // RHS chunks: 2-D ops spread them over NS streams, chunk j on stream (and workspace slot)
   // j % NS; each chunk's RHS are processed entirely on its stream (no cross-stream data).
@@ -298,6 +303,26 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
       D.spec = g.spec; D.spec_kind = g.spec_kind; D.spec_i = 0; D.spec_r = 0; D.spec_p = 1;
       D.tw = g.tw[0].ptr; D.Q = qn; D.Rn = 1; D.In = 1; D.done = done;
       HGP_TRY(run((int)(g.L[0] / 2), conv_mode, LAY_R1, D, qn));
+    } else if (d == 2 && gen2) {
+      C2<T>* w1 = reinterpret_cast<C2<T>*>(P->ws1.ptr) + (int64_t)slot * Qc * B1;
+      const int64_t H1 = g.L[1] / 2;
+      PassDesc A = base_desc();     // FWD axis 1: row pairs -> w1 [q][i0][c1] (pitch Sl)
+      A.in = View{(void*)xi, g.in_M, g.in[1], 1, (int)g.in[1]};
+      A.out = View{w1, B1, Sl, 1, 0};
+      A.tw = g.tw[1].ptr; A.Q = qn; A.Rn = (int)((g.in[0] + 1) / 2); A.nrows = (int)g.in[0]; A.done = done;
+      HGP_TRY(run((int)H1, PASS_FWD, LAY_RP, A, (int64_t)qn * A.Rn));
+      PassDesc Bd = base_desc();    // CONV axis 0 (strided, in place): lines c1, spectrum [c1][k0]
+      Bd.in = View{w1, B1, 0, Sl, (int)g.in[0]};
+      Bd.out = View{w1, B1, 0, Sl, (int)g.out[0]};
+      Bd.spec = g.spec; Bd.spec_kind = g.spec_kind; Bd.spec_i = g.L[0]; Bd.spec_r = 0; Bd.spec_p = 1;
+      Bd.tw = g.tw[0].ptr; Bd.Q = qn; Bd.Rn = 1; Bd.In = (int)(H1 + 1); Bd.done = done;
+      HGP_TRY(run((int)(g.L[0] / 2), conv_mode, LAY_STRIDED, Bd, 0));
+      PassDesc Cd = base_desc();    // INV axis 1: rebuild row pairs, crop, fused dot
+      Cd.in = View{w1, B1, Sl, 1, (int)g.L[1]};
+      Cd.out = View{yo, g.out_M, g.out[1], 1, (int)g.out[1]};
+      Cd.dot = dvc; Cd.partial = pc;
+      Cd.tw = g.tw[1].ptr; Cd.Q = qn; Cd.Rn = (int)((g.out[0] + 1) / 2); Cd.nrows = (int)g.out[0]; Cd.done = done;
+      HGP_TRY(run((int)H1, PASS_INV, LAY_RP, Cd, (int64_t)qn * Cd.Rn));
     } else if (d == 2) {
       C2<T>* w1 = reinterpret_cast<C2<T>*>(P->ws1.ptr) + (int64_t)slot * Qc * B1;
       const int64_t H1 = g.L[1] / 2;
@@ -693,6 +718,9 @@ int rn_last(const hgp_plan* P) {
 // sums over the (RHS, compact column) lines, L_1/2 + 1 partials per RHS; r.r from the fused
 // x/r update, one partial per row block of the row-inverse pass.
 int spec_np(const hgp_plan* P) { return (int)(P->LK[1] / 2 + 1); }
+// the fused 2-D PCG needs the row-pair kernels of the K / C^-1 rows
+template <typename T>
+bool fused2d(const hgp_plan* P) { return P->d == 2 && rowt_fits<T>((int)(P->LK[1] / 2)) != 0; }
 template <typename T>
 int xr_np(const hgp_plan* P) {
   const int pairs = rowt_pairs<T>((int)(P->LK[1] / 2));
@@ -708,7 +736,7 @@ int pcg_begin_t(hgp_plan* P, const void* b, void* x, int64_t nrhs, int use_preco
   HGP_TRY(P->z.ensure(vb));
   HGP_TRY(P->p.ensure(vb));
   HGP_TRY(P->Ap.ensure(vb));
-  const bool fused = P->d == 2;
+  const bool fused = fused2d<T>(P);
   const int npo = fused ? std::max(rn_last(P), spec_np(P)) : rn_last(P);
   const int npu = fused ? std::max(update_np(M), xr_np<T>(P)) : update_np(M);
   HGP_TRY(P->part_op.ensure((size_t)(nrhs * npo) * sizeof(T)));
@@ -765,7 +793,7 @@ int pcg_step_t(hgp_plan* P, double tol) {
   T* alpha = sc + nrhs;
   T* beta = sc + 2 * nrhs;
   T* rnew = sc + 3 * nrhs;
-  if (P->d == 2) {
+  if (fused2d<T>(P)) {
     // Fused 2-D iteration.  K p: the column pass leaves the spectral p.Ap partials, alpha is
     // formed per RHS chunk before the row-inverse pass, whose epilogue does x += alpha p,
     // r -= alpha Ap (+ r.r partials) with Ap never stored.  Then the break test; then C^-1 r,
@@ -1145,7 +1173,6 @@ int hgp_meanfield_stats(int dtype, const void* kn, int64_t nrhs, int64_t Mp, con
                         void* dm, void* hip_stream) {
   if (dtype != HGP_F32 && dtype != HGP_F64) return fail(HGP_E_ARG, "dtype must be HGP_F32 or HGP_F64");
   if (nrhs < 0 || Mp <= 0) return fail(HGP_E_ARG, "nrhs >= 0 and Mp > 0 required");
-  if (nrhs > 65535) return fail(HGP_E_ARG, "nrhs must be <= 65535 (grid y dimension)");
   if (kn == nullptr || qm == nullptr || qS == nullptr || lam == nullptr || dm == nullptr ||
       (nrhs > 0 && (y == nullptr || ivar == nullptr || Knn_diag == nullptr || log_sd == nullptr || an == nullptr)))
     return fail(HGP_E_ARG, "null pointer");
@@ -1320,6 +1347,42 @@ int hgp_plan_info(const hgp_plan* plan, int64_t* M, int64_t* Mprime, int64_t* L_
     if (L_K) L_K[a] = a < plan->d ? plan->LK[a] : 1;
     if (L_R) L_R[a] = a < plan->d ? plan->LR[a] : 1;
   }
+  return 0;
+}
+
+int64_t plan_scratch_bytes(const hgp_plan* P) {
+  const DevBuf* bufs[] = {&P->ws1, &P->ws2, &P->set1, &P->set2, &P->setM1, &P->setM2, &P->setC, &P->r, &P->z,
+                          &P->p, &P->Ap, &P->part_op, &P->part_u, &P->scal, &P->bT, &P->xT};
+  int64_t b = 0;
+  for (const DevBuf* d : bufs) b += (int64_t)d->bytes;
+  return b;
+}
+
+int hgp_plan_mem(const hgp_plan* plan, int64_t* scratch_bytes, int64_t* table_bytes) {
+  HGP_TRY(check_plan(plan));
+  if (scratch_bytes) *scratch_bytes = plan_scratch_bytes(plan);
+  if (table_bytes) {
+    int64_t b = 0;
+    for (int a = 0; a < 3; ++a)
+      b += (int64_t)(plan->twK[a].bytes + plan->twR[a].bytes + plan->tw64K[a].bytes + plan->tw64R[a].bytes +
+                     plan->bsPre[a].bytes + plan->bsPost[a].bytes + plan->bsFilt[a].bytes);
+    b += (int64_t)(plan->specK.bytes + plan->specI.bytes + plan->specR.bytes + plan->Dm3.bytes);
+    *table_bytes = b;
+  }
+  return 0;
+}
+
+int hgp_plan_trim(hgp_plan* plan) {
+  HGP_TRY(check_plan(plan));
+  if (plan->cg_active) plan->cg_active = false;   // the CG state goes with its buffers
+  HGP_TRY(use_device(plan));
+  HIP_TRY(hipStreamSynchronize(plan->stream));     // no kernel may still use them
+  for (int i = 0; i < 3; ++i)
+    if (plan->side[i]) HIP_TRY(hipStreamSynchronize(plan->side[i]));
+  DevBuf* bufs[] = {&plan->ws1, &plan->ws2, &plan->set1, &plan->set2, &plan->setM1, &plan->setM2, &plan->setC,
+                    &plan->r, &plan->z, &plan->p, &plan->Ap, &plan->part_op, &plan->part_u, &plan->scal,
+                    &plan->bT, &plan->xT};
+  for (DevBuf* b : bufs) b->release();
   return 0;
 }
 

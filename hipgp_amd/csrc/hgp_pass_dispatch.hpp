@@ -104,6 +104,15 @@ static hipError_t launch_rowt_h(int inv, int epi, const PassDesc& d, hipStream_t
 template <typename T, int H>
 static int rowt_pairs_h() { return RowTCfg<T, H>::C; }
 
+template <typename T, int H>
+static int rowt_fits_h() { return RowTCfg<T, H>::LDS <= LDS_CAP ? 1 : 0; }
+
+template <typename T>
+int rowt_fits(int H) {
+  HGP_H_SWITCH(rowt_fits_h)
+  return 0;
+}
+
 template <typename T>
 hipError_t launch_rowt(int H, int inv, int epi, const PassDesc& d, hipStream_t s) {
   HGP_H_SWITCH(launch_rowt_h, inv, epi, d, s)

@@ -4,4 +4,5 @@ template hipError_t launch_pass<float>(int, int, int, const PassDesc&, int64_t, 
 template PassGeom pass_geom<float>(int, int);
 template hipError_t launch_rowt<float>(int, int, int, const PassDesc&, hipStream_t);
 template int rowt_pairs<float>(int);
+template int rowt_fits<float>(int);
 }

@@ -117,8 +117,12 @@ hipError_t meanfield_stats_t(const void* kn, int64_t nrhs, int64_t Mp, const voi
   if (e != hipSuccess) return e;
   T* part = scratch;
   T* bdiff = scratch + nrhs * np * 3;
-  hipLaunchKernelGGL((k_stats_rows<T>), dim3((unsigned)np, (unsigned)nrhs), dim3(ST_THREADS), 0, s,
-                     (const T*)kn, (const T*)qm, (const T*)qS, Mp, np, part);
+  // grid.y is the RHS: chunks of at most 65535 (the y-dimension limit), any batch size
+  for (int64_t b0 = 0; b0 < nrhs; b0 += 65535) {
+    const int64_t nb0 = std::min<int64_t>(65535, nrhs - b0);
+    hipLaunchKernelGGL((k_stats_rows<T>), dim3((unsigned)np, (unsigned)nb0), dim3(ST_THREADS), 0, s,
+                       (const T*)kn + b0 * Mp, (const T*)qm, (const T*)qS, Mp, np, part + b0 * np * 3);
+  }
   hipLaunchKernelGGL((k_stats_finish<T>), dim3((unsigned)((nrhs + 3) / 4)), dim3(256), 0, s, (const T*)part, np,
                      (int)nrhs, (const T*)y, (const T*)iv, (const T*)knn, (const T*)lsd, (T*)an, bdiff);
   const int64_t nb = (Mp + ST_THREADS * 4 - 1) / (ST_THREADS * 4);

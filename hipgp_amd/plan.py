@@ -4,6 +4,7 @@ Thin: it turns torch tensors into device pointers and calls the C ABI on torch's
 stream.  All arithmetic runs in the HIP kernels of libhipgp.so.
 """
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -19,9 +20,33 @@ def expanded_dims(dims):
 
 # Idle C plans by (dims, dtype, device): the reference builds a fresh ToeplitzTensor on every
 # compute_kn call (`hipgp.py:143`); re-using an idle plan of the same grid keeps its twiddle /
-# DCT tables and HBM workspaces, so only the spectrum is recomputed (hgp_plan_set_column).
+# DCT tables, so only the spectrum is recomputed (hgp_plan_set_column).  Idle plans also keep
+# their scratch (workspaces, CG vectors: the next solve needs the same sizes) while all idle
+# scratch stays under HGP_POOL_MB (default 6 GiB of the 288 GB); beyond that a plan is trimmed to its
+# tables when it goes idle (hgp_plan_trim).  release_pool() frees every idle plan, e.g. before
+# a large torch allocation (this memory is outside torch's caching allocator).
 _POOL = {}
 _POOL_MAX = 2
+_POOL_BYTES = int(os.environ.get("HGP_POOL_MB", "6144")) << 20
+
+
+def _scratch_bytes(h):
+    b = ctypes.c_int64(0)
+    lib().hgp_plan_mem(h, ctypes.byref(b), None)
+    return b.value
+
+
+def pool_scratch_bytes():
+    """Device bytes of scratch held by idle pooled plans."""
+    return sum(_scratch_bytes(h) for hs in _POOL.values() for h in hs)
+
+
+def release_pool():
+    """Destroy every idle pooled plan (their device memory is outside torch's allocator)."""
+    for hs in _POOL.values():
+        for h in hs:
+            lib().hgp_plan_destroy(h)
+    _POOL.clear()
 
 
 class ToeplitzPlan:
@@ -227,6 +252,8 @@ class ToeplitzPlan:
             try:
                 idle = _POOL.setdefault(self._key, [])
                 if len(idle) < _POOL_MAX:
+                    if pool_scratch_bytes() + _scratch_bytes(h) > _POOL_BYTES:
+                        lib().hgp_plan_trim(h)
                     idle.append(h)          # stream-ordered re-use (see _POOL)
                 else:
                     lib().hgp_plan_destroy(h)

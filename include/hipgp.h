@@ -232,6 +232,12 @@ int hgp_plan_column_grad(hgp_plan* plan, int op, const void* x, const void* g, i
 int hgp_plan_info(const hgp_plan* plan, int64_t* M, int64_t* Mprime, int64_t* L_K,
                   int64_t* L_R);
 
+/* Device memory a plan holds: scratch (operator workspaces, CG vectors, set-up scratch; all
+ * re-allocated on demand) and tables (twiddles, Bluestein DCT tables, spectra).
+ * hgp_plan_trim frees the scratch (after synchronising the plan's streams) and keeps the tables,
+ * so an idle plan kept for re-use holds only what its next set-up needs. */
+int hgp_plan_mem(const hgp_plan* plan, int64_t* scratch_bytes, int64_t* table_bytes);
+int hgp_plan_trim(hgp_plan* plan);
 int hgp_plan_destroy(hgp_plan* plan);
 
 const char* hgp_last_error(void);

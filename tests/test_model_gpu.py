@@ -126,3 +126,66 @@ def test_meanfield_stats_kernel(dtype, per_obs_noise):
     assert abs(float(st["an_sum"] - an.sum())) <= tol * float(an.abs().sum())
     assert rel_err(st["lam_sum"].cpu().numpy(), lam.cpu().numpy()) < tol
     assert rel_err(st["dm_sum"].cpu().numpy(), dm.cpu().numpy()) < tol
+
+
+def test_meanfield_stats_large_batch():
+    """hgp_meanfield_stats with more than 65535 observations (a full-batch elbo_and_grad): the
+    row statistics run in RHS chunks of the grid's y-dimension limit; against torch."""
+    from hipgp_amd import _lib
+    import ctypes
+    B, Mp = 70000, 37
+    g = torch.Generator(device=DEV).manual_seed(3)
+    kn = torch.randn(B, Mp, device=DEV, generator=g, dtype=torch.float64) * .1
+    qm = torch.randn(Mp, device=DEV, generator=g, dtype=torch.float64)
+    qS = torch.rand(Mp, device=DEV, generator=g, dtype=torch.float64)
+    y = torch.randn(B, device=DEV, generator=g, dtype=torch.float64)
+    iv = torch.rand(B, device=DEV, generator=g, dtype=torch.float64) + .5
+    knn = torch.rand(B, device=DEV, generator=g, dtype=torch.float64) + 1
+    lsd = torch.randn(B, device=DEV, generator=g, dtype=torch.float64) * .1
+    an = torch.empty(B, device=DEV, dtype=torch.float64)
+    lam = torch.empty(Mp, device=DEV, dtype=torch.float64)
+    dm = torch.empty(Mp, device=DEV, dtype=torch.float64)
+    p = lambda t: ctypes.c_void_p(t.data_ptr())
+    _lib.check(_lib.lib().hgp_meanfield_stats(_lib.HGP_F64, p(kn), B, Mp, p(qm), p(qS), p(y), p(iv), p(knn), p(lsd),
+                                              p(an), p(lam), p(dm), _lib.stream_ptr(kn.device)))
+    knm = kn @ qm
+    an_ref = -0.5 * iv * ((knm - y) ** 2 + knn - (kn * kn).sum(1) + (kn * kn) @ qS) - lsd - 0.5 * np.log(2 * np.pi)
+    assert float((an - an_ref).abs().max()) < 1e-10
+    assert float((lam - (iv[:, None] * kn * kn).sum(0)).abs().max()) < 1e-9
+    assert float((dm + ((iv * (knm - y))[:, None] * kn).sum(0)).abs().max()) < 1e-9
+
+
+def test_plan_pool_trim_and_release():
+    """Idle pooled plans trim their scratch beyond the pool budget and release_pool() frees them;
+    a trimmed plan re-allocates on demand and computes the same result."""
+    import gc
+    from hipgp_amd import plan as hp
+    from hipgp_amd import _lib
+    hp.release_pool()
+    dims = (300, 200)
+    col = torch.tensor(zo_column(dims), device=DEV)
+    v = torch.randn(3, 300 * 200, device=DEV, dtype=torch.float64)
+    P = hp.ToeplitzPlan(dims, torch.float64, DEV)
+    P.set_column(col)
+    x1 = P.pcg(v, 10, 1e-30).clone()
+    old = hp._POOL_BYTES
+    hp._POOL_BYTES = 0                      # force trimming on the way into the pool
+    try:
+        del P
+        gc.collect()
+        assert hp.pool_scratch_bytes() == 0
+        Q = hp.ToeplitzPlan(dims, torch.float64, DEV)   # the trimmed idle plan, re-used
+        Q.set_column(col)
+        assert torch.equal(Q.pcg(v, 10, 1e-30), x1)
+        del Q
+        gc.collect()
+    finally:
+        hp._POOL_BYTES = old
+    hp.release_pool()
+    assert hp.pool_scratch_bytes() == 0 and not hp._POOL
+
+
+def zo_column(dims):
+    from oracle import ziggy_oracle as zo
+    grids = [np.linspace(-1, 1, m) for m in dims]
+    return zo.toeplitz_column(grids, lambda x, y: zo.kernel_eval("matern", x, y, (1., .1), nu=1.5), 1e-2)

@@ -59,6 +59,10 @@ int main() {
   EXPECT(hgp_plan_dqf(nullptr, buf, buf, 1, buf) == HGP_E_ARG);
   EXPECT(hgp_plan_info(nullptr, i64, i64, i64, i64) == HGP_E_ARG);
   EXPECT(hgp_plan_destroy(nullptr) == 0);
+  EXPECT(hgp_plan_trim(nullptr) == HGP_E_ARG);
+  EXPECT(hgp_plan_mem(nullptr, i64, i64) == HGP_E_ARG);
+  EXPECT(hgp_slab_info(nullptr, HGP_OP_K, i64, i64) == HGP_E_ARG);
+  EXPECT(hgp_slab_pass(nullptr, HGP_OP_K, HGP_SLAB_FWD, buf, buf + 8, 1, 1, 0, 0) == HGP_E_ARG);
 
   // ---- stand-alone kernels: argument checks and empty inputs ---------------------------
   EXPECT(hgp_rowdot(HGP_F32, buf, buf, buf, 0, 16, nullptr) == 0);            // nothing to do
@@ -78,7 +82,7 @@ int main() {
   EXPECT(hgp_kuf_semi_sqexp(HGP_F64, 2, m3, grids, buf, 0, 1., 1., buf, nullptr) == 0);
   EXPECT(hgp_knn_doubly_diag(HGP_F32, 2, buf, 3, 1., 1., buf, 1, buf, nullptr) == HGP_E_ARG);
   EXPECT(hgp_knn_doubly_diag(HGP_F32, 2, buf, 0, 1., 1., buf, 50, buf, nullptr) == 0);
-  EXPECT(hgp_meanfield_stats(HGP_F32, buf, 70000, 16, buf, buf, buf, buf, buf, buf, buf, buf, buf, nullptr) ==
+  EXPECT(hgp_meanfield_stats(HGP_F32, buf, -1, 16, buf, buf, buf, buf, buf, buf, buf, buf, buf, nullptr) ==
          HGP_E_ARG);
   EXPECT(hgp_meanfield_stats(HGP_F32, buf, 2, 16, buf, nullptr, buf, buf, buf, buf, buf, buf, buf, nullptr) ==
          HGP_E_ARG);
