@@ -100,7 +100,7 @@ struct hgp_plan {
   // scratch
   DevBuf ws1, ws2, set1, set2, setM1, setM2, setC;
   // CG state
-  DevBuf r, z, p, Ap, part_op, part_u, scal, flags, bT, xT;
+  DevBuf r, z, p, Ap, part_op, part_u, part_f, scal, flags, bT, xT;
   int64_t cg_nrhs = 0;
   int cg_precond = 0, cg_layout = 0;
   void* cg_x_user = nullptr;
@@ -120,7 +120,7 @@ struct hgp_plan {
       bsPre[a].release(); bsPost[a].release(); bsFilt[a].release();
     }
     DevBuf* bufs[] = {&specK, &specI, &specR, &Dm3, &nclamp, &ws1, &ws2, &set1, &set2, &setM1, &setM2, &setC,
-                      &r, &z, &p, &Ap, &part_op, &part_u, &scal, &flags, &bT, &xT};
+                      &r, &z, &p, &Ap, &part_op, &part_u, &part_f, &scal, &flags, &bT, &xT};
     for (DevBuf* b : bufs) b->release();
     for (int i = 0; i < 3; ++i) {
       if (side[i]) (void)hipStreamDestroy(side[i]);
@@ -235,21 +235,33 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
   // rows whose row-pair kernels do not fit one CU's LDS (fp64 H >= 8192) take the generic
   // sequence instead: row pairs -> row-major [q][i0][c] -> strided axis-0 conv -> row pairs
   const bool gen2 = d == 2 && !rowt_fits<T>((int)(g.L[1] / 2));
-  const int64_t S0 = (d == 2) ? round_up(std::max(g.in[0], g.out[0]), 16) : 0;
+  const int64_t S0 = (d >= 2) ? round_up(std::max(g.in[0], g.out[0]), 16) : 0;   // axis-0 pitch
   if (d == 2) B1 = gen2 ? std::max(g.in[0], g.out[0]) * Sl : (g.L[1] / 2 + 1) * S0;
   if (gen2 && (spart != nullptr || epi != nullptr || mid != nullptr))
     return fail(HGP_E_ARG, "internal: the generic 2-D sequence has no fused PCG epilogue");
+  // 3-D (hgp_lines.hpp): the (i1, i2) plane of every (RHS, i0) goes through the 2-D row-pair
+  // kernels -> W1 [q][i0][c2][i1] (column pitch S1); transposing axis-1 line passes <->
+  // W2 [q][c2][k1][i0] (axis-0 pitch S0), whose axis-0 lines the contiguous conv pass takes.
+  // Kernels that do not fit one CU's LDS (fp64 at H >= 8192) take the row-major 5-pass
+  // sequence with strided middle passes instead (gen3).
+  const bool gen3 = d == 3 && (!rowt_fits<T>((int)(g.L[2] / 2)) || !linet_fits<T>((int)(g.L[1] / 2)));
+  const int64_t S1 = (d == 3) ? round_up(std::max(g.in[1], g.out[1]), 16) : 0;
   if (d == 3) {
-    B1 = std::max(g.in[0] * g.in[1], g.out[0] * g.out[1]) * Sl;
-    B2 = std::max(g.in[0], g.out[0]) * g.L[1] * Sl;
+    const int64_t P0 = std::max(g.in[0], g.out[0]), NC2 = g.L[2] / 2 + 1;
+    B1 = gen3 ? std::max(g.in[0] * g.in[1], g.out[0] * g.out[1]) * Sl : P0 * NC2 * S1;
+    B2 = gen3 ? P0 * g.L[1] * Sl : NC2 * g.L[1] * S0;
+    // the axis-0 / middle passes address one RHS's W2 with 32-bit element offsets
+    if (B2 >= ((int64_t)1 << 31)) return fail(HGP_E_UNSUPPORTED, "3-D grid too large: one right-hand side's intermediate exceeds 2^31 values");
   }
+  if (gen3 && (spart != nullptr || epi != nullptr || mid != nullptr))
+    return fail(HGP_E_ARG, "internal: the generic 3-D sequence has no fused PCG epilogue");
   // the 2-D row passes address one RHS's intermediate slab (and the contiguous pass one line)
   // with 32-bit byte offsets from a scalar base (raw buffer accesses, hgp_rows.hpp)
   if (d == 2 && !gen2 && B1 * (int64_t)cs >= ((int64_t)1 << 31))
     return fail(HGP_E_UNSUPPORTED, "2-D grid too large: one right-hand side's intermediate exceeds 2 GiB");
   // RHS chunks: 2-D ops spread them over NS streams, chunk j on stream (and workspace slot)
   // j % NS; each chunk's RHS are processed entirely on its stream (no cross-stream data).
-  const int NS = (d == 2 && only_pass < 0) ? (int)std::min<int64_t>(std::max(1, P->nstreams), nrhs) : 1;
+  const int NS = (d >= 2 && only_pass < 0) ? (int)std::min<int64_t>(std::max(1, P->nstreams), nrhs) : 1;
   int64_t Qc = nrhs;
   if (B1 + B2 > 0) {
     const int64_t per = (B1 + B2) * (int64_t)cs;
@@ -261,7 +273,7 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
     // chunk there cost more in launch tails than the cache gains: C3 / C4 measured slower).
     if (d == 2 && !P->ws_explicit && per * 8 <= ((int64_t)72 << 20)) Qc = std::min<int64_t>(Qc, 8);
     HGP_TRY(P->ws1.ensure((size_t)(B1 * Qc * NS) * cs));
-    if (B2) HGP_TRY(P->ws2.ensure((size_t)(B2 * Qc) * cs));
+    if (B2) HGP_TRY(P->ws2.ensure((size_t)(B2 * Qc * NS) * cs));
   }
   hipStream_t streams[4] = {P->stream, nullptr, nullptr, nullptr};
   if (NS > 1) {
@@ -276,8 +288,9 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
   T* yout = reinterpret_cast<T*>(y);
   const T* dv = reinterpret_cast<const T*>(dotv);
   T* part = reinterpret_cast<T*>(partial);
+  // fused-dot partials per RHS: one per output row pair (3-D: per pair of each i0 plane)
   const int64_t rows_out = (d == 1) ? 1 : (d == 2 ? g.out[0] : g.out[0] * g.out[1]);
-  const int64_t rn_last = (d == 1) ? 1 : (rows_out + 1) / 2;
+  const int64_t rn_last = (d == 1) ? 1 : (d == 3 && !gen3) ? g.out[0] * ((g.out[1] + 1) / 2) : (rows_out + 1) / 2;
 
   int64_t chunk = 0;
   for (int64_t q0 = 0; q0 < nrhs; q0 += Qc, ++chunk) {
@@ -371,9 +384,79 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
         Cd.cg_part = epi->part ? reinterpret_cast<T*>(epi->part) + q0 * nrb : nullptr;
       }
       HGP_TRY(run_rowt(1, Cd, epi_mode));
+    } else if (d == 3 && !gen3) {
+      C2<T>* w1 = reinterpret_cast<C2<T>*>(P->ws1.ptr) + (int64_t)slot * Qc * B1;
+      C2<T>* w2 = reinterpret_cast<C2<T>*>(P->ws2.ptr) + (int64_t)slot * Qc * B2;
+      const int64_t L1 = g.L[1], H2 = g.L[2] / 2, NC2 = H2 + 1, plane = NC2 * S1;
+      auto run_rowt = [&](int inv, PassDesc& D, int epi_mode) -> int {
+        const int me = pass_no++;
+        if (only_pass >= 0 && only_pass != me) return 0;
+        hipError_t e = launch_rowt<T>((int)H2, inv, epi_mode, D, st);
+        if (e != hipSuccess) return fail(HGP_E_HIP, std::string("3-D row pass launch: ") + hipGetErrorString(e));
+        return 0;
+      };
+      auto run_linet = [&](int inv, PassDesc& D) -> int {
+        const int me = pass_no++;
+        if (only_pass >= 0 && only_pass != me) return 0;
+        hipError_t e = launch_linet<T>((int)(L1 / 2), inv, D, st);
+        if (e != hipSuccess) return fail(HGP_E_HIP, std::string("3-D line pass launch: ") + hipGetErrorString(e));
+        return 0;
+      };
+      // Q1: FWD axis 2 on the row pairs of every (RHS, i0) plane -> w1 [q][i0][c2][i1]
+      PassDesc A = base_desc();
+      A.in = View{(void*)xi, g.in[1] * g.in[2], g.in[2], 1, (int)g.in[2]};
+      A.out = View{w1, plane, S1, 1, 0};
+      A.tw = g.tw[2].ptr; A.Q = (int)(qn * g.in[0]); A.Rn = (int)((g.in[1] + 1) / 2); A.nrows = (int)g.in[1];
+      A.done = done;
+      HGP_TRY(run_rowt(0, A, EPI_OUT));
+      // Q2: FWD axis 1 (lines (i0, c2), i1 contiguous), transposed out -> w2 [q][c2][k1][i0]
+      PassDesc Bd = base_desc();
+      Bd.in = View{w1, g.in[0] * plane, S1, plane, (int)g.in[1]};
+      Bd.out = View{w2, B2, L1 * S0, S0, (int)L1};
+      Bd.tw = g.tw[1].ptr; Bd.Q = qn; Bd.Rn = (int)NC2; Bd.In = (int)g.in[0]; Bd.done = done;
+      HGP_TRY(run_linet(0, Bd));
+      // Q3: CONV axis 0 = contiguous lines (q, c2, k1), in place; spectrum [c2][k1][k0];
+      // optional spectral dots spart [q][c2 * L1 + k1]
+      PassDesc Cd = base_desc();
+      Cd.in = View{w2, B2, S0, 1, (int)g.in[0]};
+      Cd.out = View{w2, B2, S0, 1, (int)g.out[0]};
+      Cd.spec = g.spec; Cd.spec_kind = g.spec_kind; Cd.spec_i = 0; Cd.spec_p = 1; Cd.spec_r = g.L[0];
+      Cd.tw = g.tw[0].ptr; Cd.Q = qn; Cd.Rn = (int)(NC2 * L1); Cd.In = 1; Cd.done = done;
+      if (spart != nullptr) {
+        Cd.spart = reinterpret_cast<T*>(spart) + q0 * NC2 * L1;
+        Cd.spart_mid = (int)(H2 / 2);
+        Cd.spart_div = (int)L1;
+      }
+      HGP_TRY(run((int)(g.L[0] / 2), conv_mode, LAY_CONTIG, Cd, (int64_t)qn * Cd.Rn));
+      if (mid != nullptr) (*mid)(q0, qn, st);
+      // Q4: INV axis 1: w2 tiles -> lines (o0, c2), crop -> w1 [q][o0][c2][o1]
+      PassDesc Dd = base_desc();
+      Dd.in = View{w2, B2, L1 * S0, S0, (int)L1};
+      Dd.out = View{w1, g.out[0] * plane, S1, plane, (int)g.out[1]};
+      Dd.tw = g.tw[1].ptr; Dd.Q = qn; Dd.Rn = (int)NC2; Dd.In = (int)g.out[0]; Dd.done = done;
+      HGP_TRY(run_linet(1, Dd));
+      // Q5: INV axis 2 per (RHS, o0) plane: column-major tiles -> real rows, fused dot / PCG update
+      PassDesc E = base_desc();
+      E.in = View{w1, plane, S1, 1, 0};
+      E.out = View{yo, g.out[1] * g.out[2], g.out[2], 1, (int)g.out[2]};
+      E.dot = dvc; E.partial = pc;
+      E.tw = g.tw[2].ptr; E.Q = (int)(qn * g.out[0]); E.Rn = (int)((g.out[1] + 1) / 2); E.nrows = (int)g.out[1];
+      E.done = done;
+      int epi_mode = EPI_OUT;
+      if (epi != nullptr) {
+        epi_mode = epi->mode;
+        const int nrb = (E.Rn + rowt_pairs<T>((int)H2) - 1) / rowt_pairs<T>((int)H2);
+        E.cg_r = reinterpret_cast<T*>(epi->r) + q0 * g.out_M;
+        E.cg_x = reinterpret_cast<T*>(epi->x) + q0 * g.out_M;
+        E.cg_p = reinterpret_cast<T*>(epi->p) + q0 * g.out_M;
+        E.cg_coef = reinterpret_cast<const T*>(epi->coef) + q0;
+        E.cg_div = (int)g.out[0];                 // planes per RHS share one alpha / beta
+        E.cg_part = epi->part ? reinterpret_cast<T*>(epi->part) + q0 * g.out[0] * nrb : nullptr;
+      }
+      HGP_TRY(run_rowt(1, E, epi_mode));
     } else {
-      C2<T>* w1 = reinterpret_cast<C2<T>*>(P->ws1.ptr);
-      C2<T>* w2 = reinterpret_cast<C2<T>*>(P->ws2.ptr);
+      C2<T>* w1 = reinterpret_cast<C2<T>*>(P->ws1.ptr) + (int64_t)slot * Qc * B1;
+      C2<T>* w2 = reinterpret_cast<C2<T>*>(P->ws2.ptr) + (int64_t)slot * Qc * B2;
       const int64_t L1 = g.L[1], H2 = g.L[2] / 2;
       const int64_t rows_in = g.in[0] * g.in[1];
       // P1: FWD axis 2, row pairs -> w1 [q][i0][i1][c2]
@@ -392,7 +475,7 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
       PassDesc P3 = base_desc();
       P3.in = View{w2, B2, Sl, L1 * Sl, (int)g.in[0]};
       P3.out = View{w2, B2, Sl, L1 * Sl, (int)g.out[0]};
-      P3.spec = g.spec; P3.spec_kind = g.spec_kind; P3.spec_i = 1; P3.spec_r = Sl; P3.spec_p = L1 * Sl;
+      P3.spec = g.spec; P3.spec_kind = g.spec_kind; P3.spec_i = L1 * g.L[0]; P3.spec_r = g.L[0]; P3.spec_p = 1;
       P3.tw = g.tw[0].ptr; P3.Q = qn; P3.Rn = (int)L1; P3.In = (int)(H2 + 1); P3.done = done;
       HGP_TRY(run((int)(g.L[0] / 2), conv_mode, LAY_STRIDED, P3, 0));
       // P4: INV axis 1 (strided): lines (o0, c2) -> w1 [q][o0][o1][c2]
@@ -578,17 +661,20 @@ int set_column_t(hgp_plan* P, const void* column, double jitter, double clamp_mi
   const int compact = d > 1 ? 1 : 0;
   const int64_t LKl = P->LK[d - 1], LRl = P->LR[d - 1];
   const int64_t SK = compact ? compact_stride(LKl) : LKl, SR = compact ? compact_stride(LRl) : LRl;
-  const int64_t nK = P->prodLK / LKl * SK, nR = P->prodLR / LRl * SR;
+  // 3-D: [c2][k1][k0] (c2 <= H2, no pitch padding), the contiguous axis-0 lines (q, c2, k1)
+  const int64_t nK = d == 3 ? P->prodLK / LKl * (LKl / 2 + 1) : P->prodLK / LKl * SK;
+  const int64_t nR = d == 3 ? P->prodLR / LRl * (LRl / 2 + 1) : P->prodLR / LRl * SR;
   HGP_TRY(P->specK.ensure((size_t)nK * sizeof(T)));
   HGP_TRY(P->specI.ensure((size_t)nK * sizeof(T)));
   // 2-D: spectra transposed to [compact column c1][k0] for the contiguous column pass
   extract_pair<T>(F, P->specK.ptr, P->specI.ptr, nK, LKl, SK, compact, 1.0 / (double)P->prodLK, s,
-                  d == 2 ? P->LK[0] : 0);
+                  d >= 2 ? P->LK[0] : 0, d == 3 ? P->LK[1] : 0);
   for (int ax = 0; ax < 3; ++ax) gd.L[ax] = P->LR[ax];
   embed_R(sv, g1, gd, s);
   HGP_TRY(fwd_grid_f64(P, P->LR, P->tw64R, g1, g2, &F));
   HGP_TRY(P->specR.ensure((size_t)nR * sizeof(C2<T>)));
-  extract_cplx<T>(F, P->specR.ptr, nR, LRl, SR, compact, 1.0 / (double)P->prodLR, s, d == 2 ? P->LR[0] : 0);
+  extract_cplx<T>(F, P->specR.ptr, nR, LRl, SR, compact, 1.0 / (double)P->prodLR, s, d >= 2 ? P->LR[0] : 0,
+                  d == 3 ? P->LR[1] : 0);
   HIP_TRY(hipGetLastError());
   P->have_spec = true;
   if (n_clamped) {
@@ -701,30 +787,48 @@ int slab_pass_t(hgp_plan* P, int op, int stage, const void* in, void* out, int64
   P3.in = View{const_cast<void*>(in), P0 * Sl, nrhs * P0 * Sl, Sl, (int)g.in[0]};
   P3.out = View{out, P0 * Sl, nrhs * P0 * Sl, Sl, (int)g.out[0]};
   const size_t se = g.spec_kind == SPEC_REAL ? sizeof(T) : cs;
-  P3.spec = static_cast<const char*>(g.spec) + (size_t)(g0 * Sl) * se;
-  P3.spec_kind = g.spec_kind; P3.spec_i = 1; P3.spec_r = Sl; P3.spec_p = L1 * Sl;
+  // spectrum [c2][k1][k0]: group g = k1, inner line = c2
+  P3.spec = static_cast<const char*>(g.spec) + (size_t)(g0 * g.L[0]) * se;
+  P3.spec_kind = g.spec_kind; P3.spec_i = L1 * g.L[0]; P3.spec_r = g.L[0]; P3.spec_p = 1;
   P3.tw = g.tw[0].ptr; P3.Q = (int)nrhs; P3.Rn = (int)ng; P3.In = (int)(H2 + 1);
   return launch<T>((int)(g.L[0] / 2), conv_mode, LAY_STRIDED, P3, 0, st);
 }
 
 // ---- PCG -------------------------------------------------------------------------------------
+// the 3-D operators run their axis-2 rows through the row-pair kernels (per i0 plane) when
+// those fit one CU's LDS; the dot partials then come per (plane, row pair)
+template <typename T>
+bool planes3d(const hgp_plan* P) {
+  return P->d == 3 && rowt_fits<T>((int)(P->LK[2] / 2)) != 0 && linet_fits<T>((int)(P->LK[1] / 2)) != 0;
+}
+template <typename T>
 int rn_last(const hgp_plan* P) {
   if (P->d == 1) return 1;
   if (P->d == 2) return (int)((P->m[0] + 1) / 2);
+  if (planes3d<T>(P)) return (int)(P->m[0] * ((P->m[1] + 1) / 2));
   return (int)((P->m[0] * P->m[1] + 1) / 2);
 }
 
-// 2-D fused PCG (pcg_step_t): the dots p.Ap and z.r come from the column pass as spectral
-// sums over the (RHS, compact column) lines, L_1/2 + 1 partials per RHS; r.r from the fused
-// x/r update, one partial per row block of the row-inverse pass.
-int spec_np(const hgp_plan* P) { return (int)(P->LK[1] / 2 + 1); }
-// the fused 2-D PCG needs the row-pair kernels of the K / C^-1 rows
+// Fused PCG (pcg_step_t): the dots p.Ap and z.r come from the axis-0 conv pass as spectral
+// sums over its lines (2-D: per compact column c1, L_1/2 + 1 partials per RHS; 3-D: per (c2,
+// k1), (L_2/2 + 1) L_1 partials); r.r from the fused x/r update, one partial per row block of
+// the row-inverse pass (3-D: per block of each i0 plane).
+int spec_np(const hgp_plan* P) {
+  return P->d == 2 ? (int)(P->LK[1] / 2 + 1) : (int)((P->LK[2] / 2 + 1) * P->LK[1]);
+}
+// the fused PCG needs the row-pair kernels of the K / C^-1 rows
 template <typename T>
-bool fused2d(const hgp_plan* P) { return P->d == 2 && rowt_fits<T>((int)(P->LK[1] / 2)) != 0; }
+bool fused_pcg(const hgp_plan* P) {
+  return (P->d == 2 && rowt_fits<T>((int)(P->LK[1] / 2)) != 0) || planes3d<T>(P);
+}
 template <typename T>
 int xr_np(const hgp_plan* P) {
-  const int pairs = rowt_pairs<T>((int)(P->LK[1] / 2));
-  return (int)(((P->m[0] + 1) / 2 + pairs - 1) / pairs);
+  if (P->d == 2) {
+    const int pairs = rowt_pairs<T>((int)(P->LK[1] / 2));
+    return (int)(((P->m[0] + 1) / 2 + pairs - 1) / pairs);
+  }
+  const int pairs = rowt_pairs<T>((int)(P->LK[2] / 2));
+  return (int)(P->m[0] * (((P->m[1] + 1) / 2 + pairs - 1) / pairs));
 }
 
 template <typename T>
@@ -736,11 +840,12 @@ int pcg_begin_t(hgp_plan* P, const void* b, void* x, int64_t nrhs, int use_preco
   HGP_TRY(P->z.ensure(vb));
   HGP_TRY(P->p.ensure(vb));
   HGP_TRY(P->Ap.ensure(vb));
-  const bool fused = fused2d<T>(P);
-  const int npo = fused ? std::max(rn_last(P), spec_np(P)) : rn_last(P);
+  const bool fused = fused_pcg<T>(P);
+  const int npo = fused ? std::max(rn_last<T>(P), spec_np(P)) : rn_last<T>(P);
   const int npu = fused ? std::max(update_np(M), xr_np<T>(P)) : update_np(M);
   HGP_TRY(P->part_op.ensure((size_t)(nrhs * npo) * sizeof(T)));
   HGP_TRY(P->part_u.ensure((size_t)(nrhs * npu) * sizeof(T)));
+  if (fused && fold_groups(spec_np(P)) > 0) HGP_TRY(P->part_f.ensure((size_t)(nrhs * fold_groups(spec_np(P))) * sizeof(T)));
   HGP_TRY(P->scal.ensure((size_t)(4 * nrhs) * sizeof(T)));
   HGP_TRY(P->flags.ensure(16));
   const void* brow = b;
@@ -760,7 +865,13 @@ int pcg_begin_t(hgp_plan* P, const void* b, void* x, int64_t nrhs, int use_preco
   if (use_precond && fused) {
     // p = z = C^-1 r straight into p; rs = z.r as the column pass's spectral dot
     HGP_TRY(run_op<T>(P, HGP_OP_CINV, P->r.ptr, P->p.ptr, nrhs, nullptr, nullptr, nullptr, -1, P->part_op.ptr));
-    reduce_rows<T>(P->part_op.ptr, spec_np(P), (int)nrhs, rs, s);
+    const int G = fold_groups(spec_np(P));
+    if (G > 0) {
+      fold_rows<T>(P->part_op.ptr, spec_np(P), (int)nrhs, P->part_f.ptr, nullptr, s);
+      reduce_rows<T>(P->part_f.ptr, G, (int)nrhs, rs, s);
+    } else {
+      reduce_rows<T>(P->part_op.ptr, spec_np(P), (int)nrhs, rs, s);
+    }
   } else if (use_precond) {
     HGP_TRY(run_op<T>(P, HGP_OP_CINV, P->r.ptr, P->z.ptr, nrhs, P->r.ptr, P->part_op.ptr, nullptr));
     reduce_rows<T>(P->part_op.ptr, npo, (int)nrhs, rs, s);
@@ -784,7 +895,7 @@ template <typename T>
 int pcg_step_t(hgp_plan* P, double tol) {
   hipStream_t s = P->stream;
   const int64_t nrhs = P->cg_nrhs, M = P->M;
-  const int npo = rn_last(P), npu = update_np(M);
+  const int npo = rn_last<T>(P), npu = update_np(M);
   int* flags = reinterpret_cast<int*>(P->flags.ptr);
   int* done = flags;
   int* iters = flags + 1;
@@ -793,25 +904,33 @@ int pcg_step_t(hgp_plan* P, double tol) {
   T* alpha = sc + nrhs;
   T* beta = sc + 2 * nrhs;
   T* rnew = sc + 3 * nrhs;
-  if (fused2d<T>(P)) {
-    // Fused 2-D iteration.  K p: the column pass leaves the spectral p.Ap partials, alpha is
+  if (fused_pcg<T>(P)) {
+    // Fused iteration (2-D, 3-D).  K p: the axis-0 pass leaves the spectral p.Ap partials, alpha is
     // formed per RHS chunk before the row-inverse pass, whose epilogue does x += alpha p,
     // r -= alpha Ap (+ r.r partials) with Ap never stored.  Then the break test; then C^-1 r,
     // whose epilogue does p = z + beta p (z never stored).  Order and semantics of cg.py:63-78.
-    const int nps = spec_np(P), npx = xr_np<T>(P);
-    T* part_s = reinterpret_cast<T*>(P->part_op.ptr);
+    const int nps0 = spec_np(P), npx = xr_np<T>(P);
+    const int G = fold_groups(nps0);    // long rows (3-D) are folded per chunk first
+    const int nps = G > 0 ? G : nps0;
+    T* part_o = reinterpret_cast<T*>(P->part_op.ptr);
+    T* part_s = G > 0 ? reinterpret_cast<T*>(P->part_f.ptr) : part_o;
+    auto fold = [&](int64_t q0, int qn, hipStream_t cs) {
+      if (G > 0) fold_rows<T>(part_o + q0 * nps0, nps0, qn, part_s + q0 * G, done, cs);
+    };
     const MidFn mid_alpha = [&](int64_t q0, int qn, hipStream_t cs) {
+      fold(q0, qn, cs);
       cg_alpha<T>(part_s + q0 * nps, nps, qn, rs + q0, alpha + q0, done, cs);
     };
     const RowEpi exr{EPI_XR, P->r.ptr, P->cg_x, P->p.ptr, alpha, P->part_u.ptr};
-    HGP_TRY(run_op<T>(P, HGP_OP_K, P->p.ptr, P->Ap.ptr, nrhs, nullptr, nullptr, done, -1, part_s, &exr, &mid_alpha));
+    HGP_TRY(run_op<T>(P, HGP_OP_K, P->p.ptr, P->Ap.ptr, nrhs, nullptr, nullptr, done, -1, part_o, &exr, &mid_alpha));
     cg_check<T>(P->part_u.ptr, npx, (int)nrhs, tol, rnew, done, iters, s);
     if (P->cg_precond) {
       const MidFn mid_beta = [&](int64_t q0, int qn, hipStream_t cs) {
+        fold(q0, qn, cs);
         cg_beta<T>(part_s + q0 * nps, nps, qn, rs + q0, beta + q0, done, cs);
       };
       const RowEpi ep{EPI_P, P->r.ptr, P->cg_x, P->p.ptr, beta, nullptr};
-      HGP_TRY(run_op<T>(P, HGP_OP_CINV, P->r.ptr, P->Ap.ptr, nrhs, nullptr, nullptr, done, -1, part_s, &ep, &mid_beta));
+      HGP_TRY(run_op<T>(P, HGP_OP_CINV, P->r.ptr, P->Ap.ptr, nrhs, nullptr, nullptr, done, -1, part_o, &ep, &mid_beta));
     } else {
       cg_beta<T>(P->part_u.ptr, npx, (int)nrhs, rs, beta, done, s);
       cg_update_p<T>(P->p.ptr, P->r.ptr, beta, nrhs, M, done, s);

@@ -20,6 +20,10 @@ hipError_t launch_rowt(int H, int inv, int epi, const PassDesc& d, hipStream_t s
 template <typename T> int rowt_pairs(int H);
 // whether the row-pair kernels of H points fit one CU's LDS (else run_op takes the generic path)
 template <typename T> int rowt_fits(int H);
+// 3-D middle-axis transposing line passes (hgp_lines.hpp): inv = 0 k_line_fwd_t, 1 k_line_inv_t
+template <typename T>
+hipError_t launch_linet(int H, int inv, const PassDesc& d, hipStream_t s);
+template <typename T> int linet_fits(int H);
 
 // setup (fp64)
 // Bluestein partial DFT pieces of the DCT-I (hgp_kernels.hip)
@@ -34,9 +38,9 @@ void clamp_spectrum(const double* Draw, double* out3, int64_t M, double clamp_mi
 void embed_K(const double* cK, const double* cI, double2* out, const GridDims& g, hipStream_t s);
 void embed_R(const double* sv, double2* out, const GridDims& g, hipStream_t s);
 template <typename T> void extract_pair(const double2* F, void* a, void* b, int64_t n, int64_t L, int64_t S, int compact,
-                                        double scale, hipStream_t s, int64_t L0t = 0);
+                                        double scale, hipStream_t s, int64_t L0t = 0, int64_t L1t = 0);
 template <typename T> void extract_cplx(const double2* F, void* o, int64_t n, int64_t L, int64_t S, int compact, double scale,
-                                        hipStream_t s, int64_t L0t = 0);
+                                        hipStream_t s, int64_t L0t = 0, int64_t L1t = 0);
 template <typename T> void expand_spec(const double* src, void* out, const GridDims& g, hipStream_t s);
 
 // dense grid cross covariance (hgp_kuf.hip)
@@ -83,6 +87,9 @@ template <typename T> void vcopy(const void* src, void* dst, int64_t n, const in
 template <typename T> void transpose(const void* in, void* out, int64_t rows, int64_t cols, hipStream_t s);
 template <typename T> void rowdot_part(const void* a, const void* c, void* part, int64_t nrhs, int64_t M, int np, hipStream_t s);
 template <typename T> void reduce_rows(const void* part, int np, int nrhs, void* out, hipStream_t s);
+// rows of np > fold_groups threshold partials -> fold_groups(np) partials per RHS (0: no fold needed)
+int fold_groups(int np);
+template <typename T> void fold_rows(const void* part, int np, int nrhs, void* out, const int* done, hipStream_t s);
 template <typename T> void cg_alpha(const void* part, int np, int nrhs, const void* rs, void* alpha, const int* done, hipStream_t s);
 template <typename T> void cg_update_xr(void* x, void* r, const void* p, const void* Ap, const void* alpha, void* part,
                                         int64_t nrhs, int64_t M, const int* done, hipStream_t s);

@@ -170,12 +170,18 @@ void embed_R(const double* sv, double2* out, const GridDims& g, hipStream_t s) {
 // the layout the passes read: when `compact`, the last axis keeps only the S >= H+1 "compact"
 // half-spectrum columns c (even frequency 2c for c <= H/2, odd 2(c-H/2-1)+1 after; zero pad
 // beyond H) — the real-data passes store exactly these columns.
-__device__ __forceinline__ int64_t spec_src(int64_t idx, int64_t L, int64_t S, int compact, int64_t L0t) {
+__device__ __forceinline__ int64_t spec_src(int64_t idx, int64_t L, int64_t S, int compact, int64_t L0t,
+                                            int64_t L1t) {
   if (!compact) return idx;
   int64_t o, c;
-  if (L0t > 0) { c = idx / L0t; o = idx - c * L0t; }     // transposed: [c][k0], k0 < L0t
-  else { o = idx / S; c = idx - o * S; }
   const int64_t H = L / 2;
+  if (L0t > 0 && L1t > 0) {                               // 3-D transposed: [c][k1][k0]
+    const int64_t k0 = idx % L0t, rest = idx / L0t;
+    const int64_t k1 = rest % L1t;
+    c = rest / L1t;
+    o = k0 * L1t + k1;
+  } else if (L0t > 0) { c = idx / L0t; o = idx - c * L0t; }   // 2-D transposed: [c][k0], k0 < L0t
+  else { o = idx / S; c = idx - o * S; }
   if (c > H) return -1;
   const int64_t kp = (c <= H / 2) ? c : H + (c - H / 2 - 1);
   return o * L + kp;
@@ -183,41 +189,43 @@ __device__ __forceinline__ int64_t spec_src(int64_t idx, int64_t L, int64_t S, i
 
 template <typename T>
 __global__ void k_extract_pair(const double2* __restrict__ F, T* __restrict__ a, T* __restrict__ b, int64_t n,
-                               int64_t L, int64_t S, int compact, double scale, int64_t L0t) {
+                               int64_t L, int64_t S, int compact, double scale, int64_t L0t, int64_t L1t) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const int64_t src = spec_src(i, L, S, compact, L0t);
+  const int64_t src = spec_src(i, L, S, compact, L0t, L1t);
   const double2 f = src >= 0 ? F[src] : make_double2(0.0, 0.0);
   a[i] = (T)(f.x * scale);
   b[i] = (T)(f.y * scale);
 }
 template <typename T>
 __global__ void k_extract_cplx(const double2* __restrict__ F, C2<T>* __restrict__ o, int64_t n, int64_t L, int64_t S,
-                               int compact, double scale, int64_t L0t) {
+                               int compact, double scale, int64_t L0t, int64_t L1t) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const int64_t src = spec_src(i, L, S, compact, L0t);
+  const int64_t src = spec_src(i, L, S, compact, L0t, L1t);
   const double2 f = src >= 0 ? F[src] : make_double2(0.0, 0.0);
   o[i] = mk<T>((T)(f.x * scale), (T)(f.y * scale));
 }
 // L0t > 0: 2-D transposed layout [compact column c][axis-0 frequency k0 < L0t] read by the
-// column pass of the column-major intermediate (hgp_rows.hpp); else [outer][c] with pitch S.
+// column pass of the column-major intermediate (hgp_rows.hpp); L0t, L1t > 0: 3-D
+// [c][k1 < L1t][k0 < L0t], read by the contiguous axis-0 pass of the 3-D sequence
+// (hgp_lines.hpp); else [outer][c] with pitch S.
 template <typename T>
 void extract_pair(const double2* F, void* a, void* b, int64_t n, int64_t L, int64_t S, int compact, double scale,
-                  hipStream_t s, int64_t L0t) {
+                  hipStream_t s, int64_t L0t, int64_t L1t) {
   hipLaunchKernelGGL((k_extract_pair<T>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, F, (T*)a, (T*)b, n, L, S,
-                     compact, scale, L0t);
+                     compact, scale, L0t, L1t);
 }
 template <typename T>
 void extract_cplx(const double2* F, void* o, int64_t n, int64_t L, int64_t S, int compact, double scale, hipStream_t s,
-                  int64_t L0t) {
+                  int64_t L0t, int64_t L1t) {
   hipLaunchKernelGGL((k_extract_cplx<T>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, F, (C2<T>*)o, n, L, S,
-                     compact, scale, L0t);
+                     compact, scale, L0t, L1t);
 }
-template void extract_pair<float>(const double2*, void*, void*, int64_t, int64_t, int64_t, int, double, hipStream_t, int64_t);
-template void extract_pair<double>(const double2*, void*, void*, int64_t, int64_t, int64_t, int, double, hipStream_t, int64_t);
-template void extract_cplx<float>(const double2*, void*, int64_t, int64_t, int64_t, int, double, hipStream_t, int64_t);
-template void extract_cplx<double>(const double2*, void*, int64_t, int64_t, int64_t, int, double, hipStream_t, int64_t);
+template void extract_pair<float>(const double2*, void*, void*, int64_t, int64_t, int64_t, int, double, hipStream_t, int64_t, int64_t);
+template void extract_pair<double>(const double2*, void*, void*, int64_t, int64_t, int64_t, int, double, hipStream_t, int64_t, int64_t);
+template void extract_cplx<float>(const double2*, void*, int64_t, int64_t, int64_t, int, double, hipStream_t, int64_t, int64_t);
+template void extract_cplx<double>(const double2*, void*, int64_t, int64_t, int64_t, int, double, hipStream_t, int64_t, int64_t);
 
 // full expanded-grid spectrum from the unique m-grid values: u -> min(u, n-u) per axis
 template <typename T>
@@ -347,6 +355,40 @@ __global__ __launch_bounds__(RED_THREADS) void k_reduce_rows(const T* __restrict
   if (threadIdx.x == 0) out[b] = s;
 }
 
+// Long partial rows (the 3-D spectral dots: (L_2/2 + 1) L_1 per RHS) are folded first: block
+// (g, b) sums FOLD_PER consecutive partials of RHS b (all loads issued up front) into
+// out[b][g], so the one-block-per-RHS kernels below see ceil(np / FOLD_PER) values.  Fixed
+// summation order: deterministic.
+constexpr int FOLD_PER = 16 * RED_THREADS;
+template <typename T>
+__global__ __launch_bounds__(RED_THREADS) void k_fold_rows(const T* __restrict__ part, int np, int G,
+                                                           T* __restrict__ out, const int* done) {
+  if (done != nullptr && *done) return;
+  __shared__ T red[RED_THREADS / 64];
+  const int g = blockIdx.x, b = blockIdx.y;
+  const T* row = part + (int64_t)b * np + (int64_t)g * FOLD_PER;
+  const int n = np - g * FOLD_PER < FOLD_PER ? np - g * FOLD_PER : FOLD_PER;
+  T v[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int idx = threadIdx.x + k * RED_THREADS;
+    v[k] = idx < n ? row[idx] : (T)0;
+  }
+  T s = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) s += v[k];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    T t = 0;
+#pragma unroll
+    for (int i = 0; i < RED_THREADS / 64; ++i) t += red[i];
+    out[(int64_t)b * G + g] = t;
+  }
+}
+
 // per RHS: alpha = rs / sum(part)   (cg.py:66)
 template <typename T>
 __global__ __launch_bounds__(RED_THREADS) void k_cg_alpha(const T* __restrict__ part, int np, int nrhs,
@@ -469,6 +511,13 @@ void reduce_rows(const void* part, int np, int nrhs, void* out, hipStream_t s) {
   hipLaunchKernelGGL((k_reduce_rows<T>), dim3((unsigned)nrhs), dim3(RED_THREADS), 0, s, (const T*)part, np, nrhs,
                      (T*)out);
 }
+int fold_groups(int np) { return np > FOLD_PER ? (np + FOLD_PER - 1) / FOLD_PER : 0; }
+template <typename T>
+void fold_rows(const void* part, int np, int nrhs, void* out, const int* done, hipStream_t s) {
+  const int G = fold_groups(np);
+  hipLaunchKernelGGL((k_fold_rows<T>), dim3((unsigned)G, (unsigned)nrhs), dim3(RED_THREADS), 0, s, (const T*)part, np, G,
+                     (T*)out, done);
+}
 template <typename T>
 void cg_alpha(const void* part, int np, int nrhs, const void* rs, void* alpha, const int* done, hipStream_t s) {
   hipLaunchKernelGGL((k_cg_alpha<T>), dim3((unsigned)nrhs), dim3(RED_THREADS), 0, s, (const T*)part, np, nrhs,
@@ -529,6 +578,7 @@ void cg_set_done(int* done, const int* flag, hipStream_t s) {
   template void transpose<T>(const void*, void*, int64_t, int64_t, hipStream_t);                             \
   template void rowdot_part<T>(const void*, const void*, void*, int64_t, int64_t, int, hipStream_t);         \
   template void reduce_rows<T>(const void*, int, int, void*, hipStream_t);                                   \
+  template void fold_rows<T>(const void*, int, int, void*, const int*, hipStream_t);                         \
   template void cg_alpha<T>(const void*, int, int, const void*, void*, const int*, hipStream_t);             \
   template void cg_update_xr<T>(void*, void*, const void*, const void*, const void*, void*, int64_t, int64_t, \
                                 const int*, hipStream_t);                                                    \

@@ -83,18 +83,21 @@ struct PassDesc {
   int Rn, In;                 // lines per RHS: r in [0,Rn) (outer), i in [0,In) (inner, strided)
   int nrows;                  // LAY_RP: real rows per RHS (the pair (2r, 2r+1) needs 2r+1 < nrows)
   const int* done;            // optional device flag: skip the pass when *done != 0
-  // CONV passes (non-strided): spectral dot of the transformed line with itself weighted by
-  // the real spectrum, sum_k S_k |X_k|^2 = <x, op x> by Parseval (the crop is exact: x is zero
-  // outside it), stored as spart[q * Rn + r] x the compact-column weight (1 for columns 0 and
-  // spart_mid, else 2 = the column and its Hermitian mirror; spart_mid < 0: weight 1).
+  // CONV passes: spectral dot of the transformed line with itself weighted by the real
+  // spectrum, sum_k S_k |X_k|^2 = <x, op x> by Parseval (the crop is exact: x is zero outside
+  // it), stored as spart[q * Rn + r] (strided: spart[(q * Rn + r) * In + i]) x the weight of
+  // the compact column r (1 for columns 0 and spart_mid, else 2 = the column and its
+  // Hermitian mirror; spart_mid < 0: weight 1).
   void* spart;
   int spart_mid;
+  int spart_div;              // > 1: the compact column of line r is r / spart_div (3-D: r = c2 * L1 + k1)
   // fused PCG epilogue of the 2-D row-inverse pass (hgp_rows.hpp, EPI_XR / EPI_P)
   void* cg_r;
   void* cg_x;
   void* cg_p;
   const void* cg_coef;        // per-RHS alpha (EPI_XR) or beta (EPI_P)
   void* cg_part;              // EPI_XR: per-block partial sums of r.r  [q][row block]
+  int cg_div;                 // > 1: cg_div consecutive q (3-D: the i0 planes of one RHS) share a coefficient
 };
 
 constexpr int LDS_CAP = 160 * 1024;
@@ -519,8 +522,22 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
       if (d.spart != nullptr) {     // uniform over the block
         const T s = line_sum<T, TT>(sdot, reinterpret_cast<T*>(smem_raw));
         if (t == 0 && valid) {
-          const T w = (d.spart_mid < 0 || r == 0 || r == d.spart_mid) ? (T)1 : (T)2;
+          const int col = d.spart_div > 1 ? r / d.spart_div : r;
+          const T w = (d.spart_mid < 0 || col == 0 || col == d.spart_mid) ? (T)1 : (T)2;
           reinterpret_cast<T*>(d.spart)[(int64_t)q * d.Rn + r] = w * s;
+        }
+      }
+    } else if constexpr (MODE == PASS_CONV) {
+      if (d.spart != nullptr) {     // uniform: a line's TT threads are C apart (t-major ids)
+        T* red = reinterpret_cast<T*>(smem_raw);
+        __syncthreads();            // the last exchange image is consumed
+        red[tid] = sdot;
+        __syncthreads();
+        if (tid < C && valid) {     // fixed summation order: deterministic
+          T s = 0;
+          for (int tt2 = 0; tt2 < TT; ++tt2) s += red[tt2 * C + tid];
+          const T w = (d.spart_mid < 0 || r == 0 || r == d.spart_mid) ? (T)1 : (T)2;
+          reinterpret_cast<T*>(d.spart)[((int64_t)q * d.Rn + r) * d.In + i] = w * s;
         }
       }
     }

@@ -3,6 +3,7 @@
 #pragma once
 #include "hgp_internal.hpp"
 #include "hgp_rows.hpp"
+#include "hgp_lines.hpp"
 
 namespace hgp {
 
@@ -99,6 +100,41 @@ static hipError_t launch_rowt_h(int inv, int epi, const PassDesc& d, hipStream_t
   }
   hipLaunchKernelGGL((k_row_fwd_t<T, H>), dim3((unsigned)nb), dim3(Cfg::THREADS), Cfg::LDS, s, d);
   return hipGetLastError();
+}
+
+template <typename T, int H>
+static hipError_t launch_linet_h(int inv, const PassDesc& d, hipStream_t s) {
+  using Cfg = LineTCfg<T, H>;
+  if constexpr (Cfg::LDS > LDS_CAP) return hipErrorNotSupported;
+  const int64_t nb = (int64_t)d.Q * d.Rn * ((d.In + Cfg::C - 1) / Cfg::C);
+  if (nb <= 0) return hipSuccess;
+  if (nb > 0x7fffffff) return hipErrorInvalidValue;
+  static bool attr_f = false, attr_i = false;
+  bool& attr = inv ? attr_i : attr_f;
+  const void* fn = inv ? (const void*)k_line_inv_t<T, H> : (const void*)k_line_fwd_t<T, H>;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  if (inv) hipLaunchKernelGGL((k_line_inv_t<T, H>), dim3((unsigned)nb), dim3(Cfg::THREADS), Cfg::LDS, s, d);
+  else hipLaunchKernelGGL((k_line_fwd_t<T, H>), dim3((unsigned)nb), dim3(Cfg::THREADS), Cfg::LDS, s, d);
+  return hipGetLastError();
+}
+
+template <typename T, int H>
+static int linet_fits_h() { return LineTCfg<T, H>::LDS <= LDS_CAP ? 1 : 0; }
+
+template <typename T>
+int linet_fits(int H) {
+  HGP_H_SWITCH(linet_fits_h)
+  return 0;
+}
+
+template <typename T>
+hipError_t launch_linet(int H, int inv, const PassDesc& d, hipStream_t s) {
+  HGP_H_SWITCH(launch_linet_h, inv, d, s)
+  return hipErrorInvalidValue;
 }
 
 template <typename T, int H>

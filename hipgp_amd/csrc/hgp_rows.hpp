@@ -330,7 +330,7 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
     }
     __syncthreads();
     const int64_t g0 = (int64_t)q * d.out.q_stride + (int64_t)row0 * d.out.r_stride;
-    const T coef = reinterpret_cast<const T*>(d.cg_coef)[q];
+    const T coef = reinterpret_cast<const T*>(d.cg_coef)[d.cg_div > 1 ? q / d.cg_div : q];
     T* pg = reinterpret_cast<T*>(d.cg_p) + g0;
     T* xg = EPI == EPI_XR ? reinterpret_cast<T*>(d.cg_x) + g0 : pg;
     T* rg = EPI == EPI_XR ? reinterpret_cast<T*>(d.cg_r) + g0 : pg;
