@@ -261,11 +261,24 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
     return fail(HGP_E_UNSUPPORTED, "2-D grid too large: one right-hand side's intermediate exceeds 2 GiB");
   // RHS chunks: 2-D ops spread them over NS streams, chunk j on stream (and workspace slot)
   // j % NS; each chunk's RHS are processed entirely on its stream (no cross-stream data).
-  const int NS = (d >= 2 && only_pass < 0) ? (int)std::min<int64_t>(std::max(1, P->nstreams), nrhs) : 1;
+  int NS = (d >= 2 && only_pass < 0) ? (int)std::min<int64_t>(std::max(1, P->nstreams), nrhs) : 1;
   int64_t Qc = nrhs;
   if (B1 + B2 > 0) {
     const int64_t per = (B1 + B2) * (int64_t)cs;
-    Qc = std::max<int64_t>(1, std::min<int64_t>((nrhs + NS - 1) / NS, P->ws_budget / (per * NS)));
+    int64_t budget = P->ws_budget;
+    // 3-D R / R^T on large grids: their complex spectrum (on the L_R grid) is as large as one
+    // RHS's intermediate, and the axis-0 pass shares it only between the RHS of one chunk.  Where
+    // the byte budget allows fewer than two RHS per chunk, these ops run on one stream in chunks
+    // of up to 8 RHS as device memory allows (C5 R^T: 38 -> 36 ms; 2-D C4 R^T lost its stream
+    // overlap that way, 36 -> 43 ms, and keeps the budget)
+    if (g.spec_kind != SPEC_REAL && d == 3 && !P->ws_explicit && nrhs > 1 && per * 2 > budget) {
+      size_t fr = 0, tot = 0;
+      if (hipMemGetInfo(&fr, &tot) == hipSuccess) {
+        NS = 1;
+        budget = std::max<int64_t>(budget, std::min<int64_t>(per * 8, (int64_t)(fr / 2)));
+      }
+    }
+    Qc = std::max<int64_t>(1, std::min<int64_t>((nrhs + NS - 1) / NS, budget / (per * NS)));
     // Infinity-Cache-resident chunks: where 8 RHS of a 2-D intermediate fit in ~72 MiB, each
     // stream works on 8 RHS at a time, so the intermediate a column pass writes is still in the
     // 256 MiB Infinity Cache when the row-inverse pass reads it (C2: row inverse 4.2 -> 5.0 TB/s,
@@ -544,6 +557,36 @@ int fwd_grid_f64(hgp_plan* P, const int64_t* L, const DevBuf* tw64, double2* a, 
   return 0;
 }
 
+// Forward FFT of a REAL fp64 L-grid (d >= 2) that only needs the compact half spectrum of the
+// last axis (the R filter): real row pairs -> compact half spectra (k_pass RP, pitch S), then
+// the other axes over the H + 1 compact columns only, in place.  Result: b [k0][k1][S].
+int fwd_grid_real_f64(hgp_plan* P, const int64_t* L, const DevBuf* tw64, const double* a, double2* b, int64_t S) {
+  const int d = P->d;
+  hipStream_t s = P->stream;
+  const int64_t Ll = L[d - 1], H = Ll / 2;
+  int64_t rows = 1;
+  for (int ax = 0; ax < d - 1; ++ax) rows *= L[ax];
+  PassDesc A = base_desc();     // last axis: real row pairs (fold: rows of length 2H)
+  A.in = View{const_cast<double*>(a), 0, Ll, 1, (int)Ll};
+  A.out = View{b, 0, S, 1, 0};
+  A.tw = tw64[d - 1].ptr; A.Q = 1; A.Rn = (int)((rows + 1) / 2); A.nrows = (int)rows; A.In = 1;
+  HGP_TRY(launch<double>((int)H, PASS_FWD, LAY_RP, A, A.Rn, s));
+  if (d == 3) {                 // axis 1 (strided, in place): lines (k0, c)
+    PassDesc Bd = base_desc();
+    Bd.in = View{b, 0, L[1] * S, S, (int)L[1]};
+    Bd.out = View{b, 0, L[1] * S, S, (int)L[1]};
+    Bd.tw = tw64[1].ptr; Bd.Q = 1; Bd.Rn = (int)L[0]; Bd.In = (int)(H + 1);
+    HGP_TRY(launch<double>((int)(L[1] / 2), PASS_FWD, LAY_STRIDED, Bd, 0, s));
+  }
+  PassDesc Cd = base_desc();    // axis 0 (strided, in place): lines (k1, c)
+  const int64_t ps = (d == 3 ? L[1] : 1) * S;
+  Cd.in = View{b, 0, S, ps, (int)L[0]};
+  Cd.out = View{b, 0, S, ps, (int)L[0]};
+  Cd.tw = tw64[0].ptr; Cd.Q = 1; Cd.Rn = (int)(d == 3 ? L[1] : 1); Cd.In = (int)(H + 1);
+  HGP_TRY(launch<double>((int)(L[0] / 2), PASS_FWD, LAY_STRIDED, Cd, 0, s));
+  return 0;
+}
+
 template <typename T>
 int upload_twiddles(DevBuf& buf, int64_t L) {
   std::vector<T> h((size_t)(2 * L));
@@ -666,15 +709,25 @@ int set_column_t(hgp_plan* P, const void* column, double jitter, double clamp_mi
   const int64_t nR = d == 3 ? P->prodLR / LRl * (LRl / 2 + 1) : P->prodLR / LRl * SR;
   HGP_TRY(P->specK.ensure((size_t)nK * sizeof(T)));
   HGP_TRY(P->specI.ensure((size_t)nK * sizeof(T)));
-  // 2-D: spectra transposed to [compact column c1][k0] for the contiguous column pass
-  extract_pair<T>(F, P->specK.ptr, P->specI.ptr, nK, LKl, SK, compact, 1.0 / (double)P->prodLK, s,
-                  d >= 2 ? P->LK[0] : 0, d == 3 ? P->LK[1] : 0);
+  // d >= 2: spectra transposed to [compact column][k1][k0] for the contiguous axis-0 pass
+  if (d == 1)
+    extract_pair<T>(F, P->specK.ptr, P->specI.ptr, nK, LKl, SK, compact, 1.0 / (double)P->prodLK, s);
+  else
+    extract_t<T>(F, P->specK.ptr, P->specI.ptr, P->LK[0], d == 3 ? P->LK[1] : 1, LKl / 2, LKl, 0,
+                 1.0 / (double)P->prodLK, s);
   for (int ax = 0; ax < 3; ++ax) gd.L[ax] = P->LR[ax];
-  embed_R(sv, g1, gd, s);
-  HGP_TRY(fwd_grid_f64(P, P->LR, P->tw64R, g1, g2, &F));
   HGP_TRY(P->specR.ensure((size_t)nR * sizeof(C2<T>)));
-  extract_cplx<T>(F, P->specR.ptr, nR, LRl, SR, compact, 1.0 / (double)P->prodLR, s, d >= 2 ? P->LR[0] : 0,
-                  d == 3 ? P->LR[1] : 0);
+  if (d == 1) {
+    embed_R(sv, g1, gd, s);
+    HGP_TRY(fwd_grid_f64(P, P->LR, P->tw64R, g1, g2, &F));
+    extract_cplx<T>(F, P->specR.ptr, nR, LRl, SR, compact, 1.0 / (double)P->prodLR, s);
+  } else {
+    // the R filter is real: real row-pair transform of the last axis, compact columns only after
+    embed_R_real(sv, reinterpret_cast<double*>(g1), gd, s);
+    HGP_TRY(fwd_grid_real_f64(P, P->LR, P->tw64R, reinterpret_cast<const double*>(g1), g2, SR));
+    extract_t<T>(g2, P->specR.ptr, nullptr, P->LR[0], d == 3 ? P->LR[1] : 1, LRl / 2, SR, 1,
+                 1.0 / (double)P->prodLR, s);
+  }
   HIP_TRY(hipGetLastError());
   P->have_spec = true;
   if (n_clamped) {

@@ -37,6 +37,12 @@ void clamp_spectrum(const double* Draw, double* out3, int64_t M, double clamp_mi
                     hipStream_t s);
 void embed_K(const double* cK, const double* cI, double2* out, const GridDims& g, hipStream_t s);
 void embed_R(const double* sv, double2* out, const GridDims& g, hipStream_t s);
+void embed_R_real(const double* sv, double* out, const GridDims& g, hipStream_t s);
+// d >= 2: tiled transposing extraction into [c][k1][k0] (hgp_kernels.hip k_extract_t); b == nullptr:
+// complex spectrum into a, else the pair (Re -> a, Im -> b)
+template <typename T>
+void extract_t(const double2* F, void* a, void* b, int64_t L0, int64_t L1, int64_t H, int64_t Ssrc, int compact_src,
+               double scale, hipStream_t s);
 template <typename T> void extract_pair(const double2* F, void* a, void* b, int64_t n, int64_t L, int64_t S, int compact,
                                         double scale, hipStream_t s, int64_t L0t = 0, int64_t L1t = 0);
 template <typename T> void extract_cplx(const double2* F, void* o, int64_t n, int64_t L, int64_t S, int compact, double scale,

@@ -155,6 +155,31 @@ __global__ void k_embed_R(const double* __restrict__ s, double2* __restrict__ ou
   out[idx] = v;
 }
 
+// the same R filter as a REAL grid (the set-up transforms it with the real row-pair pass)
+__global__ void k_embed_R_real(const double* __restrict__ s, double* __restrict__ out, GridDims g, int64_t total) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  int64_t rem = idx, src = 0, mstride = 1;
+  bool ok = true;
+  for (int a = g.d - 1; a >= 0; --a) {
+    const int64_t u = rem % g.L[a];
+    rem /= g.L[a];
+    const int64_t m = g.m[a], n = g.n[a], L = g.L[a];
+    int64_t t;
+    if (u < n) t = (u <= m - 1) ? u : n - u;
+    else if (u >= L - m + 1) t = L - u;
+    else { ok = false; t = 0; }
+    src += t * mstride;
+    mstride *= m;
+  }
+  out[idx] = ok ? s[src] : 0.0;
+}
+void embed_R_real(const double* sv, double* out, const GridDims& g, hipStream_t s) {
+  int64_t total = 1;
+  for (int a = 0; a < g.d; ++a) total *= g.L[a];
+  hipLaunchKernelGGL(k_embed_R_real, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, sv, out, g, total);
+}
+
 void embed_K(const double* cK, const double* cI, double2* out, const GridDims& g, hipStream_t s) {
   int64_t total = 1;
   for (int a = 0; a < g.d; ++a) total *= g.L[a];
@@ -222,6 +247,56 @@ void extract_cplx(const double2* F, void* o, int64_t n, int64_t L, int64_t S, in
   hipLaunchKernelGGL((k_extract_cplx<T>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, F, (C2<T>*)o, n, L, S,
                      compact, scale, L0t, L1t);
 }
+// Transposing spectrum extraction for d >= 2 through 32 x 32 LDS tiles (both the grid reads
+// and the spectrum writes are contiguous): source F[(k0 * L1 + k1) * Ssrc + col] (col = c for
+// a compact source from the real row-pair transform, else the permuted-order position of
+// compact column c), destination [c][k1][k0] (2-D: L1 = 1, [c][k0]), c < NC = H + 1.
+template <typename T, bool PAIR>
+__global__ __launch_bounds__(256) void k_extract_t(const double2* __restrict__ F, T* __restrict__ a,
+                                                   T* __restrict__ b, int64_t L0, int64_t L1, int64_t NC,
+                                                   int64_t Ssrc, int compact_src, int64_t H, double scale) {
+  __shared__ double2 tile[32][33];
+  const int64_t k1 = blockIdx.z;
+  const int64_t c0 = (int64_t)blockIdx.x * 32, k00 = (int64_t)blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int j = ty; j < 32; j += 8) {
+    const int64_t k0 = k00 + j, c = c0 + tx;
+    double2 v = make_double2(0.0, 0.0);
+    if (k0 < L0 && c < NC) {
+      const int64_t col = compact_src ? c : (c <= H / 2 ? c : H + (c - H / 2 - 1));
+      v = F[(k0 * L1 + k1) * Ssrc + col];
+    }
+    tile[j][tx] = v;
+  }
+  __syncthreads();
+  for (int j = ty; j < 32; j += 8) {
+    const int64_t c = c0 + j, k0 = k00 + tx;
+    if (c < NC && k0 < L0) {
+      const double2 v = tile[tx][j];
+      const int64_t oi = (c * L1 + k1) * L0 + k0;
+      if constexpr (PAIR) {
+        a[oi] = (T)(v.x * scale);
+        b[oi] = (T)(v.y * scale);
+      } else {
+        reinterpret_cast<C2<T>*>(a)[oi] = mk<T>((T)(v.x * scale), (T)(v.y * scale));
+      }
+    }
+  }
+}
+template <typename T>
+void extract_t(const double2* F, void* a, void* b, int64_t L0, int64_t L1, int64_t H, int64_t Ssrc, int compact_src,
+               double scale, hipStream_t s) {
+  const dim3 grid((unsigned)((H + 1 + 31) / 32), (unsigned)((L0 + 31) / 32), (unsigned)L1);
+  if (b != nullptr)
+    hipLaunchKernelGGL((k_extract_t<T, true>), grid, dim3(256), 0, s, F, (T*)a, (T*)b, L0, L1, H + 1, Ssrc,
+                       compact_src, H, scale);
+  else
+    hipLaunchKernelGGL((k_extract_t<T, false>), grid, dim3(256), 0, s, F, (T*)a, (T*)nullptr, L0, L1, H + 1, Ssrc,
+                       compact_src, H, scale);
+}
+template void extract_t<float>(const double2*, void*, void*, int64_t, int64_t, int64_t, int64_t, int, double, hipStream_t);
+template void extract_t<double>(const double2*, void*, void*, int64_t, int64_t, int64_t, int64_t, int, double, hipStream_t);
+
 template void extract_pair<float>(const double2*, void*, void*, int64_t, int64_t, int64_t, int, double, hipStream_t, int64_t, int64_t);
 template void extract_pair<double>(const double2*, void*, void*, int64_t, int64_t, int64_t, int, double, hipStream_t, int64_t, int64_t);
 template void extract_cplx<float>(const double2*, void*, int64_t, int64_t, int64_t, int, double, hipStream_t, int64_t, int64_t);

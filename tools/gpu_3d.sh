@@ -10,3 +10,4 @@ timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout
 tail -1 gpurun_out/pytest_3d.log
 timeout -k 10 400 python -u tools/bench_configs.py --only ${CFGS:-C5,C4} > gpurun_out/cfg_3d.jsonl 2> gpurun_out/cfg_3d.err || { tail -20 gpurun_out/cfg_3d.err; exit 1; }
 cat gpurun_out/cfg_3d.jsonl
+timeout -k 10 300 python -u tools/kn_phases.py --only C5,C4 || exit 1
