@@ -261,24 +261,11 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
     return fail(HGP_E_UNSUPPORTED, "2-D grid too large: one right-hand side's intermediate exceeds 2 GiB");
   // RHS chunks: 2-D ops spread them over NS streams, chunk j on stream (and workspace slot)
   // j % NS; each chunk's RHS are processed entirely on its stream (no cross-stream data).
-  int NS = (d >= 2 && only_pass < 0) ? (int)std::min<int64_t>(std::max(1, P->nstreams), nrhs) : 1;
+  const int NS = (d >= 2 && only_pass < 0) ? (int)std::min<int64_t>(std::max(1, P->nstreams), nrhs) : 1;
   int64_t Qc = nrhs;
   if (B1 + B2 > 0) {
     const int64_t per = (B1 + B2) * (int64_t)cs;
-    int64_t budget = P->ws_budget;
-    // 3-D R / R^T on large grids: their complex spectrum (on the L_R grid) is as large as one
-    // RHS's intermediate, and the axis-0 pass shares it only between the RHS of one chunk.  Where
-    // the byte budget allows fewer than two RHS per chunk, these ops run on one stream in chunks
-    // of up to 8 RHS as device memory allows (C5 R^T: 38 -> 36 ms; 2-D C4 R^T lost its stream
-    // overlap that way, 36 -> 43 ms, and keeps the budget)
-    if (g.spec_kind != SPEC_REAL && d == 3 && !P->ws_explicit && nrhs > 1 && per * 2 > budget) {
-      size_t fr = 0, tot = 0;
-      if (hipMemGetInfo(&fr, &tot) == hipSuccess) {
-        NS = 1;
-        budget = std::max<int64_t>(budget, std::min<int64_t>(per * 8, (int64_t)(fr / 2)));
-      }
-    }
-    Qc = std::max<int64_t>(1, std::min<int64_t>((nrhs + NS - 1) / NS, budget / (per * NS)));
+    Qc = std::max<int64_t>(1, std::min<int64_t>((nrhs + NS - 1) / NS, P->ws_budget / (per * NS)));
     // Infinity-Cache-resident chunks: where 8 RHS of a 2-D intermediate fit in ~72 MiB, each
     // stream works on 8 RHS at a time, so the intermediate a column pass writes is still in the
     // 256 MiB Infinity Cache when the row-inverse pass reads it (C2: row inverse 4.2 -> 5.0 TB/s,

@@ -145,13 +145,28 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
   const int in_len = d.in.len;
 
   C2<T> va[P], vb[P];
-  // raw buffer loads: past the row length (zero padding) and for absent rows they return 0
-  const BufRsrc ra = buf_rsrc(in_a, pvalid ? (uint32_t)in_len * (uint32_t)sizeof(T) : 0u);
-  const BufRsrc rb_ = buf_rsrc(in_b, has2 ? (uint32_t)in_len * (uint32_t)sizeof(T) : 0u);
+  if constexpr (TT % 64 == 0) {
+    // raw buffer loads (the pair is wave-uniform): past the row length (zero padding) and for
+    // absent rows they return 0
+    const BufRsrc ra = buf_rsrc(in_a, pvalid ? (uint32_t)in_len * (uint32_t)sizeof(T) : 0u);
+    const BufRsrc rb_ = buf_rsrc(in_b, has2 ? (uint32_t)in_len * (uint32_t)sizeof(T) : 0u);
 #pragma unroll
-  for (int k = 0; k < P; ++k) {
-    const uint32_t lo = (uint32_t)t * (uint32_t)sizeof(T), so = (uint32_t)(TT * k * (int)sizeof(T));
-    va[k] = mk<T>(buf_ld<T>(ra, lo, so), buf_ld<T>(rb_, lo, so));
+    for (int k = 0; k < P; ++k) {
+      const uint32_t lo = (uint32_t)t * (uint32_t)sizeof(T), so = (uint32_t)(TT * k * (int)sizeof(T));
+      va[k] = mk<T>(buf_ld<T>(ra, lo, so), buf_ld<T>(rb_, lo, so));
+    }
+  } else {
+    // several pairs per wave: the row bases differ between lanes, and a buffer resource must be
+    // wave-uniform (a per-lane base costs a readfirstlane loop per load: 2x the VALU of the
+    // whole kernel at H = 128); plain loads at clamped positions, zeroed after
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+      const int p = t + TT * k;
+      const bool ok = p < in_len;
+      const T a = in_a[ok ? p : 0];
+      const T b = in_b[ok ? p : 0];
+      va[k] = mk<T>(ok && pvalid ? a : (T)0, ok && has2 ? b : (T)0);
+    }
   }
   __syncthreads();   // twiddle table staged
   C2<T>* W = reinterpret_cast<C2<T>*>(d.out.ptr) + (int64_t)q * d.out.q_stride;
