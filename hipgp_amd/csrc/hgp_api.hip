@@ -91,6 +91,7 @@ struct hgp_plan {
   size_t esz = 4;
   // tables
   DevBuf twK[3], twR[3], tw64K[3], tw64R[3];
+  DevBuf tw64Rh[3];                       // W_{L_R/2}^q for L_R/2 > 16384-point lines (fft_lines_f64)
   DevBuf bsPre[3], bsPost[3], bsFilt[3];   // Bluestein DCT-I tables per axis (fp64)
   // spectra
   DevBuf specK, specI, specR, Dm3;
@@ -116,7 +117,7 @@ struct hgp_plan {
 
   ~hgp_plan() {
     for (int a = 0; a < 3; ++a) {
-      twK[a].release(); twR[a].release(); tw64K[a].release(); tw64R[a].release();
+      twK[a].release(); twR[a].release(); tw64K[a].release(); tw64R[a].release(); tw64Rh[a].release();
       bsPre[a].release(); bsPost[a].release(); bsFilt[a].release();
     }
     DevBuf* bufs[] = {&specK, &specI, &specR, &Dm3, &nclamp, &ws1, &ws2, &set1, &set2, &setM1, &setM2, &setC,
@@ -500,45 +501,50 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
   return 0;
 }
 
+// Forward fp64 FFT of length L along lines r < Rn (stride r_stride) x inner lines i < In
+// (adjacent), positions at stride ps: in -> out (in may be clobbered), output in the pass
+// order (index half*L/2 + k = frequency 2k + half).  Lines of L/2 <= 8192 points are one k_pass;
+// longer ones (L_R = 32768 of an axis of 4098..8192 points) are one radix-2 step: the two
+// interleaved half-length subsequences transformed in place by a strided k_pass (twiddles
+// W_{L/2}, tw_half), then k_r2_combine into the order of the full length.
+int fft_lines_f64(hgp_plan* P, double2* in, double2* out, int64_t L, int64_t Rn, int64_t r_stride, int64_t In,
+                  int64_t ps, const void* tw, const void* tw_half) {
+  hipStream_t s = P->stream;
+  if (L / 2 <= 8192) {
+    PassDesc D = base_desc();
+    D.in = View{in, 0, r_stride, ps, (int)L};
+    D.out = View{out, 0, r_stride, ps, (int)L};
+    D.tw = tw; D.Q = 1; D.Rn = (int)Rn; D.In = (int)In;
+    if (ps == 1 && In == 1) return launch<double>((int)(L / 2), PASS_FWD, LAY_CONTIG, D, Rn, s);
+    return launch<double>((int)(L / 2), PASS_FWD, LAY_STRIDED, D, 0, s);
+  }
+  if (L / 2 > 16384 || tw_half == nullptr) return fail(HGP_E_UNSUPPORTED, "fp64 transform longer than 32768 points");
+  PassDesc D = base_desc();       // q = line r, r = subsequence e (offset e * ps), i = inner line
+  D.in = View{in, r_stride, ps, 2 * ps, (int)(L / 2)};
+  D.out = View{in, r_stride, ps, 2 * ps, (int)(L / 2)};
+  D.tw = tw_half; D.Q = (int)Rn; D.Rn = 2; D.In = (int)In;
+  HGP_TRY(launch<double>((int)(L / 4), PASS_FWD, LAY_STRIDED, D, 0, s));
+  r2_combine(in, out, L, Rn, r_stride, In, ps, reinterpret_cast<const double2*>(tw), s);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
 // Forward FFT of a full (unpruned) fp64 complex L-grid: a -> result pointer (a or b).
 int fwd_grid_f64(hgp_plan* P, const int64_t* L, const DevBuf* tw64, double2* a, double2* b, double2** result) {
   const int d = P->d;
-  hipStream_t s = P->stream;
+  const DevBuf* twh = (tw64 == P->tw64R) ? P->tw64Rh : nullptr;
+  auto half = [&](int ax) -> const void* { return twh ? twh[ax].ptr : nullptr; };
   if (d == 1) {
-    PassDesc D = base_desc();
-    D.in = View{a, L[0], 0, 1, (int)L[0]};
-    D.out = View{b, L[0], 0, 1, (int)L[0]};
-    D.tw = tw64[0].ptr; D.Q = 1; D.Rn = 1; D.In = 1;
-    HGP_TRY(launch<double>((int)(L[0] / 2), PASS_FWD, LAY_CONTIG, D, 1, s));
+    HGP_TRY(fft_lines_f64(P, a, b, L[0], 1, L[0], 1, 1, tw64[0].ptr, half(0)));
     *result = b;
   } else if (d == 2) {
-    PassDesc A = base_desc();
-    A.in = View{a, 0, L[1], 1, (int)L[1]};
-    A.out = View{b, 0, L[1], 1, (int)L[1]};
-    A.tw = tw64[1].ptr; A.Q = 1; A.Rn = (int)L[0]; A.In = 1;
-    HGP_TRY(launch<double>((int)(L[1] / 2), PASS_FWD, LAY_CONTIG, A, L[0], s));
-    PassDesc Bd = base_desc();
-    Bd.in = View{b, 0, 0, L[1], (int)L[0]};
-    Bd.out = View{a, 0, 0, L[1], (int)L[0]};
-    Bd.tw = tw64[0].ptr; Bd.Q = 1; Bd.Rn = 1; Bd.In = (int)L[1];
-    HGP_TRY(launch<double>((int)(L[0] / 2), PASS_FWD, LAY_STRIDED, Bd, 0, s));
+    HGP_TRY(fft_lines_f64(P, a, b, L[1], L[0], L[1], 1, 1, tw64[1].ptr, half(1)));
+    HGP_TRY(fft_lines_f64(P, b, a, L[0], 1, 0, L[1], L[1], tw64[0].ptr, half(0)));
     *result = a;
   } else {
-    PassDesc A = base_desc();
-    A.in = View{a, 0, L[2], 1, (int)L[2]};
-    A.out = View{b, 0, L[2], 1, (int)L[2]};
-    A.tw = tw64[2].ptr; A.Q = 1; A.Rn = (int)(L[0] * L[1]); A.In = 1;
-    HGP_TRY(launch<double>((int)(L[2] / 2), PASS_FWD, LAY_CONTIG, A, L[0] * L[1], s));
-    PassDesc Bd = base_desc();
-    Bd.in = View{b, 0, L[1] * L[2], L[2], (int)L[1]};
-    Bd.out = View{a, 0, L[1] * L[2], L[2], (int)L[1]};
-    Bd.tw = tw64[1].ptr; Bd.Q = 1; Bd.Rn = (int)L[0]; Bd.In = (int)L[2];
-    HGP_TRY(launch<double>((int)(L[1] / 2), PASS_FWD, LAY_STRIDED, Bd, 0, s));
-    PassDesc Cd = base_desc();
-    Cd.in = View{a, 0, 0, L[1] * L[2], (int)L[0]};
-    Cd.out = View{b, 0, 0, L[1] * L[2], (int)L[0]};
-    Cd.tw = tw64[0].ptr; Cd.Q = 1; Cd.Rn = 1; Cd.In = (int)(L[1] * L[2]);
-    HGP_TRY(launch<double>((int)(L[0] / 2), PASS_FWD, LAY_STRIDED, Cd, 0, s));
+    HGP_TRY(fft_lines_f64(P, a, b, L[2], L[0] * L[1], L[2], 1, 1, tw64[2].ptr, half(2)));
+    HGP_TRY(fft_lines_f64(P, b, a, L[1], L[0], L[1] * L[2], L[2], L[2], tw64[1].ptr, half(1)));
+    HGP_TRY(fft_lines_f64(P, a, b, L[0], 1, 0, L[1] * L[2], L[1] * L[2], tw64[0].ptr, half(0)));
     *result = b;
   }
   return 0;
@@ -704,15 +710,23 @@ int set_column_t(hgp_plan* P, const void* column, double jitter, double clamp_mi
                  1.0 / (double)P->prodLK, s);
   for (int ax = 0; ax < 3; ++ax) gd.L[ax] = P->LR[ax];
   HGP_TRY(P->specR.ensure((size_t)nR * sizeof(C2<T>)));
+  bool long_r = false;
+  for (int ax = 0; ax < d; ++ax) long_r = long_r || P->LR[ax] / 2 > 8192;
   if (d == 1) {
     embed_R(sv, g1, gd, s);
     HGP_TRY(fwd_grid_f64(P, P->LR, P->tw64R, g1, g2, &F));
     extract_cplx<T>(F, P->specR.ptr, nR, LRl, SR, compact, 1.0 / (double)P->prodLR, s);
-  } else {
+  } else if (!long_r) {
     // the R filter is real: real row-pair transform of the last axis, compact columns only after
     embed_R_real(sv, reinterpret_cast<double*>(g1), gd, s);
     HGP_TRY(fwd_grid_real_f64(P, P->LR, P->tw64R, reinterpret_cast<const double*>(g1), g2, SR));
     extract_t<T>(g2, P->specR.ptr, nullptr, P->LR[0], d == 3 ? P->LR[1] : 1, LRl / 2, SR, 1,
+                 1.0 / (double)P->prodLR, s);
+  } else {
+    // an axis of L_R > 16384 points: the full complex grid through fft_lines_f64's radix-2 step
+    embed_R(sv, g1, gd, s);
+    HGP_TRY(fwd_grid_f64(P, P->LR, P->tw64R, g1, g2, &F));
+    extract_t<T>(F, P->specR.ptr, nullptr, P->LR[0], d == 3 ? P->LR[1] : 1, LRl / 2, LRl, 0,
                  1.0 / (double)P->prodLR, s);
   }
   HIP_TRY(hipGetLastError());
@@ -1049,7 +1063,14 @@ int hgp_plan_create(int device, int ndim, const int64_t* m, int dtype, int64_t m
   P->d = d;
   if (d == 0) { delete P; return fail(HGP_E_UNSUPPORTED, "a grid with every axis of size 1 (M = 1) is not supported"); }
   for (int a = 0; a < d; ++a) {
-    if (P->LR[a] / 2 > 8192) { delete P; return fail(HGP_E_UNSUPPORTED, "grid axis longer than 4097 points is not supported yet"); }
+    // L_R / 2 = 16384 (axes of 4098..8192 points): fp32 operator passes hold one such line per
+    // block; fp64 lines of 16384 points exceed one CU's LDS (the set-up's fp64 transforms of
+    // them take fft_lines_f64's radix-2 step)
+    if (P->LR[a] / 2 > 16384 || P->LK[a] / 2 > 8192 || (dtype == HGP_F64 && P->LR[a] / 2 > 8192)) {
+      delete P;
+      return fail(HGP_E_UNSUPPORTED, dtype == HGP_F64 ? "fp64 plans support grid axes of up to 4097 points (fp32: 8192)"
+                                                      : "grid axis longer than 8192 points is not supported");
+    }
     P->M *= P->m[a];
     P->Mp *= P->n[a];
     P->prodLK *= P->LK[a];
@@ -1069,6 +1090,7 @@ int hgp_plan_create(int device, int ndim, const int64_t* m, int dtype, int64_t m
       if (!rc) rc = upload_twiddles<float>(P->twR[a], P->LR[a]);
     }
     if (!rc) rc = upload_twiddles<double>(P->tw64K[a], P->LK[a]);
+    if (!rc && P->LR[a] / 2 > 8192) rc = upload_twiddles<double>(P->tw64Rh[a], P->LR[a] / 2);
     if (!rc) rc = upload_twiddles<double>(P->tw64R[a], P->LR[a]);
     if (!rc) rc = make_bluestein(P, a);
   }
@@ -1511,7 +1533,7 @@ int hgp_plan_info(const hgp_plan* plan, int64_t* M, int64_t* Mprime, int64_t* L_
 
 int64_t plan_scratch_bytes(const hgp_plan* P) {
   const DevBuf* bufs[] = {&P->ws1, &P->ws2, &P->set1, &P->set2, &P->setM1, &P->setM2, &P->setC, &P->r, &P->z,
-                          &P->p, &P->Ap, &P->part_op, &P->part_u, &P->scal, &P->bT, &P->xT};
+                          &P->p, &P->Ap, &P->part_op, &P->part_u, &P->part_f, &P->scal, &P->bT, &P->xT};
   int64_t b = 0;
   for (const DevBuf* d : bufs) b += (int64_t)d->bytes;
   return b;
@@ -1539,8 +1561,8 @@ int hgp_plan_trim(hgp_plan* plan) {
   for (int i = 0; i < 3; ++i)
     if (plan->side[i]) HIP_TRY(hipStreamSynchronize(plan->side[i]));
   DevBuf* bufs[] = {&plan->ws1, &plan->ws2, &plan->set1, &plan->set2, &plan->setM1, &plan->setM2, &plan->setC,
-                    &plan->r, &plan->z, &plan->p, &plan->Ap, &plan->part_op, &plan->part_u, &plan->scal,
-                    &plan->bT, &plan->xT};
+                    &plan->r, &plan->z, &plan->p, &plan->Ap, &plan->part_op, &plan->part_u, &plan->part_f,
+                    &plan->scal, &plan->bT, &plan->xT};
   for (DevBuf* b : bufs) b->release();
   return 0;
 }

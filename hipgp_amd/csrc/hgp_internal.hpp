@@ -38,6 +38,8 @@ void clamp_spectrum(const double* Draw, double* out3, int64_t M, double clamp_mi
 void embed_K(const double* cK, const double* cI, double2* out, const GridDims& g, hipStream_t s);
 void embed_R(const double* sv, double2* out, const GridDims& g, hipStream_t s);
 void embed_R_real(const double* sv, double* out, const GridDims& g, hipStream_t s);
+void r2_combine(const double2* in, double2* out, int64_t L, int64_t Rn, int64_t r_stride, int64_t In, int64_t ps,
+                const double2* tw, hipStream_t s);
 // d >= 2: tiled transposing extraction into [c][k1][k0] (hgp_kernels.hip k_extract_t); b == nullptr:
 // complex spectrum into a, else the pair (Re -> a, Im -> b)
 template <typename T>

@@ -155,6 +155,34 @@ __global__ void k_embed_R(const double* __restrict__ s, double2* __restrict__ ou
   out[idx] = v;
 }
 
+// Radix-2 step of fft_lines_f64: the two interleaved half-length subsequences of every line
+// (e = 0, 1 at offsets e * ps, positions at 2 ps) hold their length-L/2 spectra in pass order;
+// X[f] = E[f'] +- W_L^f' O[f'] (f' = f mod L/2), written in the pass order of length L.
+__global__ void k_r2_combine(const double2* __restrict__ in, double2* __restrict__ out, int64_t L, int64_t Rn,
+                             int64_t r_stride, int64_t In, int64_t ps, const double2* __restrict__ tw) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t half_len = L / 2, Hp = L / 4;
+  if (t >= Rn * In * half_len) return;
+  const int64_t i = t % In, rest = t / In;
+  const int64_t idx = rest % half_len, r = rest / half_len;
+  const int64_t base = r * r_stride + i;
+  const int64_t hp = idx / Hp, kp = idx - hp * Hp;
+  const int64_t f = 2 * kp + hp;
+  const double2 E = in[base + (2 * idx) * ps];
+  const double2 O = in[base + (2 * idx + 1) * ps];
+  const double2 w = tw[f];
+  const double2 wo = make_double2(w.x * O.x - w.y * O.y, w.x * O.y + w.y * O.x);
+  const int64_t oa = hp * half_len + kp;
+  out[base + oa * ps] = make_double2(E.x + wo.x, E.y + wo.y);
+  out[base + (oa + half_len / 2) * ps] = make_double2(E.x - wo.x, E.y - wo.y);
+}
+void r2_combine(const double2* in, double2* out, int64_t L, int64_t Rn, int64_t r_stride, int64_t In, int64_t ps,
+                const double2* tw, hipStream_t s) {
+  const int64_t total = Rn * In * (L / 2);
+  hipLaunchKernelGGL(k_r2_combine, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, in, out, L, Rn, r_stride, In,
+                     ps, tw);
+}
+
 // the same R filter as a REAL grid (the set-up transforms it with the real row-pair pass)
 __global__ void k_embed_R_real(const double* __restrict__ s, double* __restrict__ out, GridDims g, int64_t total) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;

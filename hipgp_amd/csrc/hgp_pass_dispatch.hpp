@@ -1,6 +1,8 @@
 // hgp_pass_dispatch.hpp — instantiation + launch of k_pass for one dtype (included by
 // hgp_pass_f32.hip / hgp_pass_f64.hip so the two compile in parallel).
 #pragma once
+#include <type_traits>
+
 #include "hgp_internal.hpp"
 #include "hgp_rows.hpp"
 #include "hgp_lines.hpp"
@@ -64,6 +66,9 @@ static PassGeom geom_h(int lay) {
     case 512: return FN<T, 512>(__VA_ARGS__);   case 1024: return FN<T, 1024>(__VA_ARGS__);         \
     case 2048: return FN<T, 2048>(__VA_ARGS__); case 4096: return FN<T, 4096>(__VA_ARGS__);         \
     case 8192: return FN<T, 8192>(__VA_ARGS__);                                                      \
+    case 16384:   /* fp32 only: one 16384-point fp64 line exceeds one CU's LDS */                     \
+      if constexpr (std::is_same<T, float>::value) return FN<T, 16384>(__VA_ARGS__);                 \
+      break;                                                                                         \
     default: break;                                                                                  \
   }
 

@@ -1,0 +1,70 @@
+"""Grid axes longer than 4097 points (the reference has no length limit, `toeplitz_tensor.py:85-97`).
+
+An axis of m in 4098..8192 points needs L_R = 32768-point transforms for R / R^T: fp32 plans run
+them as one-line-per-block passes (H = 16384), and the fp64 set-up of every plan transforms
+the L_R grid with fft_lines_f64's radix-2 step (two 16384-point halves + k_r2_combine).  Here
+the fp32 operators and PCG of 1-D / 2-D grids with such an axis (last or first) are checked
+against the fp64 oracle of the same column; fp64 plans of those sizes are refused cleanly
+(one 16384-point fp64 line exceeds a CU's LDS), as are axes beyond 8192 points."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ziggy_oracle as zo
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+CASES = {"1d_5000": (5000,), "2d_4200x12": (4200, 12), "2d_10x4500": (10, 4500)}
+
+
+def _column(dims):
+    # Matern-3/2 with ell = 20 grid spacings, nugget 0.1: a well-conditioned K
+    grids = [np.linspace(-1, 1, m) for m in dims]
+    ell = 40.0 / max(dims)
+    return zo.toeplitz_column(grids, lambda x, y: zo.kernel_eval("matern", x, y, (1.0, ell), nu=1.5), 0.1)
+
+
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_long_axis_ops_and_pcg_fp32(case):
+    from hipgp_amd import _lib
+    from hipgp_amd.plan import ToeplitzPlan
+    dims = CASES[case]
+    col = _column(dims)
+    O = zo.ToeplitzOracle(col, dims)
+    P = ToeplitzPlan(dims, torch.float32, DEV)
+    P.set_column(torch.tensor(col, device=DEV, dtype=torch.float32))
+    M, Mp = O.M, O.Mp
+    rs = np.random.RandomState(3)
+    v = rs.randn(3, M)
+    w = rs.randn(3, Mp)
+    for name, op, x, ref in (("K", _lib.OP_K, v, O.matmul_K(v)), ("Cinv", _lib.OP_CINV, v, O.matmul_Cinv(v)),
+                             ("RT", _lib.OP_RT, v, O.matmul_RT(v)), ("R", _lib.OP_R, w, O.matmul_R(w))):
+        got = P.apply(op, torch.tensor(x, device=DEV, dtype=torch.float32)).double().cpu().numpy()
+        assert got.shape == ref.shape, name
+        err = float(np.abs(got - ref).max() / np.abs(ref).max())
+        # fp32 transforms of up to 32768 points: a few ulp of log2(L) ~ 15 stages
+        assert err < 2e-5, (name, err)
+    b = rs.randn(2, M)
+    x_ref = O.solve(b, do_precond=True, maxiter=10, tol=1e-30)
+    x_ref32 = zo.ToeplitzOracle(col.astype(np.float32), dims).solve(b.astype(np.float32), do_precond=True,
+                                                                     maxiter=10, tol=1e-30)
+    x = P.pcg(torch.tensor(b, device=DEV, dtype=torch.float32), 10, 1e-30, precond=True).double().cpu().numpy()
+    e = np.linalg.norm(x - x_ref) / np.linalg.norm(x_ref)
+    e_ref = np.linalg.norm(x_ref32.astype(np.float64) - x_ref) / np.linalg.norm(x_ref)
+    assert e <= 4 * e_ref + 1e-6, (e, e_ref)        # SURVEY §8(c) fp32 PCG bound
+    # the whitening identity on the same grid: R (R^T v) = K v
+    vt = torch.tensor(v, device=DEV, dtype=torch.float32)
+    rr = P.apply(_lib.OP_R, P.apply(_lib.OP_RT, vt)).double().cpu().numpy()
+    kv = O.matmul_K(v)
+    assert float(np.abs(rr - kv).max() / np.abs(kv).max()) < 3e-5
+
+
+def test_long_axis_refusals():
+    from hipgp_amd import _lib
+    from hipgp_amd.plan import ToeplitzPlan
+    with pytest.raises(_lib.HipgpError, match="fp64 plans support grid axes of up to 4097"):
+        ToeplitzPlan((4200, 12), torch.float64, DEV)
+    with pytest.raises(_lib.HipgpError, match="longer than 8192"):
+        ToeplitzPlan((8193,), torch.float32, DEV)
+    ToeplitzPlan((4097, 3), torch.float64, DEV)        # the fp64 limit itself is accepted
