@@ -3,7 +3,7 @@
 An axis of m in 4098..8192 points needs L_R = 32768-point transforms for R / R^T: fp32 plans run
 them as one-line-per-block passes (H = 16384), and the fp64 set-up of every plan transforms
 the L_R grid with fft_lines_f64's radix-2 step (two 16384-point halves + k_r2_combine).  Here
-the fp32 operators and PCG of 1-D / 2-D grids with such an axis (last or first) are checked
+the fp32 operators and PCG of 1-D / 2-D / 3-D grids with such an axis (any position) are checked
 against the fp64 oracle of the same column; fp64 plans of those sizes are refused cleanly
 (one 16384-point fp64 line exceeds a CU's LDS), as are axes beyond 8192 points."""
 import numpy as np
@@ -15,7 +15,8 @@ from oracle import ziggy_oracle as zo
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
-CASES = {"1d_5000": (5000,), "2d_4200x12": (4200, 12), "2d_10x4500": (10, 4500)}
+CASES = {"1d_5000": (5000,), "2d_4200x12": (4200, 12), "2d_10x4500": (10, 4500),
+         "3d_4100x5x4": (4100, 5, 4), "3d_4x4100x3": (4, 4100, 3), "3d_3x5x4300": (3, 5, 4300)}
 
 
 def _column(dims):
