@@ -55,7 +55,7 @@ def parse():
     return ap.parse_args()
 
 
-PMC_FILE = os.path.join(ROOT, "profiles", "pmc_kop_C2.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r2_pmc_kop_C2.json")   # tools/pmc_kop.sh, this round
 
 
 def pmc_traffic(M, B):
@@ -302,7 +302,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(M, B),
                      "achieved_note": "bytes_per_launch / ms_per_step (the timed steps' own clock)",
-                     "traffic_note": "HBM bytes per batched K matvec from profiles/pmc_kop_C2.json "
+                     "traffic_note": "HBM bytes per batched K matvec from profiles/r2_pmc_kop_C2.json "
                                      "(rocprofv3 --pmc, 2*FETCH_SIZE + WRITE_SIZE); algorithmic "
                                      "bytes per launch = bytes_per_launch",
                      "kernel": "batched K matvec = 3 pass kernels (FWD rows, CONV cols, INV rows)",
