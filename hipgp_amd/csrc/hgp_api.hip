@@ -683,7 +683,10 @@ int set_column_t(hgp_plan* P, const void* column, double jitter, double clamp_mi
   const double* cI = src + M;
   const double* sv = src + 2 * M;
   // operator spectra on the power-of-two grids
-  const int64_t big = std::max(P->prodLK, P->prodLR);
+  // the compact R grid of fwd_grid_real_f64 has a last axis of compact_stride(L) >= L/2 + 1
+  // columns, more than L itself when L = 4 (an axis of 2 points)
+  const int64_t Lr_last = P->LR[d - 1];
+  const int64_t big = std::max({P->prodLK, P->prodLR, P->prodLR / Lr_last * compact_stride(Lr_last)});
   HGP_TRY(P->set1.ensure((size_t)big * sizeof(double2)));
   HGP_TRY(P->set2.ensure((size_t)big * sizeof(double2)));
   double2* g1 = reinterpret_cast<double2*>(P->set1.ptr);

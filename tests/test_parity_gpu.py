@@ -300,3 +300,47 @@ def test_generic_2d_sequence_fp64(dims):
     assert rel_err(_np(P.apply(_lib.OP_RT, vt)), T.matmul_RT(v)) < 1e-11
     assert rel_err(_np(P.apply(_lib.OP_R, torch.tensor(w, device=DEV))), T.matmul_R(w)) < 1e-11
     assert rel_err(_np(P.apply(_lib.OP_K, vt)), T.matmul_K(v)) < 1e-11
+
+
+# ---- seeded shape sweep: edge shapes of every pass sequence ---------------------------------
+# tiny axes (H = 2: one-point half spectra), odd sizes, size-1 axes in every position, 3-D
+# planes whose row pairs / line tiles are ragged (hgp_lines.hpp), long-and-thin grids; fp64 to
+# 1e-10 and fp32 within the SURVEY §8(c) rules, ops and the fused PCG (2-D / 3-D epilogues).
+SWEEP = [(2,), (3,), (2, 2), (3, 2), (2, 5), (2, 2, 2), (3, 2, 5), (2, 17, 3), (5, 40, 2), (7, 3, 130),
+         (65, 9, 33), (129, 3, 2), (1, 6, 1), (31, 1, 9), (4, 4, 1), (200, 3), (3, 200), (17, 18, 19)]
+
+
+@pytest.mark.parametrize("dims", SWEEP, ids=lambda d: "x".join(map(str, d)))
+@pytest.mark.parametrize("tag", ["f64", "f32"])
+def test_shape_sweep_vs_oracle(dims, tag):
+    from hipgp_amd import _lib
+    from hipgp_amd.plan import ToeplitzPlan
+    dt = torch.float64 if tag == "f64" else torch.float32
+    grids = [np.linspace(-1, 1, m) for m in dims]
+    ell = 4.0 / max(dims)
+    col = zo.toeplitz_column(grids, lambda x, y: zo.kernel_eval("matern", x, y, (1., ell), nu=1.5), 0.05)
+    O = zo.ToeplitzOracle(col, dims)
+    P = ToeplitzPlan(dims, dt, DEV)
+    P.set_column(torch.tensor(col, device=DEV, dtype=dt))
+    rs = np.random.RandomState(sum(dims))
+    v = rs.randn(3, O.M)
+    w = rs.randn(3, O.Mp)
+    tol = 1e-10 if tag == "f64" else 2e-5
+    for name, op, x, ref in (("K", _lib.OP_K, v, O.matmul_K(v)), ("Cinv", _lib.OP_CINV, v, O.matmul_Cinv(v)),
+                             ("RT", _lib.OP_RT, v, O.matmul_RT(v)), ("R", _lib.OP_R, w, O.matmul_R(w))):
+        got = _np(P.apply(op, torch.tensor(x, device=DEV, dtype=dt))).astype(np.float64)
+        assert got.shape == ref.shape, name
+        assert float(np.abs(got - ref).max() / np.abs(ref).max()) < tol, name
+    b = rs.randn(2, O.M)
+    it = min(8, max(1, O.M - 1))    # short of an exhausted Krylov space (r = 0 -> 0/0 in cg.py:66 too)
+    xr = O.solve(b, True, it, 1e-30)
+    x = _np(P.pcg(torch.tensor(b, device=DEV, dtype=dt), it, 1e-30, precond=True)).astype(np.float64)
+    e = np.linalg.norm(x - xr) / np.linalg.norm(xr)
+    if tag == "f64":
+        assert e < 1e-8, e
+    else:
+        x32 = zo.ToeplitzOracle(col.astype(np.float32), dims).solve(b.astype(np.float32), True, it, 1e-30)
+        e32 = np.linalg.norm(x32.astype(np.float64) - xr) / np.linalg.norm(xr)
+        if not np.isfinite(e32):    # the fp32 reference itself hit 0/0 on a nearly exhausted Krylov space
+            e32 = 2.5e-5
+        assert e <= 4 * e32 + 1e-6, (e, e32)
