@@ -84,6 +84,16 @@ def test_solves_vs_golden(name, tag):
         else:
             ok, (e, eref) = pcg_ok(x, f32[key], f64[key])
             assert ok or chaotic, (key, e, eref)
+        if chaotic:
+            # eigenvalues at the 1e-6 clamp: 20 iterations amplify rounding chaotically, so two
+            # implementations' iterates differ; what they share is how far they got -- the true
+            # residual |K x - b| (fp64 oracle K) of ours is within 3x of the reference's own (the
+            # reference's is 0.3-12 |b| after 20 iterations here: neither has converged)
+            O = zo.ToeplitzOracle(_np(T.column).astype(np.float64), T.dims)
+            b64 = fx["v"].astype(np.float64)
+            res = lambda y: float(np.linalg.norm(O.matmul_K(y.astype(np.float64)) - b64) / np.linalg.norm(b64))
+            ref = max(res(f64[key]), res(f32[key])) if tag == "f32" else res(f64[key])
+            assert res(x) <= 3 * ref + 1e-12, (key, res(x), ref)
     x = _np(T._solve(v, do_precond=False, maxiter=5, tol=1e-8))
     if tag == "f64":
         assert rel_err(x, f64["solve_p0_it5"]) < 1e-8
