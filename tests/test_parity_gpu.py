@@ -117,6 +117,16 @@ def test_gram_solve_config1(tag):
     kf = lambda x, y: k.forward(x, y, params=(1., .1))
     g = torch.tensor(fx["grid0"], device=DEV)
     vec = torch.tensor(fx["vec"], device=DEV)
+    g64 = np.asarray(fx["grid0"], np.float64)
+    O = zo.ToeplitzOracle(zo.toeplitz_column([g64], lambda x, y: zo.kernel_eval("matern", x, y, (1., .1), nu=2.5), 0.0),
+                          (len(g64),))
+    b64 = np.asarray(fx["vec"], np.float64)
+
+    def Kres(x):      # gram_solve works on vec.t(): rows of x / b are the RHS
+        x = np.asarray(x, np.float64)
+        xr, br = (x, b64) if x.shape == b64.shape else (x.T, b64.T)
+        return float(np.linalg.norm(O.matmul_K(np.ascontiguousarray(xr)) - br) / np.linalg.norm(br))
+
     for pre in (0, 1):
         for rt in (0, 1):
             for mi in (1, 5, 20):
@@ -131,6 +141,11 @@ def test_gram_solve_config1(tag):
                     tol = 1e-5 if pre else 1e-3
                     assert rel_err(res, fx[key]) < tol, (key, rel_err(res, fx[key]))
                     assert len(its) == int(fx[key + "_ncb"]), (key, len(its))
+                    if not rt:
+                        # and the true residual |K x - b| (oracle K of the same column) agrees
+                        # with the reference's own to 1 % (or 1e-8 of |b| once converged)
+                        r_ours, r_ref = Kres(res), Kres(fx[key])
+                        assert abs(r_ours - r_ref) <= 1e-2 * r_ref + 1e-8, (key, r_ours, r_ref)
                 else:
                     ok, (e, eref) = pcg_ok(res, fx[key], f64[key])
                     assert ok, (key, e, eref)
