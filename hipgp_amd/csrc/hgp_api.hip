@@ -114,8 +114,32 @@ struct hgp_plan {
   int nstreams = 2;
   hipStream_t side[3] = {nullptr, nullptr, nullptr};
   hipEvent_t ev_fork = nullptr, ev_join[3] = {nullptr, nullptr, nullptr};
+  // hipGraph of a repeated hgp_toeplitz_apply (same op, buffers, RHS count, workspaces, stream):
+  // the second identical call is captured, later ones replay it (no per-kernel launch gaps)
+  struct ApplyKey {
+    int op = -1;
+    const void* x = nullptr;
+    void* y = nullptr;
+    int64_t nrhs = 0;
+    hipStream_t stream = nullptr;
+    void *ws1 = nullptr, *ws2 = nullptr;
+    bool operator==(const ApplyKey& o) const {
+      return op == o.op && x == o.x && y == o.y && nrhs == o.nrhs && stream == o.stream && ws1 == o.ws1 && ws2 == o.ws2;
+    }
+  };
+  ApplyKey last_apply, graph_key;
+  hipGraphExec_t graph_exec = nullptr;
+  hipStream_t cap_stream = nullptr;       // captures run here (torch's default stream cannot capture)
+  bool use_graphs = true;
+  void drop_graph() {
+    if (graph_exec) (void)hipGraphExecDestroy(graph_exec);
+    graph_exec = nullptr;
+    graph_key = ApplyKey();
+  }
 
   ~hgp_plan() {
+    drop_graph();
+    if (cap_stream) (void)hipStreamDestroy(cap_stream);
     for (int a = 0; a < 3; ++a) {
       twK[a].release(); twR[a].release(); tw64K[a].release(); tw64R[a].release(); tw64Rh[a].release();
       bsPre[a].release(); bsPost[a].release(); bsFilt[a].release();
@@ -1081,6 +1105,8 @@ int hgp_plan_create(int device, int ndim, const int64_t* m, int dtype, int64_t m
   }
   const char* wb = std::getenv("HGP_WS_MB");
   if (wb) { P->ws_budget = (int64_t)std::atoll(wb) << 20; P->ws_explicit = true; }
+  const char* hg = std::getenv("HGP_GRAPH");
+  if (hg && std::atoi(hg) == 0) P->use_graphs = false;
   const char* ns = std::getenv("HGP_STREAMS");
   if (ns) P->nstreams = std::max(1, std::min(4, std::atoi(ns)));
   int rc = 0;
@@ -1128,7 +1154,51 @@ int hgp_toeplitz_apply(hgp_plan* plan, int op, const void* x, void* y, int64_t n
   if (x == y) return fail(HGP_E_ARG, "x and y must not alias");
   if (nrhs == 0) return 0;
   HGP_TRY(use_device(plan));
-  return DISPATCH(plan, run_op, plan, op, x, y, nrhs, nullptr, nullptr, nullptr);
+  hgp_plan* P = plan;
+  hgp_plan::ApplyKey key;
+  key.op = op; key.x = x; key.y = y; key.nrhs = nrhs; key.stream = P->stream; key.ws1 = P->ws1.ptr; key.ws2 = P->ws2.ptr;
+  if (!P->use_graphs || P->d < 2) return DISPATCH(plan, run_op, plan, op, x, y, nrhs, nullptr, nullptr, nullptr);
+  if (P->graph_exec != nullptr && key == P->graph_key) {
+    HIP_TRY(hipGraphLaunch(P->graph_exec, P->stream));
+    return 0;
+  }
+  if (!(key == P->last_apply)) {
+    // first call with these arguments: run it directly (workspaces are allocated here, so a
+    // later capture never allocates); remember the workspaces it ended with
+    HGP_TRY(DISPATCH(plan, run_op, plan, op, x, y, nrhs, nullptr, nullptr, nullptr));
+    key.ws1 = P->ws1.ptr; key.ws2 = P->ws2.ptr;
+    P->last_apply = key;
+    return 0;
+  }
+  // second identical call: capture the op's launches (all streams, fork/join events) once, on
+  // the plan's capture stream (the graph is then launched on the caller's stream)
+  P->drop_graph();
+  if (P->cap_stream == nullptr) HIP_TRY(hipStreamCreateWithFlags(&P->cap_stream, hipStreamNonBlocking));
+  hipGraph_t graph = nullptr;
+  hipStream_t user = P->stream;
+  HIP_TRY(hipStreamBeginCapture(P->cap_stream, hipStreamCaptureModeThreadLocal));
+  P->stream = P->cap_stream;
+  const int rc = DISPATCH(plan, run_op, plan, op, x, y, nrhs, nullptr, nullptr, nullptr);
+  P->stream = user;
+  const hipError_t ec = hipStreamEndCapture(P->cap_stream, &graph);
+  if (rc != 0 || ec != hipSuccess || graph == nullptr) {
+    if (graph) (void)hipGraphDestroy(graph);
+    P->use_graphs = false;                      // fall back to direct launches for this plan
+    (void)hipGetLastError();
+    return rc != 0 ? rc : DISPATCH(plan, run_op, plan, op, x, y, nrhs, nullptr, nullptr, nullptr);
+  }
+  hipGraphExec_t exec = nullptr;
+  const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(graph);
+  if (ei != hipSuccess) {
+    P->use_graphs = false;
+    (void)hipGetLastError();
+    return DISPATCH(plan, run_op, plan, op, x, y, nrhs, nullptr, nullptr, nullptr);
+  }
+  P->graph_exec = exec;
+  P->graph_key = key;
+  HIP_TRY(hipGraphLaunch(exec, P->stream));
+  return 0;
 }
 
 int hgp_toeplitz_apply_pass(hgp_plan* plan, int op, const void* x, void* y, int64_t nrhs, int pass) {
@@ -1567,6 +1637,8 @@ int hgp_plan_trim(hgp_plan* plan) {
                     &plan->r, &plan->z, &plan->p, &plan->Ap, &plan->part_op, &plan->part_u, &plan->part_f,
                     &plan->scal, &plan->bT, &plan->xT};
   for (DevBuf* b : bufs) b->release();
+  plan->drop_graph();                               // its kernels addressed the freed workspaces
+  plan->last_apply = hgp_plan::ApplyKey();
   return 0;
 }
 

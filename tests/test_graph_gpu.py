@@ -1,0 +1,61 @@
+"""Repeated hgp_toeplitz_apply calls replay a captured hipGraph (the second identical call is
+captured, later ones launch the graph): results are bitwise those of direct launches (a plan
+created with HGP_GRAPH=0), across ops, 2-D / 3-D, chunked RHS on two streams, and after the
+arguments, the workspace or the stream change."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ziggy_oracle as zo
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _plans(dims, dt):
+    from hipgp_amd.plan import ToeplitzPlan
+    grids = [np.linspace(-1, 1, m) for m in dims]
+    col = torch.tensor(zo.toeplitz_column(grids, lambda x, y: zo.kernel_eval("sqexp", x, y, (1., .2)), 1e-2),
+                       device=DEV, dtype=dt)
+    P = ToeplitzPlan(dims, dt, DEV)
+    P.set_column(col)
+    os.environ["HGP_GRAPH"] = "0"
+    try:
+        Q = ToeplitzPlan(dims, dt, DEV)
+    finally:
+        del os.environ["HGP_GRAPH"]
+    Q.set_column(col)
+    return P, Q
+
+
+@pytest.mark.parametrize("dims,dt", [((96, 80), torch.float32), ((40, 24, 20), torch.float64), ((1024, 1024), torch.float32)],
+                         ids=["2d_f32", "3d_f64", "C2_f32"])
+def test_graph_replay_bitwise(dims, dt):
+    from hipgp_amd import _lib
+    P, Q = _plans(dims, dt)
+    M = int(np.prod(dims))
+    Mp = int(np.prod([2 * m - 2 for m in dims]))
+    g = torch.Generator(device=DEV).manual_seed(5)
+    for nrhs in (3, 17):
+        x = torch.randn(nrhs, M, device=DEV, generator=g, dtype=dt)
+        w = torch.randn(nrhs, Mp, device=DEV, generator=g, dtype=dt)
+        for op, v in ((_lib.OP_K, x), (_lib.OP_CINV, x), (_lib.OP_RT, x), (_lib.OP_R, w)):
+            ref = Q.apply(op, v)
+            y = torch.empty_like(ref)
+            for rep in range(4):                   # direct, captured, replayed, replayed
+                y.zero_()
+                P.apply(op, v, out=y)
+                assert torch.equal(y, ref), (op, nrhs, rep)
+            v2 = v * 2                              # new input buffer: not the captured graph
+            assert torch.equal(P.apply(op, v2), Q.apply(op, v2)), (op, "new args")
+    # a new stream: the plan rebinds, the cached graph (other stream) is not replayed
+    s = torch.cuda.Stream(device=DEV)
+    with torch.cuda.stream(s):
+        y = torch.empty_like(x)
+        for _ in range(3):
+            P.apply(_lib.OP_K, x, out=y)
+        ref = Q.apply(_lib.OP_K, x)
+    s.synchronize()
+    assert torch.equal(y, ref)
