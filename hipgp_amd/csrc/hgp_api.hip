@@ -1157,7 +1157,11 @@ int hgp_toeplitz_apply(hgp_plan* plan, int op, const void* x, void* y, int64_t n
   hgp_plan* P = plan;
   hgp_plan::ApplyKey key;
   key.op = op; key.x = x; key.y = y; key.nrhs = nrhs; key.stream = P->stream; key.ws1 = P->ws1.ptr; key.ws2 = P->ws2.ptr;
-  if (!P->use_graphs || P->d < 2) return DISPATCH(plan, run_op, plan, op, x, y, nrhs, nullptr, nullptr, nullptr);
+  // a caller that is itself capturing (e.g. torch.cuda.graphs) records our launches directly
+  hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(P->stream, &cst) != hipSuccess) { (void)hipGetLastError(); cst = hipStreamCaptureStatusActive; }
+  if (!P->use_graphs || P->d < 2 || cst != hipStreamCaptureStatusNone)
+    return DISPATCH(plan, run_op, plan, op, x, y, nrhs, nullptr, nullptr, nullptr);
   if (P->graph_exec != nullptr && key == P->graph_key) {
     HIP_TRY(hipGraphLaunch(P->graph_exec, P->stream));
     return 0;
@@ -1176,7 +1180,11 @@ int hgp_toeplitz_apply(hgp_plan* plan, int op, const void* x, void* y, int64_t n
   if (P->cap_stream == nullptr) HIP_TRY(hipStreamCreateWithFlags(&P->cap_stream, hipStreamNonBlocking));
   hipGraph_t graph = nullptr;
   hipStream_t user = P->stream;
-  HIP_TRY(hipStreamBeginCapture(P->cap_stream, hipStreamCaptureModeThreadLocal));
+  if (hipStreamBeginCapture(P->cap_stream, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+    (void)hipGetLastError();
+    P->use_graphs = false;
+    return DISPATCH(plan, run_op, plan, op, x, y, nrhs, nullptr, nullptr, nullptr);
+  }
   P->stream = P->cap_stream;
   const int rc = DISPATCH(plan, run_op, plan, op, x, y, nrhs, nullptr, nullptr, nullptr);
   P->stream = user;
