@@ -19,6 +19,15 @@
 #ifndef HGP_ROWT_PAIRS
 #define HGP_ROWT_PAIRS 8          // row pairs per block (16 rows = 128-B column segments)
 #endif
+// Block order of the row-inverse pass.  A block's column segments are 2C rows long; below one
+// 128-B line (fp32 rows of 4096: C = 4 pairs, 64 B) the two blocks reading each line are dealt
+// to the same XCD (xcd_remap), so the second one finds the line in that L2 (C4 row inverse
+// 2.11 -> 1.67 ms).  The same order in the forward pass (whose partial lines are writes)
+// measured slower (1.42 -> 1.55 ms), so it keeps the plain order.
+//   0: never remap, 1: row inverse below 128-B segments, 2: row inverse always, 3: both passes
+#ifndef HGP_ROW_XCD
+#define HGP_ROW_XCD 1
+#endif
 #ifndef HGP_ROWT_PAIRS_BIG
 #define HGP_ROWT_PAIRS_BIG 16     // the same knob for rows longer than one wave's line (TT > 64)
 #endif
@@ -50,7 +59,15 @@ template <typename T, int H> struct RowTCfg {
   static constexpr int BLOCKS_BY_LDS = LDS_CAP / LDS;
   static constexpr int MINW_LDS = (BLOCKS_BY_LDS * ((THREADS + 63) / 64)) / 4;
   static constexpr int MINW = MINW_LDS < 1 ? 1 : (MINW_LDS > 4 ? 4 : MINW_LDS);
+  static constexpr bool SHORT_SEG = 2 * C * (int)sizeof(C2<T>) < 128;
+  static constexpr bool XCD_INV = HGP_ROW_XCD >= 2 || (HGP_ROW_XCD == 1 && SHORT_SEG);
+  static constexpr bool XCD_FWD = HGP_ROW_XCD == 3;
 };
+
+template <bool REMAP>
+__device__ __forceinline__ int row_block_id() {
+  return REMAP ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+}
 
 // The forward row transform of a block's row pairs after their real values are in va (Re = row
 // 2l, Im = row 2l+1, positions t + TT k < H, zero padded): twiddled odd half, both halves' FFTs,
@@ -129,8 +146,9 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
   const C2<T>* __restrict__ twg = reinterpret_cast<const C2<T>*>(d.tw);
   stage_tw<T, H>(tab, twg, threadIdx.x, Cfg::THREADS);
   const int nrb = (d.Rn + C - 1) / C;
-  const int q = blockIdx.x / nrb;
-  const int rb = blockIdx.x - q * nrb;
+  const int lb = row_block_id<Cfg::XCD_FWD>();
+  const int q = lb / nrb;
+  const int rb = lb - q * nrb;
   // a pair's line spans whole waves at every H used here (TT >= 64): l is wave-uniform (scalar
   // register, scalar row bases), t's known range folds the half-table sign tests
   const int l = (TT % 64 == 0) ? __builtin_amdgcn_readfirstlane(threadIdx.x / TT) : threadIdx.x / TT;
@@ -236,8 +254,9 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
   const C2<T>* __restrict__ twg = reinterpret_cast<const C2<T>*>(d.tw);
   stage_tw<T, H>(tab, twg, threadIdx.x, Cfg::THREADS);
   const int nrb = (d.Rn + C - 1) / C;
-  const int q = blockIdx.x / nrb;
-  const int rb = blockIdx.x - q * nrb;
+  const int lb = row_block_id<Cfg::XCD_INV>();
+  const int q = lb / nrb;
+  const int rb = lb - q * nrb;
   // a pair's line spans whole waves at every H used here (TT >= 64): l is wave-uniform (scalar
   // register, scalar row bases), t's known range folds the half-table sign tests
   const int l = (TT % 64 == 0) ? __builtin_amdgcn_readfirstlane(threadIdx.x / TT) : threadIdx.x / TT;

@@ -40,7 +40,8 @@ def main():
     st = torch.cuda.current_stream(dev)
 
     def tm(fn, reps=10):
-        fn()
+        for _ in range(3):   # warm (the op's graph is captured on its second identical call)
+            fn()
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record(st)
         for _ in range(reps):
