@@ -107,6 +107,7 @@ struct hgp_plan {
   void* cg_x_user = nullptr;
   void* cg_x = nullptr;
   bool cg_active = false;
+  int cg_rs_par = 0;                      // which of the two rs buffers the next step reads
   int64_t ws_budget = (int64_t)1 << 30;
   bool ws_explicit = false;               // HGP_WS_MB given: the byte budget alone sets the chunks
   // 2-D operators run their RHS chunks on `nstreams` streams (the plan's own + side streams),
@@ -232,9 +233,24 @@ struct RowEpi {
   void* r;
   void* x;
   void* p;
-  const void* coef;   // per-RHS alpha (EPI_XR) or beta (EPI_P)
+  const void* coef;   // per-RHS alpha (EPI_XR) or beta (EPI_P), when sp == nullptr
   void* part;         // EPI_XR: r.r partials [q][row block]
+  // in-kernel alpha / beta (PassDesc::cg_sp): spectral partials [q][np], rs in / out per RHS
+  const void* sp = nullptr;
+  int np = 0;
+  const void* rs = nullptr;
+  void* rs_out = nullptr;
 };
+
+// the chunk (first RHS q0) view of an epilogue's in-kernel CG scalar
+template <typename T>
+void set_cg_scalar(PassDesc& D, const RowEpi* epi, int64_t q0) {
+  if (epi->sp == nullptr) return;
+  D.cg_sp = reinterpret_cast<const T*>(epi->sp) + q0 * epi->np;
+  D.cg_np = epi->np;
+  D.cg_rs = reinterpret_cast<const T*>(epi->rs) + q0;
+  D.cg_rs_out = epi->rs_out ? reinterpret_cast<T*>(epi->rs_out) + q0 : nullptr;
+}
 
 // Called between the 2-D column pass and the row-inverse pass of each RHS chunk (q0, qn):
 // computes the chunk's alpha / beta from the column pass's spectral dots.
@@ -407,6 +423,7 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
         Cd.cg_p = reinterpret_cast<T*>(epi->p) + q0 * g.out_M;
         Cd.cg_coef = reinterpret_cast<const T*>(epi->coef) + q0;
         Cd.cg_part = epi->part ? reinterpret_cast<T*>(epi->part) + q0 * nrb : nullptr;
+        set_cg_scalar<T>(Cd, epi, q0);
       }
       HGP_TRY(run_rowt(1, Cd, epi_mode));
     } else if (d == 3 && !gen3) {
@@ -477,6 +494,7 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
         E.cg_coef = reinterpret_cast<const T*>(epi->coef) + q0;
         E.cg_div = (int)g.out[0];                 // planes per RHS share one alpha / beta
         E.cg_part = epi->part ? reinterpret_cast<T*>(epi->part) + q0 * g.out[0] * nrb : nullptr;
+        set_cg_scalar<T>(E, epi, q0);
       }
       HGP_TRY(run_rowt(1, E, epi_mode));
     } else {
@@ -927,7 +945,7 @@ int pcg_begin_t(hgp_plan* P, const void* b, void* x, int64_t nrhs, int use_preco
   HGP_TRY(P->part_op.ensure((size_t)(nrhs * npo) * sizeof(T)));
   HGP_TRY(P->part_u.ensure((size_t)(nrhs * npu) * sizeof(T)));
   if (fused && fold_groups(spec_np(P)) > 0) HGP_TRY(P->part_f.ensure((size_t)(nrhs * fold_groups(spec_np(P))) * sizeof(T)));
-  HGP_TRY(P->scal.ensure((size_t)(4 * nrhs) * sizeof(T)));
+  HGP_TRY(P->scal.ensure((size_t)(5 * nrhs) * sizeof(T)));   // rs, alpha, beta, rnew, rs (2nd)
   HGP_TRY(P->flags.ensure(16));
   const void* brow = b;
   void* xrow = x;
@@ -968,6 +986,7 @@ int pcg_begin_t(hgp_plan* P, const void* b, void* x, int64_t nrhs, int use_preco
   P->cg_layout = layout;
   P->cg_x_user = x;
   P->cg_x = xrow;
+  P->cg_rs_par = 0;
   P->cg_active = true;
   return 0;
 }
@@ -986,34 +1005,56 @@ int pcg_step_t(hgp_plan* P, double tol) {
   T* beta = sc + 2 * nrhs;
   T* rnew = sc + 3 * nrhs;
   if (fused_pcg<T>(P)) {
-    // Fused iteration (2-D, 3-D).  K p: the axis-0 pass leaves the spectral p.Ap partials, alpha is
-    // formed per RHS chunk before the row-inverse pass, whose epilogue does x += alpha p,
-    // r -= alpha Ap (+ r.r partials) with Ap never stored.  Then the break test; then C^-1 r,
+    // Fused iteration (2-D, 3-D).  K p: the axis-0 pass leaves the spectral p.Ap partials, from
+    // which alpha is formed per RHS (in the row-inverse kernel, or by a small kernel between the
+    // passes); the row-inverse epilogue does x += alpha p, r -= alpha Ap (+ r.r partials) with
+    // Ap never stored.  Then the break test; then C^-1 r,
     // whose epilogue does p = z + beta p (z never stored).  Order and semantics of cg.py:63-78.
     const int nps0 = spec_np(P), npx = xr_np<T>(P);
-    const int G = fold_groups(nps0);    // long rows (3-D) are folded per chunk first
+    // alpha and beta are formed inside the row-inverse kernels (each block sums its RHS's
+    // spectral partials, PassDesc::cg_sp) when the partials fit CG_LOADS per thread; rs then
+    // alternates between two buffers (the beta epilogue writes the next one).  Otherwise
+    // (long 3-D rows are folded per chunk first) k_cg_alpha / k_cg_beta run between the passes
+    // of each chunk.
+    // Reading the raw partials in every row-inverse block pays when they are a small share of
+    // the block's tile (C2: 3 %, 15.9 -> 15.4 ms per PCG(20)).  C4's 4097 partials per 64-B
+    // tile (6 %) measured 280 -> 285 ms, and folded partials (C4 after the fold, C5) +1 % / +-0,
+    // so those keep the fold + small-kernel form.
+    const int Hl = (int)(P->LK[P->d - 1] / 2);
+    const int thr = rowt_threads<T>(Hl);
+    const int64_t tile_vals = 2 * (int64_t)(Hl + 1) * 2 * rowt_pairs<T>(Hl);   // reals per block tile
+    const bool direct = nps0 <= CG_LOADS * thr && 25 * (int64_t)nps0 <= tile_vals;
+    const int G = direct ? 0 : fold_groups(nps0);
     const int nps = G > 0 ? G : nps0;
+    const bool inkern = direct;
     T* part_o = reinterpret_cast<T*>(P->part_op.ptr);
     T* part_s = G > 0 ? reinterpret_cast<T*>(P->part_f.ptr) : part_o;
     auto fold = [&](int64_t q0, int qn, hipStream_t cs) {
       if (G > 0) fold_rows<T>(part_o + q0 * nps0, nps0, qn, part_s + q0 * G, done, cs);
     };
+    T* rs_cur = P->cg_rs_par ? sc + 4 * nrhs : rs;
+    T* rs_nxt = P->cg_rs_par ? rs : sc + 4 * nrhs;
     const MidFn mid_alpha = [&](int64_t q0, int qn, hipStream_t cs) {
       fold(q0, qn, cs);
-      cg_alpha<T>(part_s + q0 * nps, nps, qn, rs + q0, alpha + q0, done, cs);
+      if (!inkern) cg_alpha<T>(part_s + q0 * nps, nps, qn, rs_cur + q0, alpha + q0, done, cs);
     };
-    const RowEpi exr{EPI_XR, P->r.ptr, P->cg_x, P->p.ptr, alpha, P->part_u.ptr};
-    HGP_TRY(run_op<T>(P, HGP_OP_K, P->p.ptr, P->Ap.ptr, nrhs, nullptr, nullptr, done, -1, part_o, &exr, &mid_alpha));
+    RowEpi exr{EPI_XR, P->r.ptr, P->cg_x, P->p.ptr, alpha, P->part_u.ptr};
+    if (inkern) { exr.sp = part_s; exr.np = nps; exr.rs = rs_cur; }
+    HGP_TRY(run_op<T>(P, HGP_OP_K, P->p.ptr, P->Ap.ptr, nrhs, nullptr, nullptr, done, -1, part_o, &exr,
+                      (G > 0 || !inkern) ? &mid_alpha : nullptr));
     cg_check<T>(P->part_u.ptr, npx, (int)nrhs, tol, rnew, done, iters, s);
     if (P->cg_precond) {
       const MidFn mid_beta = [&](int64_t q0, int qn, hipStream_t cs) {
         fold(q0, qn, cs);
-        cg_beta<T>(part_s + q0 * nps, nps, qn, rs + q0, beta + q0, done, cs);
+        if (!inkern) cg_beta<T>(part_s + q0 * nps, nps, qn, rs_cur + q0, beta + q0, done, cs);
       };
-      const RowEpi ep{EPI_P, P->r.ptr, P->cg_x, P->p.ptr, beta, nullptr};
-      HGP_TRY(run_op<T>(P, HGP_OP_CINV, P->r.ptr, P->Ap.ptr, nrhs, nullptr, nullptr, done, -1, part_o, &ep, &mid_beta));
+      RowEpi ep{EPI_P, P->r.ptr, P->cg_x, P->p.ptr, beta, nullptr};
+      if (inkern) { ep.sp = part_s; ep.np = nps; ep.rs = rs_cur; ep.rs_out = rs_nxt; }
+      HGP_TRY(run_op<T>(P, HGP_OP_CINV, P->r.ptr, P->Ap.ptr, nrhs, nullptr, nullptr, done, -1, part_o, &ep,
+                        (G > 0 || !inkern) ? &mid_beta : nullptr));
+      if (inkern) P->cg_rs_par ^= 1;
     } else {
-      cg_beta<T>(P->part_u.ptr, npx, (int)nrhs, rs, beta, done, s);
+      cg_beta<T>(P->part_u.ptr, npx, (int)nrhs, rs_cur, beta, done, s);
       cg_update_p<T>(P->p.ptr, P->r.ptr, beta, nrhs, M, done, s);
     }
     HIP_TRY(hipGetLastError());

@@ -18,6 +18,8 @@ template <typename T>
 hipError_t launch_rowt(int H, int inv, int epi, const PassDesc& d, hipStream_t s);
 // row pairs per block of the 2-D row passes (partials of the fused PCG epilogue are per block)
 template <typename T> int rowt_pairs(int H);
+// threads per block of the row-pair kernels
+template <typename T> int rowt_threads(int H);
 // whether the row-pair kernels of H points fit one CU's LDS (else run_op takes the generic path)
 template <typename T> int rowt_fits(int H);
 // 3-D middle-axis transposing line passes (hgp_lines.hpp): inv = 0 k_line_fwd_t, 1 k_line_inv_t

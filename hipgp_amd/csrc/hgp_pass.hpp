@@ -98,9 +98,20 @@ struct PassDesc {
   const void* cg_coef;        // per-RHS alpha (EPI_XR) or beta (EPI_P)
   void* cg_part;              // EPI_XR: per-block partial sums of r.r  [q][row block]
   int cg_div;                 // > 1: cg_div consecutive q (3-D: the i0 planes of one RHS) share a coefficient
+  // in-kernel CG scalar (cg_sp != nullptr; else cg_coef is read): the block sums the RHS's
+  // cg_np spectral-dot partials itself (fixed order, so every block of the RHS gets the same
+  // bits) -- EPI_XR: alpha = cg_rs / sum (cg.py:66); EPI_P: beta = sum / cg_rs (cg.py:74), and
+  // the sum is the next iteration's rs, written to cg_rs_out (cg.py:64).
+  const void* cg_sp;
+  int cg_np;
+  const void* cg_rs;
+  void* cg_rs_out;
 };
 
 constexpr int LDS_CAP = 160 * 1024;
+// at most CG_LOADS partials per thread for the in-kernel CG scalar (the host checks
+// cg_np <= CG_LOADS x THREADS, else it passes cg_coef from a k_cg_alpha / k_cg_beta launch)
+constexpr int CG_LOADS = 8;
 
 template <typename T, int H, int LAY> struct PassCfg {
   static constexpr int P = (H < PMax<T>::v) ? H : PMax<T>::v;

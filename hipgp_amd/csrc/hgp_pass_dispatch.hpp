@@ -146,6 +146,9 @@ template <typename T, int H>
 static int rowt_pairs_h() { return RowTCfg<T, H>::C; }
 
 template <typename T, int H>
+static int rowt_threads_h() { return RowTCfg<T, H>::THREADS; }
+
+template <typename T, int H>
 static int rowt_fits_h() { return RowTCfg<T, H>::LDS <= LDS_CAP ? 1 : 0; }
 
 template <typename T>
@@ -163,6 +166,12 @@ hipError_t launch_rowt(int H, int inv, int epi, const PassDesc& d, hipStream_t s
 template <typename T>
 int rowt_pairs(int H) {
   HGP_H_SWITCH(rowt_pairs_h)
+  return 0;
+}
+
+template <typename T>
+int rowt_threads(int H) {
+  HGP_H_SWITCH(rowt_threads_h)
   return 0;
 }
 

@@ -247,6 +247,8 @@ template <typename T, int H, int EPI = EPI_OUT>
 __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) void k_row_inv_t(const PassDesc d) {
   using Cfg = RowTCfg<T, H>;
   constexpr int P = Cfg::P, TT = Cfg::TT, C = Cfg::C, PITCH = Cfg::PITCH;
+  // staged rows (2C x out_len <= 2C x H values) + two wave-sum areas fit the LDS area
+  static_assert((2 * C * H + 2 * (Cfg::THREADS / 64)) * (int)sizeof(T) <= Cfg::AREA * (int)sizeof(C2<T>), "epilogue LDS");
   if (d.done != nullptr && *d.done) return;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   C2<T>* lds = reinterpret_cast<C2<T>*>(smem_raw);
@@ -327,6 +329,28 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
   using H0 = std::integral_constant<int, 0>;
   using H1 = std::integral_constant<int, 1>;
   load_tile(H0{});
+  // in-kernel CG scalar: the RHS's spectral partials are loaded behind the first tile (their
+  // latency hides under the tile's) and summed per thread and per wave right after it lands;
+  // the wave sums are combined in the epilogue (cg_scalar)
+  T csum = 0;
+  if constexpr (EPI != EPI_OUT) {
+    if (d.cg_sp != nullptr) {   // uniform
+      const int qc = d.cg_div > 1 ? q / d.cg_div : q;
+      const T* sp = reinterpret_cast<const T*>(d.cg_sp) + (int64_t)qc * d.cg_np;
+      const int lim = d.cg_np - 1;
+      T cv[CG_LOADS];
+#pragma unroll
+      for (int u = 0; u < CG_LOADS; ++u) {
+        const int i = threadIdx.x + u * Cfg::THREADS;
+        cv[u] = 0;
+        if (u * Cfg::THREADS < d.cg_np)     // uniform: only the rounds that hold partials
+          cv[u] = sp[i < lim ? i : lim];    // (clamped) loads, the tail zeroed below
+      }
+#pragma unroll
+      for (int u = 0; u < CG_LOADS; ++u)
+        if (threadIdx.x + u * Cfg::THREADS < d.cg_np) csum += cv[u];
+    }
+  }
   __syncthreads();   // twiddles staged (the tile area is free)
   park_tile(H0{});
   __syncthreads();
@@ -362,9 +386,32 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
         }
       }
     }
+    // wave sums of the CG scalar's partials, behind the staged rows and the r.r partials
+    T* red2 = ys + 2 * C * out_len + Cfg::THREADS / 64;
+    if (d.cg_sp != nullptr) {
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) csum += __shfl_xor(csum, off, 64);
+      if ((threadIdx.x & 63) == 0) red2[threadIdx.x >> 6] = csum;
+    }
     __syncthreads();
     const int64_t g0 = (int64_t)q * d.out.q_stride + (int64_t)row0 * d.out.r_stride;
-    const T coef = reinterpret_cast<const T*>(d.cg_coef)[d.cg_div > 1 ? q / d.cg_div : q];
+    const int qc = d.cg_div > 1 ? q / d.cg_div : q;
+    T coef;
+    if (d.cg_sp != nullptr) {
+      T tot = 0;
+#pragma unroll
+      for (int w = 0; w < Cfg::THREADS / 64; ++w) tot += red2[w];   // wave order: deterministic
+      const T rs = reinterpret_cast<const T*>(d.cg_rs)[qc];
+      if constexpr (EPI == EPI_XR) {
+        coef = rs / tot;
+      } else {
+        coef = tot / rs;
+        if (rb == 0 && threadIdx.x == 0 && (d.cg_div <= 1 || q % d.cg_div == 0))
+          reinterpret_cast<T*>(d.cg_rs_out)[qc] = tot;
+      }
+    } else {
+      coef = reinterpret_cast<const T*>(d.cg_coef)[qc];
+    }
     T* pg = reinterpret_cast<T*>(d.cg_p) + g0;
     T* xg = EPI == EPI_XR ? reinterpret_cast<T*>(d.cg_x) + g0 : pg;
     T* rg = EPI == EPI_XR ? reinterpret_cast<T*>(d.cg_r) + g0 : pg;
