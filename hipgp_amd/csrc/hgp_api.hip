@@ -108,6 +108,7 @@ struct hgp_plan {
   void* cg_x = nullptr;
   bool cg_active = false;
   int cg_rs_par = 0;                      // which of the two rs buffers the next step reads
+  int cg_step = 0;                        // steps queued since hgp_pcg_begin
   int64_t ws_budget = (int64_t)1 << 30;
   bool ws_explicit = false;               // HGP_WS_MB given: the byte budget alone sets the chunks
   // 2-D operators run their RHS chunks on `nstreams` streams (the plan's own + side streams),
@@ -233,18 +234,24 @@ struct RowEpi {
   void* r;
   void* x;
   void* p;
-  const void* coef;   // per-RHS alpha (EPI_XR) or beta (EPI_P), when sp == nullptr
-  void* part;         // EPI_XR: r.r partials [q][row block]
+  const void* coef;   // per-RHS alpha (EPI_XR, EPI_R) or beta (EPI_XP), when sp == nullptr
+  void* part;         // EPI_XR / EPI_R: r.r partials [q][row block]
   // in-kernel alpha / beta (PassDesc::cg_sp): spectral partials [q][np], rs in / out per RHS
   const void* sp = nullptr;
   int np = 0;
   const void* rs = nullptr;
   void* rs_out = nullptr;
+  const void* coef2 = nullptr;   // EPI_XP: alpha per RHS
+  void* alpha_out = nullptr;     // EPI_R (in-kernel alpha): where EPI_XP reads it
+  int fix = 0;                   // EPI_XP: PassDesc::cg_fix
 };
 
 // the chunk (first RHS q0) view of an epilogue's in-kernel CG scalar
 template <typename T>
 void set_cg_scalar(PassDesc& D, const RowEpi* epi, int64_t q0) {
+  D.cg_coef2 = epi->coef2 ? reinterpret_cast<const T*>(epi->coef2) + q0 : nullptr;
+  D.cg_alpha_out = epi->alpha_out ? reinterpret_cast<T*>(epi->alpha_out) + q0 : nullptr;
+  D.cg_fix = epi->fix;
   if (epi->sp == nullptr) return;
   D.cg_sp = reinterpret_cast<const T*>(epi->sp) + q0 * epi->np;
   D.cg_np = epi->np;
@@ -987,6 +994,7 @@ int pcg_begin_t(hgp_plan* P, const void* b, void* x, int64_t nrhs, int use_preco
   P->cg_x_user = x;
   P->cg_x = xrow;
   P->cg_rs_par = 0;
+  P->cg_step = 0;
   P->cg_active = true;
   return 0;
 }
@@ -994,6 +1002,7 @@ int pcg_begin_t(hgp_plan* P, const void* b, void* x, int64_t nrhs, int use_preco
 template <typename T>
 int pcg_step_t(hgp_plan* P, double tol) {
   hipStream_t s = P->stream;
+  const int step = P->cg_step++;
   const int64_t nrhs = P->cg_nrhs, M = P->M;
   const int npo = rn_last<T>(P), npu = update_np(M);
   int* flags = reinterpret_cast<int*>(P->flags.ptr);
@@ -1038,8 +1047,10 @@ int pcg_step_t(hgp_plan* P, double tol) {
       fold(q0, qn, cs);
       if (!inkern) cg_alpha<T>(part_s + q0 * nps, nps, qn, rs_cur + q0, alpha + q0, done, cs);
     };
-    RowEpi exr{EPI_XR, P->r.ptr, P->cg_x, P->p.ptr, alpha, P->part_u.ptr};
-    if (inkern) { exr.sp = part_s; exr.np = nps; exr.rs = rs_cur; }
+    // with the preconditioner the x update moves to the C^-1 pass (EPI_R here, EPI_XP there)
+    const bool defer = P->cg_precond != 0;
+    RowEpi exr{defer ? EPI_R : EPI_XR, P->r.ptr, P->cg_x, P->p.ptr, alpha, P->part_u.ptr};
+    if (inkern) { exr.sp = part_s; exr.np = nps; exr.rs = rs_cur; exr.alpha_out = alpha; }
     HGP_TRY(run_op<T>(P, HGP_OP_K, P->p.ptr, P->Ap.ptr, nrhs, nullptr, nullptr, done, -1, part_o, &exr,
                       (G > 0 || !inkern) ? &mid_alpha : nullptr));
     cg_check<T>(P->part_u.ptr, npx, (int)nrhs, tol, rnew, done, iters, s);
@@ -1048,7 +1059,9 @@ int pcg_step_t(hgp_plan* P, double tol) {
         fold(q0, qn, cs);
         if (!inkern) cg_beta<T>(part_s + q0 * nps, nps, qn, rs_cur + q0, beta + q0, done, cs);
       };
-      RowEpi ep{EPI_P, P->r.ptr, P->cg_x, P->p.ptr, beta, nullptr};
+      RowEpi ep{EPI_XP, P->r.ptr, P->cg_x, P->p.ptr, beta, nullptr};
+      ep.coef2 = alpha;
+      ep.fix = step + 1;           // the done value this step's break test writes
       if (inkern) { ep.sp = part_s; ep.np = nps; ep.rs = rs_cur; ep.rs_out = rs_nxt; }
       HGP_TRY(run_op<T>(P, HGP_OP_CINV, P->r.ptr, P->Ap.ptr, nrhs, nullptr, nullptr, done, -1, part_o, &ep,
                         (G > 0 || !inkern) ? &mid_beta : nullptr));
@@ -1283,7 +1296,7 @@ int hgp_pcg_step(hgp_plan* plan, double tol, int* converged) {
     int h = 0;
     HIP_TRY(hipMemcpyAsync(&h, plan->flags.ptr, sizeof(int), hipMemcpyDeviceToHost, plan->stream));
     HIP_TRY(hipStreamSynchronize(plan->stream));
-    *converged = h;
+    *converged = h != 0;
   }
   return 0;
 }

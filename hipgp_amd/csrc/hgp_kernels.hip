@@ -555,7 +555,7 @@ __global__ __launch_bounds__(1024) void k_cg_check(const T* __restrict__ part, i
   __syncthreads();
   if (threadIdx.x == 0) {
     *iters += 1;
-    if (!any_not) *done = 1;
+    if (!any_not) *done = *iters;   // nonzero; = the iteration it fired in (PassDesc::cg_fix)
   }
 }
 

@@ -61,7 +61,9 @@ namespace hgp {
 enum { PASS_FWD = 0, PASS_INV = 1, PASS_CONV = 2, PASS_CONVC = 3 };   // CONV: real spectrum, CONVC: complex
 enum { LAY_STRIDED = 0, LAY_CONTIG = 1, LAY_RP = 2, LAY_R1 = 3 };
 enum { SPEC_REAL = 0, SPEC_CPLX = 1, SPEC_CPLX_CONJ = 2 };
-enum { EPI_OUT = 0, EPI_XR = 1, EPI_P = 2 };   // 2-D row-inverse epilogue (hgp_rows.hpp)
+// row-inverse epilogue (hgp_rows.hpp): EPI_XR x/r update (unpreconditioned PCG); with the
+// preconditioner the x update is deferred to the C^-1 pass: EPI_R r update, EPI_XP x and p
+enum { EPI_OUT = 0, EPI_XR = 1, EPI_R = 2, EPI_XP = 3 };
 
 struct View {
   void* ptr;
@@ -91,16 +93,20 @@ struct PassDesc {
   void* spart;
   int spart_mid;
   int spart_div;              // > 1: the compact column of line r is r / spart_div (3-D: r = c2 * L1 + k1)
-  // fused PCG epilogue of the 2-D row-inverse pass (hgp_rows.hpp, EPI_XR / EPI_P)
+  // fused PCG epilogue of the row-inverse pass (hgp_rows.hpp, EPI_XR / EPI_R / EPI_XP)
   void* cg_r;
   void* cg_x;
   void* cg_p;
-  const void* cg_coef;        // per-RHS alpha (EPI_XR) or beta (EPI_P)
+  const void* cg_coef;        // per-RHS alpha (EPI_XR, EPI_R) or beta (EPI_XP)
+  const void* cg_coef2;       // EPI_XP: per-RHS alpha of the same iteration (x += alpha p)
+  void* cg_alpha_out;         // EPI_R with the in-kernel alpha: alpha per RHS for EPI_XP
+  int cg_fix;                 // EPI_XP: *done == cg_fix (the break fired in this iteration):
+                              // the pass only applies the pending x += alpha p
   void* cg_part;              // EPI_XR: per-block partial sums of r.r  [q][row block]
   int cg_div;                 // > 1: cg_div consecutive q (3-D: the i0 planes of one RHS) share a coefficient
   // in-kernel CG scalar (cg_sp != nullptr; else cg_coef is read): the block sums the RHS's
   // cg_np spectral-dot partials itself (fixed order, so every block of the RHS gets the same
-  // bits) -- EPI_XR: alpha = cg_rs / sum (cg.py:66); EPI_P: beta = sum / cg_rs (cg.py:74), and
+  // bits) -- EPI_XR/R: alpha = cg_rs / sum (cg.py:66); EPI_XP: beta = sum / cg_rs (cg.py:74), and
   // the sum is the next iteration's rs, written to cg_rs_out (cg.py:64).
   const void* cg_sp;
   int cg_np;

@@ -94,7 +94,8 @@ static hipError_t launch_rowt_h(int inv, int epi, const PassDesc& d, hipStream_t
   if (nb <= 0) return hipSuccess;
   if (inv) {
     if (epi == EPI_XR) return launch_rowt_inv<T, H, EPI_XR>(d, nb, s);
-    if (epi == EPI_P) return launch_rowt_inv<T, H, EPI_P>(d, nb, s);
+    if (epi == EPI_R) return launch_rowt_inv<T, H, EPI_R>(d, nb, s);
+    if (epi == EPI_XP) return launch_rowt_inv<T, H, EPI_XP>(d, nb, s);
     return launch_rowt_inv<T, H, EPI_OUT>(d, nb, s);
   }
   static bool attr_set = false;

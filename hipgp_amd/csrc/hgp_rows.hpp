@@ -200,11 +200,16 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
 // Fused PCG update of one block's output rows y (staged in LDS, `ys` [row][col], pitch
 // out_len), streamed with the row layout of the (nrhs, M) vectors:
 //   EPI_XR (y = A p):     x += a p;  r -= a y;  returns this thread's share of r.r  (cg.py:67-69)
-//   EPI_P  (y = C^-1 r):  p = y + b p                                                 (cg.py:75)
+//   EPI_R  (y = A p):     r -= a y;  returns this thread's share of r.r           (cg.py:68-69)
+//   EPI_XP (y = C^-1 r):  x += a p;  p = y + b p  (the iteration's x update, deferred) (cg.py:67, 75)
+// x is never read by the recurrence, so moving its update from the A p pass to the C^-1 r pass
+// (where p is read anyway) saves one read of p per iteration with the same arithmetic; a
+// break after the r update is finished by the EPI_XP pass alone (PassDesc::cg_fix).
 // Four elements per thread are loaded before any is stored (the vectors never alias).
 template <typename T, int EPI, int THREADS>
 __device__ __forceinline__ T cg_epilogue(const T* __restrict__ ys, int nrow, int out_len, T* __restrict__ xg,
-                                         T* __restrict__ rg, T* __restrict__ pg, int64_t rpitch, T coef) {
+                                         T* __restrict__ rg, T* __restrict__ pg, int64_t rpitch, T coef,
+                                         T coef2 = 0) {
   const int nel = nrow * out_len;
   // the block's rows are one < 2 GiB window of each vector: raw buffers, 32-bit lane offsets
   const BufRsrc rp = buf_rsrc(pg, 0x7fffffffu), rx = buf_rsrc(xg, 0x7fffffffu), rr = buf_rsrc(rg, 0x7fffffffu);
@@ -220,21 +225,20 @@ __device__ __forceinline__ T cg_epilogue(const T* __restrict__ ys, int nrow, int
       const int c = ee - row * out_len;
       g[u] = ((uint32_t)row * (uint32_t)rpitch + (uint32_t)c) * (uint32_t)sizeof(T);
       yv[u] = ys[ee];
-      pv[u] = buf_ld<T>(rp, g[u]);
-      if constexpr (EPI == EPI_XR) {
-        xv[u] = buf_ld<T>(rx, g[u]);
-        rv[u] = buf_ld<T>(rr, g[u]);
-      }
+      if constexpr (EPI != EPI_R) pv[u] = buf_ld<T>(rp, g[u]);
+      if constexpr (EPI == EPI_XR || EPI == EPI_XP) xv[u] = buf_ld<T>(rx, g[u]);
+      if constexpr (EPI == EPI_XR || EPI == EPI_R) rv[u] = buf_ld<T>(rr, g[u]);
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if (e0 + u * THREADS < nel) {
-        if constexpr (EPI == EPI_XR) {
-          buf_st<T>(xv[u] + coef * pv[u], rx, g[u]);
+        if constexpr (EPI == EPI_XR || EPI == EPI_R) {
+          if constexpr (EPI == EPI_XR) buf_st<T>(xv[u] + coef * pv[u], rx, g[u]);
           const T rn = rv[u] - coef * yv[u];
           buf_st<T>(rn, rr, g[u]);
           s += rn * rn;
         } else {
+          buf_st<T>(xv[u] + coef2 * pv[u], rx, g[u]);
           buf_st<T>(yv[u] + coef * pv[u], rp, g[u]);
         }
       }
@@ -243,22 +247,50 @@ __device__ __forceinline__ T cg_epilogue(const T* __restrict__ ys, int nrow, int
   return s;
 }
 
+// The x update of an iteration whose break test fired after its r update (EPI_XP pass of that
+// iteration, nothing else of it runs): x += a p over the block's rows.
+template <typename T, int THREADS>
+__device__ __forceinline__ void cg_fix_x(int nrow, int out_len, T* __restrict__ xg, const T* __restrict__ pg,
+                                         int64_t rpitch, T a) {
+  const int nel = nrow * out_len;
+  for (int e = threadIdx.x; e < nel; e += THREADS) {
+    const int row = e / out_len;
+    const int64_t o = (int64_t)row * rpitch + (e - row * out_len);
+    xg[o] = xg[o] + a * pg[o];
+  }
+}
+
 template <typename T, int H, int EPI = EPI_OUT>
 __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) void k_row_inv_t(const PassDesc d) {
   using Cfg = RowTCfg<T, H>;
   constexpr int P = Cfg::P, TT = Cfg::TT, C = Cfg::C, PITCH = Cfg::PITCH;
   // staged rows (2C x out_len <= 2C x H values) + two wave-sum areas fit the LDS area
   static_assert((2 * C * H + 2 * (Cfg::THREADS / 64)) * (int)sizeof(T) <= Cfg::AREA * (int)sizeof(C2<T>), "epilogue LDS");
-  if (d.done != nullptr && *d.done) return;
+  const int nrb = (d.Rn + C - 1) / C;
+  const int lb = row_block_id<Cfg::XCD_INV>();
+  const int q = lb / nrb;
+  const int rb = lb - q * nrb;
+  if (d.done != nullptr) {
+    const int dv = *d.done;                      // uniform
+    if (dv != 0) {
+      if constexpr (EPI == EPI_XP) {
+        if (dv == d.cg_fix) {                    // the break fired in this iteration
+          const int row0 = 2 * rb * C;
+          const int nrow_blk = d.nrows - row0 < 2 * C ? d.nrows - row0 : 2 * C;
+          const int64_t g0 = (int64_t)q * d.out.q_stride + (int64_t)row0 * d.out.r_stride;
+          const T a = reinterpret_cast<const T*>(d.cg_coef2)[d.cg_div > 1 ? q / d.cg_div : q];
+          cg_fix_x<T, Cfg::THREADS>(nrow_blk, d.out.len, reinterpret_cast<T*>(d.cg_x) + g0,
+                                    reinterpret_cast<const T*>(d.cg_p) + g0, d.out.r_stride, a);
+        }
+      }
+      return;
+    }
+  }
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   C2<T>* lds = reinterpret_cast<C2<T>*>(smem_raw);
   C2<T>* tab = lds + Cfg::AREA;
   const C2<T>* __restrict__ twg = reinterpret_cast<const C2<T>*>(d.tw);
   stage_tw<T, H>(tab, twg, threadIdx.x, Cfg::THREADS);
-  const int nrb = (d.Rn + C - 1) / C;
-  const int lb = row_block_id<Cfg::XCD_INV>();
-  const int q = lb / nrb;
-  const int rb = lb - q * nrb;
   // a pair's line spans whole waves at every H used here (TT >= 64): l is wave-uniform (scalar
   // register, scalar row bases), t's known range folds the half-table sign tests
   const int l = (TT % 64 == 0) ? __builtin_amdgcn_readfirstlane(threadIdx.x / TT) : threadIdx.x / TT;
@@ -402,8 +434,11 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
 #pragma unroll
       for (int w = 0; w < Cfg::THREADS / 64; ++w) tot += red2[w];   // wave order: deterministic
       const T rs = reinterpret_cast<const T*>(d.cg_rs)[qc];
-      if constexpr (EPI == EPI_XR) {
+      if constexpr (EPI == EPI_XR || EPI == EPI_R) {
         coef = rs / tot;
+        if (EPI == EPI_R && d.cg_alpha_out != nullptr && rb == 0 && threadIdx.x == 0 &&
+            (d.cg_div <= 1 || q % d.cg_div == 0))
+          reinterpret_cast<T*>(d.cg_alpha_out)[qc] = coef;   // for this iteration's EPI_XP
       } else {
         coef = tot / rs;
         if (rb == 0 && threadIdx.x == 0 && (d.cg_div <= 1 || q % d.cg_div == 0))
@@ -413,10 +448,11 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
       coef = reinterpret_cast<const T*>(d.cg_coef)[qc];
     }
     T* pg = reinterpret_cast<T*>(d.cg_p) + g0;
-    T* xg = EPI == EPI_XR ? reinterpret_cast<T*>(d.cg_x) + g0 : pg;
-    T* rg = EPI == EPI_XR ? reinterpret_cast<T*>(d.cg_r) + g0 : pg;
-    T s = cg_epilogue<T, EPI, Cfg::THREADS>(ys, nrow_blk, out_len, xg, rg, pg, d.out.r_stride, coef);
-    if constexpr (EPI == EPI_XR) {   // deterministic block sum of r.r -> partial [q][rb]
+    T* xg = EPI != EPI_R ? reinterpret_cast<T*>(d.cg_x) + g0 : pg;
+    T* rg = EPI != EPI_XP ? reinterpret_cast<T*>(d.cg_r) + g0 : pg;
+    const T coef2 = EPI == EPI_XP ? reinterpret_cast<const T*>(d.cg_coef2)[qc] : (T)0;
+    T s = cg_epilogue<T, EPI, Cfg::THREADS>(ys, nrow_blk, out_len, xg, rg, pg, d.out.r_stride, coef, coef2);
+    if constexpr (EPI == EPI_XR || EPI == EPI_R) {   // deterministic block sum of r.r -> partial [q][rb]
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
       T* red = ys + 2 * C * out_len;   // past the staged rows (2C x out_len <= C x H values)
