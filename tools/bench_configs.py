@@ -149,6 +149,12 @@ def main():
         r = run(name, dev)
         res.append(r)
         print(json.dumps(r), flush=True)
+        # each config is its own workload: drop the previous grid's pooled plans (their
+        # workspaces sit outside torch's allocator) before the next one
+        import gc
+        from hipgp_amd.plan import release_pool
+        gc.collect()
+        release_pool()
         torch.cuda.empty_cache()
     return res
 

@@ -16,6 +16,7 @@ python - <<'PY'
 import json
 for l in open("gpurun_out/cfg_q.jsonl"):
     d = json.loads(l)
+    if "kmatvec_batched_ms" not in d: print(d["config"], d.get("gram_solve_s")); continue
     print(d["config"], "kmatvec_ms", round(d["kmatvec_batched_ms"], 3), "frac", round(d["kmatvec_hbm_frac"], 3),
           "compute_kn_s", round(d["compute_kn_s"], 4), "frac", round(d["compute_kn_hbm_frac"], 3), "peak_gb", round(d["peak_mem_gb"], 1))
 PY
