@@ -3,7 +3,7 @@ with 50 ms host gaps; tools/pcg_trace.py --analyze <kernel_trace.csv> then split
 the gaps and reports, for the last run, wall time, GPU-busy time (union of kernel intervals over
 all streams), idle gaps and the time per kernel.
 
-    rocprofv3 --kernel-trace -d out -o run --output-format csv -- python3 tools/pcg_trace.py
+    rocprofv3 --kernel-trace -d out -o run --output-format csv -- python3 tools/pcg_trace.py [C4]
     python3 tools/pcg_trace.py --analyze out/.../run_kernel_trace.csv"""
 import csv
 import os
@@ -12,16 +12,31 @@ import time
 from collections import defaultdict
 
 
-def run():
+def run(cfg="C2"):
     import torch
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    import bench
     dev = torch.device("cuda", 0)
-    grids, kf, Knm = bench.make_problem(1024, 32, dev, seed=1234)
     from ziggy.misc.toeplitz_tensor import ToeplitzTensor
+    if cfg == "C2":
+        import bench
+        grids, kf, Knm = bench.make_problem(1024, 32, dev, seed=1234)
+        jitter, maxiter, tol = 1e-3, 20, 1e-8
+    else:                                   # a BASELINE config of tools/bench_configs.py
+        from tools.bench_configs import BOX, CONFIGS, kernel
+        from hipgp_amd.kuf import kuf_grid
+        dims, (kind, nu), params, jitter, B, maxiter, tol, _ = CONFIGS[cfg]
+        d = len(dims)
+        k = kernel(kind, nu, torch.float32)
+        kf = lambda x, y: k.forward(x, y, params=params)
+        grids = [torch.linspace(lo, hi, m, device=dev) for (lo, hi), m in zip(BOX[d], dims)]
+        g = torch.Generator(device="cpu").manual_seed(42)
+        lo = torch.tensor([b[0] for b in BOX[d]])
+        hi = torch.tensor([b[1] for b in BOX[d]])
+        xobs = (lo + (hi - lo) * torch.rand(B, d, generator=g)).to(dev)
+        Knm = kuf_grid(k, grids, xobs, params)
     for _ in range(3):
-        Tk = ToeplitzTensor(grids, kf, batch_shape=None, jitter_val=1e-3)
-        d0 = Tk.inv_matmul(Knm, do_precond=True, maxiter=20, tol=1e-8)
+        Tk = ToeplitzTensor(grids, kf, batch_shape=None, jitter_val=jitter)
+        d0 = Tk.inv_matmul(Knm, do_precond=True, maxiter=maxiter, tol=tol)
         Tk._matmul_by_RT(d0)
         torch.cuda.synchronize()
         time.sleep(0.05)
@@ -63,4 +78,4 @@ if __name__ == "__main__":
     if len(sys.argv) > 2 and sys.argv[1] == "--analyze":
         analyze(sys.argv[2])
     else:
-        run()
+        run(sys.argv[1] if len(sys.argv) > 1 else "C2")
