@@ -96,6 +96,9 @@ struct hgp_plan {
   // spectra
   DevBuf specK, specI, specR, Dm3;
   bool have_spec = false;
+  // R / R^T spectrum real (the filter embedded evenly: L_R >= 2n - 1 on every axis, d >= 2):
+  // real-spectrum conv passes instead of complex ones, half the spectrum bytes
+  bool r_real = false;
   double clamp_min = 1e-6;                // of the last set_column (the clamp's gradient mask)
   DevBuf nclamp;
   // scratch
@@ -183,8 +186,8 @@ OpGeom op_geom(const hgp_plan* P, int op) {
   g.tw = (op == HGP_OP_RT || op == HGP_OP_R) ? P->twR : P->twK;
   if (op == HGP_OP_K) { g.spec = P->specK.ptr; g.spec_kind = SPEC_REAL; }
   else if (op == HGP_OP_CINV) { g.spec = P->specI.ptr; g.spec_kind = SPEC_REAL; }
-  else if (op == HGP_OP_RT) { g.spec = P->specR.ptr; g.spec_kind = SPEC_CPLX; }
-  else { g.spec = P->specR.ptr; g.spec_kind = SPEC_CPLX_CONJ; }
+  else if (op == HGP_OP_RT) { g.spec = P->specR.ptr; g.spec_kind = P->r_real ? SPEC_REAL : SPEC_CPLX; }
+  else { g.spec = P->specR.ptr; g.spec_kind = P->r_real ? SPEC_REAL : SPEC_CPLX_CONJ; }
   return g;
 }
 
@@ -761,19 +764,26 @@ int set_column_t(hgp_plan* P, const void* column, double jitter, double clamp_mi
     extract_t<T>(F, P->specK.ptr, P->specI.ptr, P->LK[0], d == 3 ? P->LK[1] : 1, LKl / 2, LKl, 0,
                  1.0 / (double)P->prodLK, s);
   for (int ax = 0; ax < 3; ++ax) gd.L[ax] = P->LR[ax];
-  HGP_TRY(P->specR.ensure((size_t)nR * sizeof(C2<T>)));
   bool long_r = false;
   for (int ax = 0; ax < d; ++ax) long_r = long_r || P->LR[ax] / 2 > 8192;
+  bool sym = d >= 2 && !long_r;
+  for (int ax = 0; ax < d; ++ax) sym = sym && P->LR[ax] >= 2 * P->n[ax] - 1;
+  P->r_real = sym;
+  HGP_TRY(P->specR.ensure((size_t)nR * (sym ? sizeof(T) : sizeof(C2<T>))));
   if (d == 1) {
     embed_R(sv, g1, gd, s);
     HGP_TRY(fwd_grid_f64(P, P->LR, P->tw64R, g1, g2, &F));
     extract_cplx<T>(F, P->specR.ptr, nR, LRl, SR, compact, 1.0 / (double)P->prodLR, s);
   } else if (!long_r) {
     // the R filter is real: real row-pair transform of the last axis, compact columns only after
-    embed_R_real(sv, reinterpret_cast<double*>(g1), gd, s);
+    embed_R_real(sv, reinterpret_cast<double*>(g1), gd, sym ? 1 : 0, s);
     HGP_TRY(fwd_grid_real_f64(P, P->LR, P->tw64R, reinterpret_cast<const double*>(g1), g2, SR));
-    extract_t<T>(g2, P->specR.ptr, nullptr, P->LR[0], d == 3 ? P->LR[1] : 1, LRl / 2, SR, 1,
-                 1.0 / (double)P->prodLR, s);
+    if (sym)   // even filter: its spectrum is real (the imaginary parts are rounding noise)
+      extract_t_re<T>(g2, P->specR.ptr, P->LR[0], d == 3 ? P->LR[1] : 1, LRl / 2, SR, 1,
+                      1.0 / (double)P->prodLR, s);
+    else
+      extract_t<T>(g2, P->specR.ptr, nullptr, P->LR[0], d == 3 ? P->LR[1] : 1, LRl / 2, SR, 1,
+                   1.0 / (double)P->prodLR, s);
   } else {
     // an axis of L_R > 16384 points: the full complex grid through fft_lines_f64's radix-2 step
     embed_R(sv, g1, gd, s);

@@ -39,7 +39,9 @@ void clamp_spectrum(const double* Draw, double* out3, int64_t M, double clamp_mi
                     hipStream_t s);
 void embed_K(const double* cK, const double* cI, double2* out, const GridDims& g, hipStream_t s);
 void embed_R(const double* sv, double2* out, const GridDims& g, hipStream_t s);
-void embed_R_real(const double* sv, double* out, const GridDims& g, hipStream_t s);
+// sym: mirror the filter over (-n, n) on every axis (needs L >= 2n - 1): the embedded filter is
+// then even and its spectrum real (set_column_t, hgp_plan::r_real)
+void embed_R_real(const double* sv, double* out, const GridDims& g, int sym, hipStream_t s);
 void r2_combine(const double2* in, double2* out, int64_t L, int64_t Rn, int64_t r_stride, int64_t In, int64_t ps,
                 const double2* tw, hipStream_t s);
 // d >= 2: tiled transposing extraction into [c][k1][k0] (hgp_kernels.hip k_extract_t); b == nullptr:
@@ -47,6 +49,10 @@ void r2_combine(const double2* in, double2* out, int64_t L, int64_t Rn, int64_t 
 template <typename T>
 void extract_t(const double2* F, void* a, void* b, int64_t L0, int64_t L1, int64_t H, int64_t Ssrc, int compact_src,
                double scale, hipStream_t s);
+// the same extraction keeping the real part only (a real spectrum: Re -> a)
+template <typename T>
+void extract_t_re(const double2* F, void* a, int64_t L0, int64_t L1, int64_t H, int64_t Ssrc, int compact_src,
+                  double scale, hipStream_t s);
 template <typename T> void extract_pair(const double2* F, void* a, void* b, int64_t n, int64_t L, int64_t S, int compact,
                                         double scale, hipStream_t s, int64_t L0t = 0, int64_t L1t = 0);
 template <typename T> void extract_cplx(const double2* F, void* o, int64_t n, int64_t L, int64_t S, int compact, double scale,

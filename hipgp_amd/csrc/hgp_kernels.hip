@@ -184,7 +184,8 @@ void r2_combine(const double2* in, double2* out, int64_t L, int64_t Rn, int64_t 
 }
 
 // the same R filter as a REAL grid (the set-up transforms it with the real row-pair pass)
-__global__ void k_embed_R_real(const double* __restrict__ s, double* __restrict__ out, GridDims g, int64_t total) {
+__global__ void k_embed_R_real(const double* __restrict__ s, double* __restrict__ out, GridDims g, int64_t total,
+                               int sym) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= total) return;
   int64_t rem = idx, src = 0, mstride = 1;
@@ -194,18 +195,20 @@ __global__ void k_embed_R_real(const double* __restrict__ s, double* __restrict_
     rem /= g.L[a];
     const int64_t m = g.m[a], n = g.n[a], L = g.L[a];
     int64_t t;
+    // the n-periodic even filter r[j] (r[j] = s[j], j < m; s[n - j] above) at offsets (-m, n), or
+    // with `sym` at (-n, n): the extra offsets (-n, -m] are never read by outputs j < n
     if (u < n) t = (u <= m - 1) ? u : n - u;
-    else if (u >= L - m + 1) t = L - u;
+    else if (u >= L - (sym ? n : m) + 1) { const int64_t j = L - u; t = (j <= m - 1) ? j : n - j; }
     else { ok = false; t = 0; }
     src += t * mstride;
     mstride *= m;
   }
   out[idx] = ok ? s[src] : 0.0;
 }
-void embed_R_real(const double* sv, double* out, const GridDims& g, hipStream_t s) {
+void embed_R_real(const double* sv, double* out, const GridDims& g, int sym, hipStream_t s) {
   int64_t total = 1;
   for (int a = 0; a < g.d; ++a) total *= g.L[a];
-  hipLaunchKernelGGL(k_embed_R_real, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, sv, out, g, total);
+  hipLaunchKernelGGL(k_embed_R_real, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, sv, out, g, total, sym);
 }
 
 void embed_K(const double* cK, const double* cI, double2* out, const GridDims& g, hipStream_t s) {
@@ -304,7 +307,7 @@ __global__ __launch_bounds__(256) void k_extract_t(const double2* __restrict__ F
       const int64_t oi = (c * L1 + k1) * L0 + k0;
       if constexpr (PAIR) {
         a[oi] = (T)(v.x * scale);
-        b[oi] = (T)(v.y * scale);
+        if (b != nullptr) b[oi] = (T)(v.y * scale);
       } else {
         reinterpret_cast<C2<T>*>(a)[oi] = mk<T>((T)(v.x * scale), (T)(v.y * scale));
       }
@@ -322,6 +325,15 @@ void extract_t(const double2* F, void* a, void* b, int64_t L0, int64_t L1, int64
     hipLaunchKernelGGL((k_extract_t<T, false>), grid, dim3(256), 0, s, F, (T*)a, (T*)nullptr, L0, L1, H + 1, Ssrc,
                        compact_src, H, scale);
 }
+template <typename T>
+void extract_t_re(const double2* F, void* a, int64_t L0, int64_t L1, int64_t H, int64_t Ssrc, int compact_src,
+                  double scale, hipStream_t s) {
+  const dim3 grid((unsigned)((H + 1 + 31) / 32), (unsigned)((L0 + 31) / 32), (unsigned)L1);
+  hipLaunchKernelGGL((k_extract_t<T, true>), grid, dim3(256), 0, s, F, (T*)a, (T*)nullptr, L0, L1, H + 1, Ssrc,
+                     compact_src, H, scale);
+}
+template void extract_t_re<float>(const double2*, void*, int64_t, int64_t, int64_t, int64_t, int, double, hipStream_t);
+template void extract_t_re<double>(const double2*, void*, int64_t, int64_t, int64_t, int64_t, int, double, hipStream_t);
 template void extract_t<float>(const double2*, void*, void*, int64_t, int64_t, int64_t, int64_t, int, double, hipStream_t);
 template void extract_t<double>(const double2*, void*, void*, int64_t, int64_t, int64_t, int64_t, int, double, hipStream_t);
 
