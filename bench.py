@@ -203,8 +203,17 @@ def main():
     y = torch.empty_like(Knm)
     step = lambda: plan.apply(_lib.OP_K, Knm, out=y)
 
-    # ---- PCG wall-clock: compute_kn = setup + PCG(20) + R^T (untimed for the metric; it also
-    # brings the GPU to its steady clock before the timed steps) -------------------------------
+    def settle():
+        # sustained untimed load: the clock keeps rising over the first few hundred ms of
+        # back-to-back work (tools/step_profile.py: 0.300 -> 0.286 ms per K step over three
+        # 20-step rounds after 60 warm steps), so timed work runs at the steady clock
+        t_end = time.perf_counter() + args.settle_s
+        while time.perf_counter() < t_end:
+            for _ in range(20):
+                step()
+            torch.cuda.synchronize()
+
+    # ---- PCG wall-clock: compute_kn = setup + PCG(20) + R^T (untimed for the metric) ---------
     def compute_kn():
         Tk = ToeplitzTensor(grids, kf, batch_shape=None, jitter_val=1e-3)
         d0 = Tk.inv_matmul(Knm, do_precond=True, maxiter=20, tol=1e-8)
@@ -214,6 +223,7 @@ def main():
     if not args.kop_only:
         compute_kn()
         torch.cuda.synchronize()
+        settle()
         for _ in range(args.pcg_reps):
             torch.cuda.synchronize()
             t1 = time.perf_counter()
@@ -246,14 +256,7 @@ def main():
             pass_ms.append(time_events(fn, 20, stream))
 
     # ---- the metric: W warmup + K timed batched K matvec steps --------------------------------
-    # sustained untimed load first: the clock keeps rising over the first few hundred ms of
-    # back-to-back work (tools/step_profile.py: 0.300 -> 0.286 ms per step over three 20-step
-    # rounds after 60 warm steps), so the K timed steps run at the steady clock
-    t_end = time.perf_counter() + args.settle_s
-    while time.perf_counter() < t_end:
-        for _ in range(20):
-            step()
-        torch.cuda.synchronize()
+    settle()
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
