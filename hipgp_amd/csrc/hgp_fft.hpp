@@ -77,9 +77,15 @@ template <> __device__ __forceinline__ void buf_st_c2<float>(C2<float> v, BufRsr
   using V = decltype(__builtin_amdgcn_raw_buffer_load_b64(r, 0, 0, 0));
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(V, v), r, off, soff, 0);
 }
+// 128-bit stores never take an SGPR soffset: a store of more than 8 bytes reads its data VGPRs
+// after issue, and a VALU write of them in the next cycle changes the stored data of the last
+// lanes (run-to-run different fp64 results on contiguous lines, profiles/r3_buf64_race.txt).
+// LLVM's hazard recognizer inserts that wait state only when soffset is NOT a register
+// (GCNHazardRecognizer::createsVALUHazard), so the scalar offset is folded into the lane offset
+// here; the wait state then follows every such store (tools/hazard_lint.py checks the build).
 template <> __device__ __forceinline__ void buf_st_c2<double>(C2<double> v, BufRsrc r, uint32_t off, uint32_t soff) {
   using V = decltype(__builtin_amdgcn_raw_buffer_load_b128(r, 0, 0, 0));
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(V, v), r, off, soff, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(V, v), r, off + soff, 0, 0);
 }
 template <typename T> __device__ __forceinline__ T buf_ld(BufRsrc r, uint32_t off, uint32_t soff = 0);
 template <> __device__ __forceinline__ float buf_ld<float>(BufRsrc r, uint32_t off, uint32_t soff) {

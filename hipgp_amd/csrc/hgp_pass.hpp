@@ -366,7 +366,10 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
   // fp32 only: the fp64 form (128-bit raw buffer loads / stores) gave run-to-run different
   // results at the 1e-8 level on lines of >= 4 waves (tools/diag_contig.py REPEAT=1,
   // profiles/r2_fp64_contig_race.txt); the plain-pointer form is bitwise reproducible
-  constexpr bool BUF = std::is_same<T, float>::value && (LAY == LAY_CONTIG) && (TT % 64 == 0) && !CAN_FOLD;
+#ifndef HGP_BUF_F64
+#define HGP_BUF_F64 0
+#endif
+  constexpr bool BUF = (std::is_same<T, float>::value || HGP_BUF_F64) && (LAY == LAY_CONTIG) && (TT % 64 == 0) && !CAN_FOLD;
   const BufRsrc rin = buf_rsrc(BUF ? (const void*)in_c : nullptr,
                                (BUF && valid) ? (uint32_t)d.in.len * (uint32_t)sizeof(C2<T>) : 0u);
   const BufRsrc rout = buf_rsrc(BUF ? (const void*)out_c : nullptr,

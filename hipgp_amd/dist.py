@@ -60,14 +60,66 @@ def allreduce_stats(stats, group=None):
     return {"lam_sum": lam, "dm_sum": dm, "an_sum": small[0], "n": int(round(float(small[1])))}
 
 
+class AllRanksInvMatmul(torch.autograd.Function):
+    """`InvMatmul` (`_inv_matmul.py:9-64`) for one rank's share of the RHS, with the reference's
+    all-RHS break rule (`cg.py:69-71`) applied over every rank of `group`
+    (`ToeplitzPlan.pcg_allranks`) in BOTH solves: the forward K^-1 b and the backward's left
+    solves K^-1 grad (`_inv_matmul.py:34-36`), whose break the single process also decides over
+    all B gradient rows.  The column gradient is the rank's share of the quadratic form
+    (`_inv_matmul.py:52-60`, hgp_plan_dqf); `allreduce_hyper_grads` sums the shares.  A rank with
+    no RHS joins both solves' all-reduces (`pcg_idle_rank`) and contributes zero gradients, so
+    every rank must run backward (sharded_elbo_and_grad keeps a graph on empty ranks)."""
+
+    @staticmethod
+    def forward(ctx, tt, column, rhs, maxiter, tol, group):
+        ctx.tt, ctx.maxiter, ctx.tol, ctx.group = tt, int(maxiter), float(tol), group
+        x = _allranks_solve(tt, rhs.detach(), ctx.maxiter, ctx.tol, group)
+        ctx.save_for_backward(x)
+        return x
+
+    @staticmethod
+    def backward(ctx, grad):
+        (right,) = ctx.saved_tensors
+        left = _allranks_solve(ctx.tt, grad.detach().contiguous(), ctx.maxiter, ctx.tol, ctx.group)
+        gcol = None
+        if ctx.needs_input_grad[1]:
+            column = ctx.tt.column
+            if right.shape[0] == 0:
+                gcol = torch.zeros_like(column)
+            else:
+                with torch.no_grad():
+                    lv = torch.cat([left, right], 0)
+                    rv = torch.cat([right, left], 0).mul(-0.5)
+                    gcol = ctx.tt._plan.dqf(lv, rv).view(column.shape)
+        return None, gcol, (left if ctx.needs_input_grad[2] else None), None, None, None
+
+
+def _allranks_solve(tt, b, maxiter, tol, group):
+    """K^-1 b (PCG, preconditioned) with the break rule over all ranks; b may have 0 rows."""
+    with torch.no_grad():
+        if b.shape[0] == 0:
+            from hipgp_amd.plan import pcg_idle_rank
+            pcg_idle_rank(maxiter, b.device, group)
+            return b.new_zeros(b.shape)
+        tt.set_batch_shape(b.shape[:-1])       # as _solve does (toeplitz_tensor.py:61)
+        x, _ = tt._plan.pcg_allranks(b, maxiter, tol, precond=True, group=group)
+        return x
+
+
 def sharded_compute_kn(model, Knm_local, maxiter_cg=10, tol=1e-8, exact_break=None, group=None, Kmm=None):
     """kn = R^T K^{-1} Knm^T for this rank's rows (`hipgp.py:117-146`).  exact_break applies
     the all-RHS break rule across ranks (see module docstring); default: on for fp64 (where
-    tol = 1e-8 can be met) and off for fp32 (where it never is at these sizes).  A rank whose
-    shard is empty returns a (0, M') kn and still joins the break rule's all-reduces."""
+    tol = 1e-8 can be met) and off for fp32 (where it never is at these sizes).  The exact-break
+    solve is differentiable (AllRanksInvMatmul), like the reference's InvMatmul.  A rank whose
+    shard is empty returns a (0, M') kn and still joins the break rule's all-reduces (and, when
+    kn carries a graph, the backward solve's)."""
     if exact_break is None:
         exact_break = Knm_local.dtype == torch.float64
-    if Knm_local.shape[0] == 0:
+    # the solve carries a graph iff the kernel parameters are learned (column and Knm need grad);
+    # the same on every rank, so an empty rank then keeps it too
+    kernel_grad = (torch.is_grad_enabled() and bool(model.learn_kernel)
+                   and bool(model.log_sig2.requires_grad or model.log_ell.requires_grad))
+    if Knm_local.shape[0] == 0 and not (exact_break and kernel_grad):
         if exact_break:
             from hipgp_amd.plan import pcg_idle_rank
             pcg_idle_rank(maxiter_cg, Knm_local.device, group)
@@ -75,10 +127,13 @@ def sharded_compute_kn(model, Knm_local, maxiter_cg=10, tol=1e-8, exact_break=No
     if Kmm is None:
         Kmm = model.toeplitz()
     if exact_break:
-        Kmm.set_batch_shape(Knm_local.shape[:-1])   # as _solve does (toeplitz_tensor.py:61)
-        d0, _ = Kmm._plan.pcg_allranks(Knm_local, maxiter_cg, tol, precond=True, group=group)
+        d0 = AllRanksInvMatmul.apply(Kmm, Kmm.column, Knm_local, maxiter_cg, tol, group)
     else:
         d0 = Kmm.inv_matmul(Knm_local, do_precond=True, maxiter=maxiter_cg, tol=tol)
+    if Knm_local.shape[0] == 0:
+        # keep the solve in the graph (its backward joins the other ranks' all-reduces)
+        return Knm_local.new_zeros((0, model.Mprime)) + 0 * d0.sum()
+    Kmm.set_batch_shape(d0.shape[:-1])
     return Kmm._matmul_by_RT(d0)
 
 
@@ -112,7 +167,13 @@ def sharded_elbo_and_grad(model, xbatch, ybatch, noise_std_batch=None, maxiter_c
         if n_local > 0:
             share = model.autograd_elbo(xbatch[sl], ybatch[sl], nsd, Knm, Knn_diag, kn, nsum=n_local,
                                         bsz=xbatch.shape[0])
-            elbo = elbo.detach() + (share - share.detach())
+        else:
+            # an empty shard: a zero share that still holds a graph, so backward() runs here too
+            # (it joins the exact-break backward solve's all-reduces) and allreduce_hyper_grads
+            # is reached on every rank
+            params = [p for p in (model.log_sig2, model.log_ell, model.log_noise2) if p.requires_grad]
+            share = 0 * (kn.sum() + sum(p.sum() for p in params))
+        elbo = elbo.detach() + (share - share.detach())
     return elbo
 
 

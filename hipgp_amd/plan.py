@@ -268,13 +268,25 @@ def pcg_idle_rank(maxiter, device, group=None):
     import torch.distributed as dist
     gloo = dist.get_backend(group) == "gloo"
     flag = torch.ones(1, dtype=torch.int32, device="cpu" if gloo else device)
-    it = 0
-    for it in range(1, int(maxiter) + 1):
+    if gloo:
+        it = 0
+        for it in range(1, int(maxiter) + 1):
+            flag.fill_(1)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+            if int(flag.item()):
+                break
+        return it
+    # RCCL: no host round trip per iteration; count on the device the iterations up to and
+    # including the first whose reduced flag is 1 -- the count the active ranks report
+    # (hgp_pcg_iters) -- and read it once at the end
+    count = torch.zeros(1, dtype=torch.int32, device=device)
+    stopped = torch.zeros(1, dtype=torch.int32, device=device)
+    for _ in range(int(maxiter)):
         flag.fill_(1)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
-        if gloo and int(flag.item()):
-            break
-    return it
+        count += 1 - stopped
+        torch.maximum(stopped, flag, out=stopped)
+    return int(count.item())
 
 
 def sym_toeplitz_dqf(left_vectors, right_vectors):

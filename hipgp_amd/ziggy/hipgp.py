@@ -28,6 +28,7 @@ import torch
 from torch import nn
 
 from hipgp_amd.ziggy.misc.toeplitz_tensor import ToeplitzTensor
+from hipgp_amd.ziggy.svi_gp import SviGP
 
 LN_2PI = float(np.log(2 * np.pi))
 
@@ -40,67 +41,6 @@ def diag_kl_to_standard(m, S):
 def expanded_size(xgrids):
     """M' = prod(2 m_i - 2) (m_i > 1) else m_i  (`hipgp.py:72`)."""
     return int(np.prod([2 * len(g) - 2 if len(g) > 1 else len(g) for g in xgrids]))
-
-
-class SviGP(nn.Module):
-    """Base pieces of `ziggy/svi_gp.py:14-97` the models use: dtype coercion, the point
-    observation gram matrices (`_make_grams`, :48-76) and batched prediction (:78-97)."""
-
-    def __init__(self):
-        super().__init__()
-        self.pred_scale_factor = 1.
-
-    def torch(self, arr):
-        if isinstance(arr, np.ndarray):
-            return torch.tensor(arr, dtype=self.dtype)
-        if isinstance(arr, torch.Tensor):
-            assert arr.dtype == self.dtype, f"model dtype = {self.dtype}, data dtype = {arr.dtype}"
-            return arr
-        raise ValueError(f"Only accepts np.ndarray or torch.Tensor, got {type(arr)}")
-
-    def _make_grams(self, xbatch, integrated_obs=False, semi_integrated_estimator="analytic",
-                    semi_integrated_samps=10):
-        params = self.get_kernel_params()
-        if integrated_obs:
-            return self._make_integrated_grams(xbatch, params, semi_integrated_estimator, semi_integrated_samps)
-        Knm = None
-        if getattr(self, "xgrids", None) is not None:
-            from hipgp_amd.kuf import kuf_grid
-            Knm = kuf_grid(self.kernel, self.xgrids, xbatch, params)    # fused HIP kernel
-        if Knm is None:
-            Knm = self.kernel(xbatch, self.xinduce, params)
-        return Knm, self.kernel.diag(xbatch, params)
-
-    def _make_integrated_grams(self, xbatch, params, estimator, samps):
-        """Line-integral observations, `svi_gp.py:55-69`: Knm by the analytic SqExp integral or
-        the biased MC estimator (fused HIP kernels on the grid, `hipgp_amd.kuf`), Knn_diag by the
-        doubly-integrated table (`hgp_knn_doubly_diag`)."""
-        from hipgp_amd import kuf
-        grids = getattr(self, "xgrids", None)
-        if estimator == "analytic":
-            Knm = kuf.kuf_semi_sqexp(self.kernel, grids, xbatch, params) if grids is not None else None
-            if Knm is None:
-                Knm = self.kernel.k_semi(self.xinduce, xbatch, params).transpose(0, 1)
-        elif estimator == "mc-biased":
-            Knm = kuf.kuf_semi_mc(self.kernel, grids, xbatch, params, samps) if grids is not None else None
-            if Knm is None:
-                Knm = self.kernel.k_semi_mc(self.xinduce, xbatch, params, npts=samps).transpose(0, 1)
-        elif estimator == "numerical":
-            Knm = self.kernel.k_semi_num(self.xinduce, xbatch, params).transpose(0, 1)
-        else:
-            raise NotImplementedError
-        return Knm, self.kernel.k_doubly_diag(xbatch, params)
-
-    def batch_predict(self, x, batch_size, verbose=True, **kwargs):
-        nb = int(np.ceil(len(x) / batch_size))
-        mus, sigs = [], []
-        for b in range(nb):
-            mu, sig = self.predict(x[b * batch_size:(b + 1) * batch_size], **kwargs)
-            mus.append(mu)
-            sigs.append(sig)
-            if verbose and b % 100 == 0:
-                print(" ... batch_predict %d / %d batches" % (b, nb))
-        return torch.cat(mus, dim=0), torch.cat(sigs, dim=0)
 
 
 class ToeplitzInducingGP(SviGP):
@@ -257,6 +197,72 @@ class ToeplitzInducingGP(SviGP):
             # `hipgp.py:214-227`, with the variational parameters held fixed (`:216-217`)
             elbo = self.autograd_elbo(xbatch, ybatch, noise_std_batch, Knm, Knn_diag, kn)
         return elbo
+
+    def batch_solve(self, xobs, yobs, noise_std=None, batch_size=-1, maxiter_cg=10, integrated_obs=False,
+                    semi_integrated_estimator="analytic", semi_integrated_samps=10, compute_elbo=False,
+                    Kmm=None, print_debug_info=False):
+        """Closed-form variational parameters from all observations (`hipgp.py:278-368`):
+           lam  = I_lam + sum_n ivar_n kn_n kn_n^T restricted to the family (diag / blocks),
+           b    = sum_n ivar_n y_n kn_n,
+           m    = (I + sum_n ivar_n kn_n kn_n^T)^{-1} b   (dense M' x M' solve),
+           theta2 = -lam / 2, theta1 = lam m (mean-field) / blockdiag(lam) m (block);
+        with compute_elbo the ELBO of the solved model over the same batches.
+
+        kn per batch is the device compute_kn (one plan reused for every batch: the reference
+        builds an identical ToeplitzTensor per call, `:294`).  The dense M' x M' system limits this
+        to small grids (M' = 1444 on 20 x 20), as in the reference.  The reference reads
+        `noise_std_batch` before assigning it (`:314`, UnboundLocalError on every call); here the
+        intended rule holds: per-observation noise_std[bi] when given, else exp(-log_noise2)."""
+        if xobs.shape[0] != self.N:
+            print("x obs shape = {}, total_num_obs = {}".format(xobs.shape[0], self.N))
+        if batch_size == -1:
+            batch_size = xobs.shape[0]
+        nb = int(np.ceil(len(xobs) / batch_size))
+        batches = [slice(i * batch_size, min((i + 1) * batch_size, len(xobs))) for i in range(nb)]
+        dev = self.xgrids[0].device
+        if self.whitened_type == 'cholesky':
+            Kmm = self.kernel(self.xinduce, self.xinduce, self.get_kernel_params())
+        elif Kmm is None:
+            Kmm = self.toeplitz()
+        gram_kw = dict(integrated_obs=integrated_obs, semi_integrated_estimator=semi_integrated_estimator,
+                       semi_integrated_samps=semi_integrated_samps)
+
+        def noise_of(bi):
+            return None if noise_std is None else noise_std[bi].to(dev)
+
+        lam = self.get_identity_for_lam()
+        b = 0
+        big_lam = torch.eye(self.Mprime, dtype=self.dtype, device=dev)
+        with torch.no_grad():
+            for bi in batches:
+                xb, yb = xobs[bi].to(dev), yobs[bi].to(dev)
+                Knm, _ = self._make_grams(xb, **gram_kw)
+                kn = self.compute_kn(Knm, maxiter_cg=maxiter_cg, Kmm=Kmm)
+                sb = noise_of(bi)
+                ivar = 1 / sb ** 2 if sb is not None else torch.exp(-self.log_noise2)
+                lam = lam + self.get_lam(ivar_noise=ivar, kn=kn, bscale=1.0, add_identity=False)
+                b = b + torch.sum(ivar * yb * kn, dim=0)
+                big_lam += (ivar * kn).t().matmul(kn)
+            mhat = torch.linalg.solve(big_lam, b[:, None])
+            if self.parameterization == 'standard':
+                self.global_S.data[:] = self.get_S_from_lam(lam)
+                self.global_m.data[:] = mhat
+            else:
+                self.global_theta2.data[:] = -.5 * lam
+                if self.name == 'mean-field':
+                    self.global_theta1.data[:] = (mhat.squeeze() * lam.squeeze())[:, None]
+                else:
+                    self.global_theta1.data[:] = self.block_diag_multiply(lam, mhat.t()).t()
+        if not compute_elbo:
+            return None
+        qm, qS = self.standard_variational_params()
+        elbo = 0
+        for bi in batches:
+            an = self.compute_batch_an(xobs[bi].to(dev), yobs[bi].to(dev), noise_of(bi), qm=qm, qS=qS,
+                                       maxiter_cg=maxiter_cg, Kmm=Kmm, print_debug_info=print_debug_info,
+                                       **gram_kw)
+            elbo += torch.sum(an)
+        return elbo / xobs.shape[0] - self.get_kl_to_prior(qm, qS) / self.N
 
     def hyper_grad_needed(self, noise_std_batch=None):
         """True when the ELBO must carry an autograd graph to the kernel / noise parameters."""

@@ -411,3 +411,30 @@ def block_elbo_and_grad(kn, y, Knn_diag, theta1, theta2, idx, N, ivar, log_sd):
     dS = -0.5 * lam - theta2
     deta1 = dm + block_diag_multiply(dS, -2 * qm.T, idx).T
     return elbo, -deta1, -dS, an, knSkn
+
+
+# --------------------------------------------------------------------------------------
+# full-batch solve of the mean-field family (ziggy/hipgp.py:278-368)
+# --------------------------------------------------------------------------------------
+def meanfield_batch_solve(kn, y, Knn_diag, ivar, log_sd, N):
+    """`hipgp.py:296-345` ('mean-field', expectation family) given every observation's kn
+    (n, M'): lam = 1 + sum_n ivar_n kn_n^2, b = sum_n ivar_n y_n kn_n, m = (I + sum_n ivar_n
+    kn_n kn_n^T)^{-1} b, theta2 = -lam/2, theta1 = m lam; and the ELBO of `:347-368`
+    (mean_n a_n - KL/N, shared or per-observation noise).  The reference's own batch_solve
+    raises UnboundLocalError at `:314` before any of this runs (see hipgp_amd batch_solve).
+    Returns (theta1 (M',1), theta2 (M',1), elbo)."""
+    n, Mp = kn.shape
+    iv = np.broadcast_to(np.asarray(ivar, dtype=kn.dtype).reshape(-1), (n,))
+    lsd = np.broadcast_to(np.asarray(log_sd, dtype=kn.dtype).reshape(-1), (n,))
+    y = y.reshape(-1)
+    lam = 1 + np.einsum("n,nm->m", iv, kn * kn)
+    b = kn.T @ (iv * y)
+    big = np.eye(Mp) + (kn * iv[:, None]).T @ kn
+    m = np.linalg.solve(big, b)
+    theta1, theta2 = (m * lam)[:, None], (-0.5 * lam)[:, None]
+    S = 1 / lam
+    knm = kn @ m
+    an = (-0.5 * iv * ((knm - y) ** 2 + Knn_diag.reshape(-1) - np.sum(kn * kn, -1) + (kn * kn) @ S)
+          - lsd - 0.5 * np.log(2 * np.pi))
+    kl = 0.5 * (S.sum() + m @ m - np.log(S).sum() - Mp)
+    return theta1, theta2, an.mean() - kl / N

@@ -1,0 +1,113 @@
+"""The SVI driver and the full-batch solve on the GPU path.
+
+* `svigp_fit` (`ziggy/svi_gp.py:172-442`) through `SviGP.fit`: one epoch of 4 minibatches
+  against the reference's own trajectory (G18, `tests/golden/make_golden_fit.py`): the
+  variational parameters at the start of every batch and after the fit, the ELBO trace, and
+  with learn_kernel the Adam-updated log_ell / log_sig2.
+* `batch_solve` (`hipgp.py:278-368`) against the oracle restatement
+  (`oracle.ziggy_oracle.meanfield_batch_solve`) on the reference-made kn of G5.
+"""
+import numpy as np
+import pytest
+import torch
+
+from golden_cases import load, rel_err
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _fit_model(fx, case, dtype):
+    import ziggy.hipgp as hg
+    import ziggy.kernels as zk
+    grids = [torch.tensor(fx[f"{case}_grid0"], dtype=dtype), torch.tensor(fx[f"{case}_grid1"], dtype=dtype)]
+    mod = hg.MeanFieldToeplitzGP(zk.Matern(nu=1.5, dtype=dtype), grids, num_obs=64, sig2_init=1., ell_init=.15,
+                                 noise2_init=.01, init_Svar=.5, learn_kernel=case == "hk", learn_noise=False,
+                                 dtype=dtype)
+    with torch.no_grad():
+        mod.global_theta1.copy_(torch.tensor(fx[f"{case}_theta1_init"], dtype=dtype))
+        mod.global_theta2.copy_(torch.tensor(fx[f"{case}_theta2_init"], dtype=dtype))
+    return mod
+
+
+def _run_fit(fx, case, dtype, tmp_path):
+    mod = _fit_model(fx, case, dtype)
+    snaps = []
+
+    def batch_cb(m, xb, yb, sb):
+        assert xb.is_cuda and sb.is_cuda
+        snaps.append([m.global_theta1.detach().double().cpu().numpy().copy(),
+                      m.global_theta2.detach().double().cpu().numpy().copy(),
+                      float(m.log_sig2), float(m.log_ell)])
+
+    traces = []
+
+    def epoch_cb(odir, m, *args, **kw):
+        traces.append(list(args[15]))
+        return (None,) * 6
+
+    x, y, s = (fx[f"{case}_{k}"].astype(np.float64 if dtype == torch.float64 else np.float32) for k in "xys")
+    mod.fit(str(tmp_path), x, y, s, None, None, None, None, None, None, batch_callback=batch_cb,
+            epoch_callback=epoch_cb, do_cuda=True, lr=.05, step_decay=.9, batch_size=16, epochs=1,
+            maxiter_cg=20, kernel_lr=.05, batch_log_interval=1, learn_kernel=case == "hk")
+    batch_cb(mod, torch.zeros(1, device=DEV), None, torch.zeros(1, device=DEV))
+    assert (tmp_path / "time_report.csv").exists()
+    return snaps, traces[0]
+
+
+@pytest.mark.parametrize("case", ["ng", "hk"])
+def test_svigp_fit_trajectory_fp64(case, tmp_path):
+    fx = load("G18", "f64")
+    snaps, trace = _run_fit(fx, case, torch.float64, tmp_path)
+    assert len(snaps) == 5
+    for k, sn in enumerate(snaps):
+        assert rel_err(sn[0], fx[f"{case}_theta1_steps"][k]) < 1e-7, k
+        assert rel_err(sn[1], fx[f"{case}_theta2_steps"][k]) < 1e-7, k
+        assert abs(sn[2] - fx[f"{case}_log_sig2_steps"][k]) < 1e-8, k
+        assert abs(sn[3] - fx[f"{case}_log_ell_steps"][k]) < 1e-8, k
+    assert np.allclose(trace, fx[f"{case}_elbo_trace"], rtol=1e-7, atol=0)
+
+
+@pytest.mark.parametrize("case", ["ng", "hk"])
+def test_svigp_fit_trajectory_fp32(case, tmp_path):
+    """fp32 (the reference's model dtype): no worse than 4x the reference's own fp32 error
+    vs its fp64 run, per recorded step."""
+    fx32, fx64 = load("G18", "f32"), load("G18", "f64")
+    snaps, trace = _run_fit(fx32, case, torch.float32, tmp_path)
+    for k, sn in enumerate(snaps):
+        for j, name in ((0, "theta1"), (1, "theta2")):
+            ref64 = fx64[f"{case}_{name}_steps"][k]
+            e_me = np.linalg.norm(sn[j] - ref64)
+            e_ref = np.linalg.norm(fx32[f"{case}_{name}_steps"][k].astype(np.float64) - ref64)
+            assert e_me <= 4 * e_ref + 1e-6 * np.linalg.norm(ref64), (k, name, e_me, e_ref)
+    t64 = fx64[f"{case}_elbo_trace"]
+    e_me = np.abs(np.array(trace) - t64)
+    e_ref = np.abs(fx32[f"{case}_elbo_trace"].astype(np.float64) - t64)
+    assert np.all(e_me <= 4 * e_ref + 1e-5 * np.abs(t64)), (e_me, e_ref)
+
+
+@pytest.mark.parametrize("noise", ["shared", "per_obs"])
+def test_batch_solve_meanfield_G5(noise):
+    from oracle import ziggy_oracle as zo
+    import ziggy.hipgp as hg
+    import ziggy.kernels as zk
+    fx = load("G5", "f64")
+    dt = torch.float64
+    grids = [torch.tensor(fx["grid0"], dtype=dt), torch.tensor(fx["grid1"], dtype=dt)]
+    mod = hg.MeanFieldToeplitzGP(zk.Matern(nu=1.5, dtype=dt), grids, num_obs=64, sig2_init=1., ell_init=.1,
+                                 noise2_init=.01, learn_kernel=False, dtype=dt).cuda_params(0)
+    x = torch.tensor(fx["xobs"], device=DEV)
+    y = torch.tensor(fx["yobs"], device=DEV)
+    sd = None
+    ivar, log_sd = 100.0, 0.5 * np.log(.01)
+    if noise == "per_obs":
+        sdv = np.linspace(.05, .2, 64)[:, None]
+        sd = torch.tensor(sdv, device=DEV)
+        ivar, log_sd = 1 / sdv[:, 0] ** 2, np.log(sdv[:, 0])
+    elbo = mod.batch_solve(x, y, sd, batch_size=16, maxiter_cg=20, compute_elbo=True)
+    t1, t2, elbo_ref = zo.meanfield_batch_solve(fx["kn"], fx["yobs"], fx["Knn_diag"], ivar, log_sd, 64)
+    assert rel_err(mod.global_theta2.detach().cpu().numpy(), t2) < 1e-8
+    assert rel_err(mod.global_theta1.detach().cpu().numpy(), t1) < 1e-6
+    if noise == "shared":
+        # per-observation noise keeps the reference's (bsz, bsz) broadcast of a_n (hipgp.py:396-398)
+        assert abs(float(elbo) - elbo_ref) < 1e-7 * abs(elbo_ref)

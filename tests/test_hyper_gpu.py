@@ -112,3 +112,53 @@ def test_sharded_hyper_grads_two_ranks():
         assert abs(elbo - float(fx["elbo"])) < 1e-8 * abs(float(fx["elbo"]))
         assert rel_err(g1, fx["theta1_grad"]) < 1e-7
         assert np.all(np.abs(gh - ref) <= 1e-6 * np.abs(ref) + 1e-9), (gh, ref)
+
+
+def _worker_exact(rank, world_size, port, out, nobs):
+    """The default exact_break (on for fp64): the all-ranks break rule in the forward AND the
+    backward solve (AllRanksInvMatmul), with the kernel hyper-parameters learned."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world_size)
+    try:
+        from hipgp_amd import dist as hdist
+        torch.cuda.set_device(0)
+        fx = load("G16", "f64")
+        mod = _model(fx, "G16", torch.float64)
+        x = torch.tensor(fx["xobs"], device=DEV)[:nobs]
+        y = torch.tensor(fx["yobs"], device=DEV)[:nobs]
+        elbo = hdist.sharded_elbo_and_grad(mod, x, y, maxiter_cg=20)
+        assert elbo.requires_grad, "the exact-break kn must carry the autograd graph (ADVICE r2)"
+        elbo.backward()
+        hdist.allreduce_hyper_grads(mod)
+        out[rank] = (float(elbo), mod.global_theta1.grad.cpu().numpy(), _hyper(mod))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world_size,nobs", [(2, 40), (3, 2)])
+def test_sharded_hyper_grads_exact_break(world_size, nobs):
+    """fp64 with the default exact_break: every rank's ELBO, natural gradient and summed
+    hyper-parameter gradients equal the single-process values (G16 itself for the full batch;
+    for a 2-row minibatch on 3 ranks -- one empty shard -- the single-process GPU run)."""
+    fx = load("G16", "f64")
+    if nobs == 40:
+        ref_elbo, ref_g1 = float(fx["elbo"]), fx["theta1_grad"]
+        ref_h = np.array([float(fx[k]) for k in HYPER])
+    else:
+        mod = _model(fx, "G16", torch.float64)
+        x = torch.tensor(fx["xobs"], device=DEV)[:nobs]
+        y = torch.tensor(fx["yobs"], device=DEV)[:nobs]
+        e = mod.elbo_and_grad(x, y, maxiter_cg=20)
+        e.backward()
+        ref_elbo, ref_g1, ref_h = float(e), mod.global_theta1.grad.cpu().numpy(), _hyper(mod)
+    mgr = mp.Manager()
+    out = mgr.dict()
+    port = 29800 + os.getpid() % 90 + world_size
+    mp.spawn(_worker_exact, args=(world_size, port, out, nobs), nprocs=world_size, join=True)
+    for r in range(world_size):
+        elbo, g1, gh = out[r]
+        assert abs(elbo - ref_elbo) < 1e-8 * abs(ref_elbo)
+        assert rel_err(g1, ref_g1) < 1e-7
+        assert np.all(np.abs(gh - ref_h) <= 1e-6 * np.abs(ref_h) + 1e-9), (gh, ref_h)

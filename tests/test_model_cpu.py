@@ -147,3 +147,48 @@ def test_hyper_grad_needed_flags():
     assert not mod.hyper_grad_needed(torch.ones(3, 1, dtype=torch.float64))
     with torch.no_grad():
         assert not mod.hyper_grad_needed()
+
+
+def _dist_worker_hyper_short(rank, world_size, port, out):
+    """learn_noise with a 2-row minibatch on 3 ranks: one empty shard still runs backward()."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world_size)
+    try:
+        from hipgp_amd import dist as hdist
+        fx = load("G5", "f64")
+        mod = _model(fx)
+        mod.log_noise2.requires_grad_(True)
+        kn_full = torch.tensor(fx["kn"])[:2]
+        x, y = torch.tensor(fx["xobs"])[:2], torch.tensor(fx["yobs"])[:2]
+        sl = hdist.rhs_shard(2, world_size, rank)
+        elbo = hdist.sharded_elbo_and_grad(mod, x, y, compute_kn=lambda model, Knm_local: kn_full[sl])
+        elbo.backward()
+        hdist.allreduce_hyper_grads(mod)
+        out[rank] = (float(elbo), float(mod.log_noise2.grad))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_hyper_grad_empty_shard_gloo():
+    """an empty shard with hyper-parameter learning must run backward() and reach
+    allreduce_hyper_grads (no exception on that rank, no hang on the others); every rank gets
+    the single-process log_noise2 gradient (`hipgp.py:214-227` with the noise learned)."""
+    fx = load("G5", "f64")
+    mod = _model(fx)
+    mod.log_noise2.requires_grad_(True)
+    x, y = torch.tensor(fx["xobs"])[:2], torch.tensor(fx["yobs"])[:2]
+    _, Knn = mod._make_grams(x)
+    ref = mod.autograd_elbo(x, y, None, None, Knn, torch.tensor(fx["kn"])[:2])
+    ref.backward()
+    g_ref = float(mod.log_noise2.grad)
+    mgr = mp.Manager()
+    out = mgr.dict()
+    port = 29500 + os.getpid() % 1000 + 11
+    mp.spawn(_dist_worker_hyper_short, args=(3, port, out), nprocs=3, join=True)
+    assert len(out) == 3
+    for r in range(3):
+        elbo, g = out[r]
+        assert abs(elbo - float(ref)) < 1e-12 * abs(float(ref))
+        assert abs(g - g_ref) < 1e-12 * abs(g_ref), (g, g_ref)

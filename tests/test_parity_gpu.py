@@ -281,12 +281,16 @@ def test_large_grid_fp32_vs_fp64(m):
 
 @pytest.mark.parametrize("dims,dtype", [((1025, 8), torch.float64), ((2048, 8), torch.float64), ((4096, 8), torch.float64),
                                         ((8, 2048), torch.float64), ((600, 600), torch.float64),
-                                        ((2048, 2048), torch.float32), ((1024, 1024), torch.float32)],
-                         ids=["1025x8_f64", "2048x8_f64", "4096x8_f64", "8x2048_f64", "600x600_f64", "C3_f32", "C2_f32"])
+                                        ((2048, 2048), torch.float32), ((1024, 1024), torch.float32),
+                                        ((4096, 8), torch.float32), ((4096, 4096), torch.float32)],
+                         ids=["1025x8_f64", "2048x8_f64", "4096x8_f64", "8x2048_f64", "600x600_f64", "C3_f32", "C2_f32",
+                              "4096x8_f32", "C4_f32"])
 def test_long_lines_accuracy_and_repeatability(dims, dtype):
     """Contiguous-line passes with lines of several waves (axis-0 columns of 2048 / 4096 points,
     fp64 setup DCTs along long rows): fp64 ops at fp64 accuracy against the oracle, and every op
-    bitwise identical from run to run (a race once showed as 1e-8 run-to-run noise in fp64)."""
+    bitwise identical from run to run (a race once showed as 1e-8 run-to-run noise in fp64: the
+    VMEM store-data hazard of 128-bit stores).  fp32 lines of 4 waves (4096 points,
+    C4) against the fp64 oracle / the fp64 plan of the same grid."""
     from hipgp_amd import _lib
     from hipgp_amd.plan import ToeplitzPlan
     grids = [np.linspace(-1, 1, m) for m in dims]
@@ -299,6 +303,18 @@ def test_long_lines_accuracy_and_repeatability(dims, dtype):
         ys = [P.apply(op, vt) for _ in range(4)]
         for y in ys[1:]:
             assert torch.equal(y, ys[0]), op
+    if dtype == torch.float32:
+        if np.prod(dims) < 5e6:
+            T = zo.ToeplitzOracle(col, dims)
+            refs = {_lib.OP_K: T.matmul_K(v), _lib.OP_RT: T.matmul_RT(v)}
+        else:       # C4: the fp64 plan of the same grid (itself pinned by the fp64 cases)
+            P64 = ToeplitzPlan(dims, torch.float64, DEV)
+            P64.set_column(torch.tensor(col, device=DEV))
+            v64 = torch.tensor(v, device=DEV)
+            refs = {op: _np(P64.apply(op, v64)) for op in (_lib.OP_K, _lib.OP_RT)}
+            del P64, v64
+        for op, ref in refs.items():
+            assert rel_err(_np(P.apply(op, vt)), ref) < 5e-6, op
     if dtype == torch.float64 and np.prod(dims) < 5e6:
         T = zo.ToeplitzOracle(col, dims)
         assert rel_err(P.spectrum(_lib.SPEC_D).cpu().numpy(), T.D) < 1e-12
