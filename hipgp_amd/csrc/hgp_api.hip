@@ -35,6 +35,13 @@ int fail(int code, const std::string& msg) {
     if (_rc != 0) return _rc;                                                                      \
   } while (0)
 
+// smallest 3 * 2^k >= v with k >= 3 (a transform half-length 3 * 2^(k-1) >= 12, hgp_fft.hpp is_tri)
+int64_t next_tri(int64_t v) {
+  int64_t t = 24;
+  while (t < v) t <<= 1;
+  return t;
+}
+
 int64_t next_pow2(int64_t v) {
   int64_t p = 1;
   while (p < v) p <<= 1;
@@ -285,9 +292,11 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
   // 2-D: column-major intermediate W[q][c][i0], c < H1 + 1, column pitch S0 (hgp_rows.hpp);
   // rows whose row-pair kernels do not fit one CU's LDS (fp64 H >= 8192) take the generic
   // sequence instead: row pairs -> row-major [q][i0][c] -> strided axis-0 conv -> row pairs
-  const bool gen2 = d == 2 && !rowt_fits<T>((int)(g.L[1] / 2));
+  const bool gen2 = d == 2 && !rowt_fits<T>((int)(g.L[1] / 2), 1);
+  // long fp32 rows: the 2-D intermediate in the grouped-column layout (hgp_rows.hpp)
+  const int G2 = (d == 2 && !gen2) ? rowt_group<T>((int)(g.L[1] / 2)) : 1;
   const int64_t S0 = (d >= 2) ? round_up(std::max(g.in[0], g.out[0]), 16) : 0;   // axis-0 pitch
-  if (d == 2) B1 = gen2 ? std::max(g.in[0], g.out[0]) * Sl : (g.L[1] / 2 + 1) * S0;
+  if (d == 2) B1 = gen2 ? std::max(g.in[0], g.out[0]) * Sl : (g.L[1] / 2 + G2) / G2 * G2 * S0;
   if (gen2 && (spart != nullptr || epi != nullptr || mid != nullptr))
     return fail(HGP_E_ARG, "internal: the generic 2-D sequence has no fused PCG epilogue");
   // 3-D (hgp_lines.hpp): the (i1, i2) plane of every (RHS, i0) goes through the 2-D row-pair
@@ -295,7 +304,7 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
   // W2 [q][c2][k1][i0] (axis-0 pitch S0), whose axis-0 lines the contiguous conv pass takes.
   // Kernels that do not fit one CU's LDS (fp64 at H >= 8192) take the row-major 5-pass
   // sequence with strided middle passes instead (gen3).
-  const bool gen3 = d == 3 && (!rowt_fits<T>((int)(g.L[2] / 2)) || !linet_fits<T>((int)(g.L[1] / 2)));
+  const bool gen3 = d == 3 && (!rowt_fits<T>((int)(g.L[2] / 2), 0) || !linet_fits<T>((int)(g.L[1] / 2)));
   const int64_t S1 = (d == 3) ? round_up(std::max(g.in[1], g.out[1]), 16) : 0;
   if (d == 3) {
     const int64_t P0 = std::max(g.in[0], g.out[0]), NC2 = g.L[2] / 2 + 1;
@@ -393,7 +402,7 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
       auto run_rowt = [&](int inv, PassDesc& D, int epi_mode) -> int {
         const int me = pass_no++;
         if (only_pass >= 0 && only_pass != me) return 0;
-        hipError_t e = launch_rowt<T>((int)H1, inv, epi_mode, D, st);
+        hipError_t e = launch_rowt<T>((int)H1, inv, epi_mode, D, st, 1);
         if (e == hipErrorNotSupported)
           return fail(HGP_E_UNSUPPORTED, "row transform of H = " + std::to_string(H1) +
                                              " points does not fit one CU's LDS in this dtype (use fp32)");
@@ -401,6 +410,7 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
         return 0;
       };
       // A: FWD along axis 1, row pairs of each RHS -> column-major half spectra w1 [q][c1][i0]
+      //    (grouped by G2 columns: w1 [q][c1 / G2][i0][c1 % G2])
       PassDesc A = base_desc();
       A.in = View{(void*)xi, g.in_M, g.in[1], 1, (int)g.in[1]};
       A.out = View{w1, B1, S0, 1, 0};
@@ -416,7 +426,12 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
         Bd.spart = reinterpret_cast<T*>(spart) + q0 * (H1 + 1);
         Bd.spart_mid = (int)(H1 / 2);
       }
-      HGP_TRY(run((int)(g.L[0] / 2), conv_mode, LAY_CONTIG, Bd, (int64_t)qn * Bd.Rn));
+      if (G2 > 1) {     // lines (column group, RHS, column in group): ceil(Rn / G2) G2 per RHS
+        Bd.grp = G2;
+        HGP_TRY(run((int)(g.L[0] / 2), conv_mode, LAY_CONTIG_G, Bd, (int64_t)qn * ((H1 + G2) / G2) * G2));
+      } else {
+        HGP_TRY(run((int)(g.L[0] / 2), conv_mode, LAY_CONTIG, Bd, (int64_t)qn * Bd.Rn));
+      }
       if (mid != nullptr) (*mid)(q0, qn, st);
       // C: INV along axis 1: column-major tiles -> row pairs, crop, fused dot or PCG update
       PassDesc Cd = base_desc();
@@ -427,7 +442,7 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
       int epi_mode = EPI_OUT;
       if (epi != nullptr) {
         epi_mode = epi->mode;
-        const int nrb = (Cd.Rn + rowt_pairs<T>((int)H1) - 1) / rowt_pairs<T>((int)H1);
+        const int nrb = (Cd.Rn + rowt_pairs<T>((int)H1, 1) - 1) / rowt_pairs<T>((int)H1, 1);
         Cd.cg_r = reinterpret_cast<T*>(epi->r) + q0 * g.out_M;
         Cd.cg_x = reinterpret_cast<T*>(epi->x) + q0 * g.out_M;
         Cd.cg_p = reinterpret_cast<T*>(epi->p) + q0 * g.out_M;
@@ -443,7 +458,7 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
       auto run_rowt = [&](int inv, PassDesc& D, int epi_mode) -> int {
         const int me = pass_no++;
         if (only_pass >= 0 && only_pass != me) return 0;
-        hipError_t e = launch_rowt<T>((int)H2, inv, epi_mode, D, st);
+        hipError_t e = launch_rowt<T>((int)H2, inv, epi_mode, D, st, 0);
         if (e != hipSuccess) return fail(HGP_E_HIP, std::string("3-D row pass launch: ") + hipGetErrorString(e));
         return 0;
       };
@@ -497,7 +512,7 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
       int epi_mode = EPI_OUT;
       if (epi != nullptr) {
         epi_mode = epi->mode;
-        const int nrb = (E.Rn + rowt_pairs<T>((int)H2) - 1) / rowt_pairs<T>((int)H2);
+        const int nrb = (E.Rn + rowt_pairs<T>((int)H2, 0) - 1) / rowt_pairs<T>((int)H2, 0);
         E.cg_r = reinterpret_cast<T*>(epi->r) + q0 * g.out_M;
         E.cg_x = reinterpret_cast<T*>(epi->x) + q0 * g.out_M;
         E.cg_p = reinterpret_cast<T*>(epi->p) + q0 * g.out_M;
@@ -825,7 +840,7 @@ int slab_pass_t(hgp_plan* P, int op, int stage, const void* in, void* out, int64
   hipStream_t st = P->stream;
   const size_t cs = sizeof(C2<T>);
   auto rowt = [&](int inv, PassDesc& D, int64_t H) -> int {
-    hipError_t e = launch_rowt<T>((int)H, inv, EPI_OUT, D, st);
+    hipError_t e = launch_rowt<T>((int)H, inv, EPI_OUT, D, st, 0);
     if (e == hipErrorNotSupported)
       return fail(HGP_E_UNSUPPORTED, "row transform of H = " + std::to_string(H) + " points does not fit one CU's LDS");
     if (e != hipSuccess) return fail(HGP_E_HIP, std::string("slab row pass: ") + hipGetErrorString(e));
@@ -915,7 +930,7 @@ int slab_pass_t(hgp_plan* P, int op, int stage, const void* in, void* out, int64
 // those fit one CU's LDS; the dot partials then come per (plane, row pair)
 template <typename T>
 bool planes3d(const hgp_plan* P) {
-  return P->d == 3 && rowt_fits<T>((int)(P->LK[2] / 2)) != 0 && linet_fits<T>((int)(P->LK[1] / 2)) != 0;
+  return P->d == 3 && rowt_fits<T>((int)(P->LK[2] / 2), 0) != 0 && linet_fits<T>((int)(P->LK[1] / 2)) != 0;
 }
 template <typename T>
 int rn_last(const hgp_plan* P) {
@@ -935,15 +950,15 @@ int spec_np(const hgp_plan* P) {
 // the fused PCG needs the row-pair kernels of the K / C^-1 rows
 template <typename T>
 bool fused_pcg(const hgp_plan* P) {
-  return (P->d == 2 && rowt_fits<T>((int)(P->LK[1] / 2)) != 0) || planes3d<T>(P);
+  return (P->d == 2 && rowt_fits<T>((int)(P->LK[1] / 2), 1) != 0) || planes3d<T>(P);
 }
 template <typename T>
 int xr_np(const hgp_plan* P) {
   if (P->d == 2) {
-    const int pairs = rowt_pairs<T>((int)(P->LK[1] / 2));
+    const int pairs = rowt_pairs<T>((int)(P->LK[1] / 2), 1);
     return (int)(((P->m[0] + 1) / 2 + pairs - 1) / pairs);
   }
-  const int pairs = rowt_pairs<T>((int)(P->LK[2] / 2));
+  const int pairs = rowt_pairs<T>((int)(P->LK[2] / 2), 0);
   return (int)(P->m[0] * (((P->m[1] + 1) / 2 + pairs - 1) / pairs));
 }
 
@@ -1040,8 +1055,8 @@ int pcg_step_t(hgp_plan* P, double tol) {
     // tile (6 %) measured 280 -> 285 ms, and folded partials (C4 after the fold, C5) +1 % / +-0,
     // so those keep the fold + small-kernel form.
     const int Hl = (int)(P->LK[P->d - 1] / 2);
-    const int thr = rowt_threads<T>(Hl);
-    const int64_t tile_vals = 2 * (int64_t)(Hl + 1) * 2 * rowt_pairs<T>(Hl);   // reals per block tile
+    const int thr = rowt_threads<T>(Hl, P->d == 2);
+    const int64_t tile_vals = 2 * (int64_t)(Hl + 1) * 2 * rowt_pairs<T>(Hl, P->d == 2);   // reals per block tile
     const bool direct = nps0 <= CG_LOADS * thr && 25 * (int64_t)nps0 <= tile_vals;
     const int G = direct ? 0 : fold_groups(nps0);
     const int nps = G > 0 ? G : nps0;
@@ -1152,6 +1167,27 @@ int hgp_plan_create(int device, int ndim, const int64_t* m, int dtype, int64_t m
     ++d;
   }
   P->d = d;
+  // R / R^T length.  Exact for any L_R >= n + m - 1 = 3m - 3 per axis.  Default: the
+  // power of two >= 2n, where the filter embeds evenly and the spectrum is real (r_real).  The
+  // shortest admissible lengths -- 2^k or 3 * 2^k >= 3m - 3 -- take a complex spectrum instead;
+  // they are used when their grid is below 0.6 of the real one's (a complex-spectrum point costs
+  // more: C5's 768 x 768 x 384 is 0.42 of 1024 x 1024 x 512).  HGP_LR=pow2 keeps the default.
+  {
+    const char* lr = std::getenv("HGP_LR");
+    const bool allow = !(lr && std::string(lr) == "pow2");
+    double real_pts = 1, short_pts = 1;
+    int64_t Ls[3] = {1, 1, 1};
+    bool ok = allow && d >= 2;
+    for (int a = 0; a < d; ++a) {
+      const int64_t need = 3 * P->m[a] - 3;
+      Ls[a] = std::min(next_pow2(need), next_tri(need));
+      real_pts *= (double)P->LR[a];
+      short_pts *= (double)Ls[a];
+      if (Ls[a] / 2 > 8192) ok = false;      // the fp64 set-up transforms hold L_R / 2 <= 8192
+    }
+    if (ok && short_pts < 0.6 * real_pts)
+      for (int a = 0; a < d; ++a) P->LR[a] = Ls[a];
+  }
   if (d == 0) { delete P; return fail(HGP_E_UNSUPPORTED, "a grid with every axis of size 1 (M = 1) is not supported"); }
   for (int a = 0; a < d; ++a) {
     // L_R / 2 = 16384 (axes of 4098..8192 points): fp32 operator passes hold one such line per

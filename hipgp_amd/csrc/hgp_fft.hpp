@@ -109,10 +109,37 @@ template <typename T> struct PMax;
 template <> struct PMax<float> { static constexpr int v = 16; };
 template <> struct PMax<double> { static constexpr int v = 8; };
 
+// Transform half-lengths: powers of two, and H = 3 * 2^j (j >= 2, "tri": the R / R^T lengths
+// L_R = 3 * 2^k that replace the next power of two where they are shorter, hgp_plan_create).
+constexpr bool is_pow2(int h) { return h > 0 && (h & (h - 1)) == 0; }
+constexpr bool is_tri(int h) { return h >= 12 && h % 3 == 0 && is_pow2(h / 3); }
+// points per thread: P = min(H, PMax) for powers of two, 12 for tri lengths (TT = H / 12 then
+// stays a power of two, and 12 holds the radix-3 stage)
+template <typename T, int H> struct PFor {
+  static_assert(is_pow2(H) || is_tri(H), "transform half-length: 2^k or 3 * 2^k (k >= 2)");
+  static constexpr int v = is_pow2(H) ? (H < PMax<T>::v ? H : PMax<T>::v) : 12;
+};
+
+// Stockham stage radices.  Powers of two: radix P stages (the last one smaller).  Tri lengths:
+// radix-4 / -2 stages first and the factor 3 in the LAST stage (radix 3 * min(4, H / 3), which
+// divides P = 12): every non-last stage's span NS is then a power of two dividing TT, as the
+// exchange index math of fft_xchg needs.
 template <int H, int P> struct Stages {
-  static constexpr int count() { int n = 0, rem = H; while (rem > 1) { int r = rem >= P ? P : rem; rem /= r; ++n; } return n; }
-  static constexpr int radix(int s) { int rem = H; for (int i = 0; i < s; ++i) rem /= (rem >= P ? P : rem); return rem >= P ? P : rem; }
-  static constexpr int ns(int s) { int ns = 1, rem = H; for (int i = 0; i < s; ++i) { int r = rem >= P ? P : rem; ns *= r; rem /= r; } return ns; }
+  static constexpr bool TRI = !is_pow2(H);
+  static constexpr int last_tri() { return 3 * (H / 3 >= 4 ? 4 : H / 3); }
+  static constexpr int count() {
+    if (!TRI) { int n = 0, rem = H; while (rem > 1) { int r = rem >= P ? P : rem; rem /= r; ++n; } return n; }
+    int n = 1, rem = H / last_tri();
+    while (rem > 1) { rem /= (rem >= 4 ? 4 : rem); ++n; }
+    return n;
+  }
+  static constexpr int radix(int s) {
+    if (!TRI) { int rem = H; for (int i = 0; i < s; ++i) rem /= (rem >= P ? P : rem); return rem >= P ? P : rem; }
+    int rem = H / last_tri(), i = 0;
+    while (rem > 1) { const int r = rem >= 4 ? 4 : rem; if (i == s) return r; rem /= r; ++i; }
+    return last_tri();
+  }
+  static constexpr int ns(int s) { int v = 1; for (int i = 0; i < s; ++i) v *= radix(i); return v; }
 };
 
 // multiply by exp(DIR * 2*pi*i*Q/16), DIR = -1 forward / +1 inverse; Q a compile-time
@@ -142,11 +169,65 @@ __device__ __forceinline__ C2<T> rot16(C2<T> v, int Q) {
   }
 }
 
-// In-register DFT of size R (natural order in and out), R in {1,2,4,8,16}.
+// multiply by exp(DIR * 2*pi*i*Q/12) (the radix-12 / -6 / -3 stages); Q a compile-time constant.
+template <typename T, int DIR>
+__device__ __forceinline__ C2<T> rot12(C2<T> v, int Q) {
+  const T c = (T)0.86602540378443864676, h = (T)0.5;
+  Q %= 12;
+  if (DIR > 0) Q = (12 - Q) % 12;           // inverse: exp(+i th) = forward rotation by -Q
+  switch (Q) {                              // forward: multiply by (cos th, -sin th), th = 2pi Q/12
+    case 0: return v;
+    case 3: return mk<T>(v.y, -v.x);
+    case 6: return mk<T>(-v.x, -v.y);
+    case 9: return mk<T>(-v.y, v.x);
+    case 1: return cmul<T>(v, mk<T>(c, -h));
+    case 2: return cmul<T>(v, mk<T>(h, -c));
+    case 4: return cmul<T>(v, mk<T>(-h, -c));
+    case 5: return cmul<T>(v, mk<T>(-c, -h));
+    case 7: return cmul<T>(v, mk<T>(-c, h));
+    case 8: return cmul<T>(v, mk<T>(-h, c));
+    case 10: return cmul<T>(v, mk<T>(h, c));
+    default: return cmul<T>(v, mk<T>(c, h));    // 11
+  }
+}
+
+// In-register DFT of size R (natural order in and out), R in {1,2,3,4,6,8,12,16}.
 template <typename T, int R, int DIR>
 __device__ __forceinline__ void dft(C2<T>* v) {
   if constexpr (R == 1) {
     return;
+  } else if constexpr (R == 3) {
+    // y0 = a + s, y1,2 = a - s/2 -+ i DIR' (sqrt(3)/2) d with s = b + c, d = b - c
+    const T c = (T)0.86602540378443864676;
+    const C2<T> a = v[0], s = cadd<T>(v[1], v[2]), d = csub<T>(v[1], v[2]);
+    const C2<T> m = mk<T>(a.x - (T)0.5 * s.x, a.y - (T)0.5 * s.y);
+    // forward: -i c d = (c d.y, -c d.x); inverse: +i c d
+    const C2<T> rd = (DIR < 0) ? mk<T>(c * d.y, -c * d.x) : mk<T>(-c * d.y, c * d.x);
+    v[0] = cadd<T>(a, s);
+    v[1] = cadd<T>(m, rd);
+    v[2] = csub<T>(m, rd);
+  } else if constexpr (R % 3 == 0) {
+    // R = R1 x 3 (R1 = 4 or 2): R1-point DFTs of stride 3, twiddles exp(-+2 pi i n2 k1 / R), 3-point DFTs
+    constexpr int R1 = R / 3, R2 = 3;
+    C2<T> y[R];
+#pragma unroll
+    for (int n2 = 0; n2 < R2; ++n2) {
+      C2<T> a[R1];
+#pragma unroll
+      for (int n1 = 0; n1 < R1; ++n1) a[n1] = v[R2 * n1 + n2];
+      dft<T, R1, DIR>(a);
+#pragma unroll
+      for (int k1 = 0; k1 < R1; ++k1) y[n2 * R1 + k1] = rot12<T, DIR>(a[k1], (n2 * k1 * (12 / R)) % 12);
+    }
+#pragma unroll
+    for (int k1 = 0; k1 < R1; ++k1) {
+      C2<T> b[R2];
+#pragma unroll
+      for (int n2 = 0; n2 < R2; ++n2) b[n2] = y[n2 * R1 + k1];
+      dft<T, R2, DIR>(b);
+#pragma unroll
+      for (int k2 = 0; k2 < R2; ++k2) v[k1 + R1 * k2] = b[k2];
+    }
   } else if constexpr (R == 2) {
     C2<T> a = v[0], b = v[1];
     v[0] = cadd<T>(a, b);
@@ -205,10 +286,12 @@ __device__ __forceinline__ void xsync() {
 //    halves the blocks a CU holds; 4096^2 K matvec 10.3 -> 6.2 ms): tab = [A | B], A[j] = W_L^j (j < S),
 //    B[i] = W_L^{iS} (i < H/S), W_L^q = A[q mod S] B[q div S] (one extra product, ~1 ulp).
 #ifndef HGP_TW_FULL_MAX
-#define HGP_TW_FULL_MAX (16 * 1024)   // largest half table (bytes) kept whole in LDS
+#define HGP_TW_FULL_MAX (8 * 1024)    // largest half table (bytes) kept whole in LDS (8 KB: the
+                                      // grouped 2048-point row blocks then fit two per CU)
 #endif
 template <typename T, int H> struct TwTab {
   static constexpr bool TWO = H * (int)sizeof(C2<T>) > HGP_TW_FULL_MAX;
+  // ceil(log2 H); S = 2^ceil(LG / 2) divides H for every supported H (2^k, 3 * 2^k, k >= 2)
   static constexpr int LG = [] { int l = 0; while ((1 << l) < H) ++l; return l; }();
   static constexpr int S = TWO ? (1 << ((LG + 1) / 2)) : H;
   static constexpr int ENTRIES = TWO ? S + H / S : H;
@@ -225,15 +308,26 @@ __device__ __forceinline__ void stage_tw(C2<T>* tab, const C2<T>* __restrict__ t
   }
 }
 
+// W_L^q for q in [0, 2H) (L = 2H), W_L^{q+H} = -W_L^q
 template <typename T, int H>
 __device__ __forceinline__ C2<T> tw_at(const C2<T>* __restrict__ tab, int q) {
   using TW = TwTab<T, H>;
   C2<T> w;
-  const int qq = q & (H - 1);
+  int qq;
+  bool neg;
+  if constexpr (is_pow2(H)) { qq = q & (H - 1); neg = (q & H) != 0; }
+  else { neg = q >= H; qq = neg ? q - H : q; }
   if constexpr (TW::TWO) w = cmul<T>(tab[qq & (TW::S - 1)], tab[TW::S + (qq >> (TW::LG + 1) / 2)]);
   else w = tab[qq];
-  if (q & H) { w.x = -w.x; w.y = -w.y; }
+  if (neg) { w.x = -w.x; w.y = -w.y; }
   return w;
+}
+
+// Hermitian partner of position p in the even frequency half: (H - p) mod H
+template <int H>
+__device__ __forceinline__ int herm_partner0(int p) {
+  if constexpr (is_pow2(H)) return (H - p) & (H - 1);
+  return p == 0 ? 0 : H - p;
 }
 
 // LDS address of logical element e (padding breaks the power-of-two strides of the

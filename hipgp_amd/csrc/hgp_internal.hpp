@@ -13,15 +13,19 @@ struct PassGeom { int C; int threads; int lds; };
 template <typename T>
 hipError_t launch_pass(int H, int mode, int lay, const PassDesc& d, int64_t nblocks, hipStream_t s);
 template <typename T> PassGeom pass_geom(int H, int lay);
-// 2-D row-pair passes with the column-major intermediate (hgp_rows.hpp); inv = 0 FWD, 1 INV
+// 2-D row-pair passes with the column-major intermediate (hgp_rows.hpp); inv = 0 FWD, 1 INV;
+// grouped = 1: the grouped-column layout of the 2-D operators (G = rowt_group(H) columns
+// interleaved; the axis-0 pass then reads it as LAY_CONTIG_G), 0: plain (3-D planes, slabs)
 template <typename T>
-hipError_t launch_rowt(int H, int inv, int epi, const PassDesc& d, hipStream_t s);
-// row pairs per block of the 2-D row passes (partials of the fused PCG epilogue are per block)
-template <typename T> int rowt_pairs(int H);
+hipError_t launch_rowt(int H, int inv, int epi, const PassDesc& d, hipStream_t s, int grouped);
+// row pairs per block of the row passes (partials of the fused PCG epilogue are per block)
+template <typename T> int rowt_pairs(int H, int grouped);
 // threads per block of the row-pair kernels
-template <typename T> int rowt_threads(int H);
+template <typename T> int rowt_threads(int H, int grouped);
 // whether the row-pair kernels of H points fit one CU's LDS (else run_op takes the generic path)
-template <typename T> int rowt_fits(int H);
+template <typename T> int rowt_fits(int H, int grouped);
+// columns per group of the 2-D operators' intermediate at row half-length H (1: plain layout)
+template <typename T> int rowt_group(int H);
 // 3-D middle-axis transposing line passes (hgp_lines.hpp): inv = 0 k_line_fwd_t, 1 k_line_inv_t
 template <typename T>
 hipError_t launch_linet(int H, int inv, const PassDesc& d, hipStream_t s);

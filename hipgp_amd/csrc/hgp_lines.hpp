@@ -28,7 +28,7 @@
 namespace hgp {
 
 template <typename T, int H> struct LineTCfg {
-  static constexpr int P = (H < PMax<T>::v) ? H : PMax<T>::v;
+  static constexpr int P = PFor<T, H>::v;
   static constexpr int TT = H / P;
   static constexpr int ex_elems(int c) { return c * H + (c * H) / 16; }
   static constexpr int tile_elems(int c) { return H * (c + 1); }   // one frequency half, pitch c+1

@@ -28,6 +28,11 @@
 //   LAY_RP      : last axis of (nrhs, M) real vectors, row pair (2j, 2j+1) of RHS q
 //                 <-> two compact half-spectrum rows (FWD input / INV output).
 //   LAY_R1      : 1-D: one real line per RHS (z = x + 0i), CONV only.
+//   LAY_CONTIG_G: LAY_CONTIG over the grouped-column intermediate of the long-row 2-D operators
+//                 (hgp_rows.hpp): G = d.grp columns interleaved, element (c, p) of one RHS at
+//                 ((c / G) * S0 + p) * G + c % G; a block's C lines are the G columns of one group
+//                 (x C / G right-hand sides), so the 128-B segments a line touches are used whole
+//                 by the block.
 #pragma once
 #include <type_traits>
 
@@ -59,7 +64,7 @@
 namespace hgp {
 
 enum { PASS_FWD = 0, PASS_INV = 1, PASS_CONV = 2, PASS_CONVC = 3 };   // CONV: real spectrum, CONVC: complex
-enum { LAY_STRIDED = 0, LAY_CONTIG = 1, LAY_RP = 2, LAY_R1 = 3 };
+enum { LAY_STRIDED = 0, LAY_CONTIG = 1, LAY_RP = 2, LAY_R1 = 3, LAY_CONTIG_G = 4 };
 enum { SPEC_REAL = 0, SPEC_CPLX = 1, SPEC_CPLX_CONJ = 2 };
 // row-inverse epilogue (hgp_rows.hpp): EPI_XR x/r update (unpreconditioned PCG); with the
 // preconditioner the x update is deferred to the C^-1 pass: EPI_R r update, EPI_XP x and p
@@ -84,6 +89,7 @@ struct PassDesc {
   int Q;                      // right-hand sides (setup grids: 1)
   int Rn, In;                 // lines per RHS: r in [0,Rn) (outer), i in [0,In) (inner, strided)
   int nrows;                  // LAY_RP: real rows per RHS (the pair (2r, 2r+1) needs 2r+1 < nrows)
+  int grp;                    // LAY_CONTIG_G: columns per group G (r_stride = S0, the group's pitch / G)
   const int* done;            // optional device flag: skip the pass when *done != 0
   // CONV passes: spectral dot of the transformed line with itself weighted by the real
   // spectrum, sum_k S_k |X_k|^2 = <x, op x> by Parseval (the crop is exact: x is zero outside
@@ -120,7 +126,7 @@ constexpr int LDS_CAP = 160 * 1024;
 constexpr int CG_LOADS = 8;
 
 template <typename T, int H, int LAY> struct PassCfg {
-  static constexpr int P = (H < PMax<T>::v) ? H : PMax<T>::v;
+  static constexpr int P = PFor<T, H>::v;
   static constexpr int TT = H / P;
   // LDS: exchange image of C lines (H complex each, 1 pad slot per 16) + twiddle half table
   static constexpr int ex_elems(int c) { return c * H + ((c * H) >> 4); }
@@ -131,7 +137,7 @@ template <typename T, int H, int LAY> struct PassCfg {
     while (c > 1 && (c * TT > 1024 || lds_bytes_for(c) > LDS_CAP)) c >>= 1;
     return c;
   }
-  static constexpr int ROWT = (LAY == LAY_CONTIG) ? HGP_CONTIG_THREADS : HGP_ROW_THREADS;
+  static constexpr int ROWT = (LAY == LAY_CONTIG || LAY == LAY_CONTIG_G) ? HGP_CONTIG_THREADS : HGP_ROW_THREADS;
   static constexpr int c_contig() {
     int c = (TT >= ROWT) ? 1 : ROWT / TT;
     while (c > 1 && (c * TT > 1024 || lds_bytes_for(c) > LDS_CAP / 2)) c >>= 1;
@@ -150,7 +156,7 @@ template <typename T, int H, int LAY> struct PassCfg {
   static constexpr int MINW_LDS = (BLOCKS_BY_LDS * WAVES_PER_BLOCK) / 4;
   static constexpr int MINW_AUTO = MINW_LDS < 1 ? 1 : (MINW_LDS > 4 ? 4 : MINW_LDS);
   static constexpr int MINW_SET = (LAY == LAY_STRIDED) ? (TT >= 16 ? HGP_MINW_STRIDED : HGP_MINW_STRIDED_SMALL)
-                                 : (LAY == LAY_CONTIG) ? HGP_MINW_CONTIG : HGP_MINW_ROW;
+                                 : (LAY == LAY_CONTIG || LAY == LAY_CONTIG_G) ? HGP_MINW_CONTIG : HGP_MINW_ROW;
   static constexpr int MINW = MINW_SET > 0 ? MINW_SET : MINW_AUTO;
 };
 
@@ -237,6 +243,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
   // adds a 32-bit element offset lc + p*stride to uniform base pointers, so no 64-bit address
   // is held per position across the FFT.
   int q, r, i, i0 = 0, lc = 0;
+  int64_t gbase = 0;          // LAY_CONTIG_G: element offset of the line in its RHS's slab
   bool valid;
   if constexpr (LAY == LAY_STRIDED) {
     // logical block = (q, g) with g fastest; the XCD remap keeps consecutive g (adjacent
@@ -251,6 +258,20 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
     i = i0 + l;
     valid = i < d.In;               // (q, r, i0) of a launched block are always in range
     lc = valid ? l : 0;             // keep every (unconditional) load in bounds
+  } else if constexpr (LAY == LAY_CONTIG_G) {
+    // lines (cg, q, cl), cl fastest: a block's C lines are the G columns of one group (x C / G
+    // RHS); the XCD remap keeps consecutive groups on one XCD
+    const int G = d.grp;
+    const int64_t line = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * C + l;
+    const int64_t rest = line / G;
+    const int cl = (int)(line - rest * G);
+    const int cg = (int)(rest / d.Q);
+    q = (int)(rest - (int64_t)cg * d.Q);
+    r = cg * G + cl;
+    i = 0;
+    valid = r < d.Rn;
+    if (!valid) { q = 0; r = 0; }
+    gbase = (int64_t)(r / G) * d.in.r_stride * G + (r % G);
   } else if constexpr (LAY == LAY_CONTIG) {
     // RHS-fastest: the C lines of a block are the same column r of C right-hand sides, so
     // they share one spectrum line; the XCD remap keeps the blocks of one column (all its
@@ -284,6 +305,8 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
     in_c2 = has2 ? in_c + d.in.r_stride : in_c;
   } else if constexpr (LAY == LAY_STRIDED) {
     in_c = reinterpret_cast<const C2<T>*>(d.in.ptr) + (int64_t)q * d.in.q_stride + (int64_t)r * d.in.r_stride + i0;
+  } else if constexpr (LAY == LAY_CONTIG_G) {
+    in_c = reinterpret_cast<const C2<T>*>(d.in.ptr) + (int64_t)q * d.in.q_stride + gbase;
   } else {
     in_c = reinterpret_cast<const C2<T>*>(d.in.ptr) + (int64_t)q * d.in.q_stride + (int64_t)r * d.in.r_stride;
   }
@@ -299,14 +322,16 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
     out_c2 = out_c + d.out.r_stride;
   } else if constexpr (LAY == LAY_STRIDED) {
     out_c = reinterpret_cast<C2<T>*>(d.out.ptr) + (int64_t)q * d.out.q_stride + (int64_t)r * d.out.r_stride + i0;
+  } else if constexpr (LAY == LAY_CONTIG_G) {
+    out_c = reinterpret_cast<C2<T>*>(d.out.ptr) + (int64_t)q * d.out.q_stride + gbase;
   } else {
     out_c = reinterpret_cast<C2<T>*>(d.out.ptr) + (int64_t)q * d.out.q_stride + (int64_t)r * d.out.r_stride;
   }
   // element offset of position p in this lane's line (32-bit: one RHS slab < 2^31 elements)
-  const int ips = (LAY == LAY_STRIDED) ? (int)d.in.p_stride : 1;
-  const int ops = (LAY == LAY_STRIDED) ? (int)d.out.p_stride : 1;
-  auto in_at = [&](int p) -> int { return (LAY == LAY_STRIDED) ? lc + p * ips : p; };
-  auto out_at = [&](int p) -> int { return (LAY == LAY_STRIDED) ? lc + p * ops : p; };
+  const int ips = (LAY == LAY_STRIDED) ? (int)d.in.p_stride : (LAY == LAY_CONTIG_G) ? d.grp : 1;
+  const int ops = (LAY == LAY_STRIDED) ? (int)d.out.p_stride : (LAY == LAY_CONTIG_G) ? d.grp : 1;
+  auto in_at = [&](int p) -> int { return (LAY == LAY_STRIDED) ? lc + p * ips : (LAY == LAY_CONTIG_G) ? p * ips : p; };
+  auto out_at = [&](int p) -> int { return (LAY == LAY_STRIDED) ? lc + p * ops : (LAY == LAY_CONTIG_G) ? p * ops : p; };
 
   // Loads are unconditional on clamped (always in-bounds) addresses and zeroed afterwards:
   // a per-element branch around a load makes hipcc wait vmcnt(0) per element.
@@ -362,18 +387,21 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
   }
   // contiguous lines of whole waves: wave-uniform line bases -> raw buffer accesses (32-bit
   // lane offsets; the zero padding beyond in_len and the crop beyond out_len come from the
-  // resource's range, invalid lines get an empty range)
-  // fp32 only: the fp64 form (128-bit raw buffer loads / stores) gave run-to-run different
-  // results at the 1e-8 level on lines of >= 4 waves (tools/diag_contig.py REPEAT=1,
-  // profiles/r2_fp64_contig_race.txt); the plain-pointer form is bitwise reproducible
+  // resource's range, invalid lines get an empty range).  fp64 too: its 128-bit stores once
+  // raced (round 2, run-to-run different results on lines of >= 4 waves) through the store-data
+  // hazard of an SGPR soffset; buf_st_c2<double> no longer uses one (profiles/r3_buf64_race.txt)
 #ifndef HGP_BUF_F64
-#define HGP_BUF_F64 0
+#define HGP_BUF_F64 1
 #endif
-  constexpr bool BUF = (std::is_same<T, float>::value || HGP_BUF_F64) && (LAY == LAY_CONTIG) && (TT % 64 == 0) && !CAN_FOLD;
+  constexpr bool CONTIG = (LAY == LAY_CONTIG || LAY == LAY_CONTIG_G);
+  constexpr bool BUF = (std::is_same<T, float>::value || HGP_BUF_F64) && CONTIG && (TT % 64 == 0) && !CAN_FOLD;
+  // element stride of a line's positions: 1, or G in the grouped layout; the range then ends
+  // one element past the line's last valid position ((len - 1) G + 1 elements)
+  const uint32_t es = (uint32_t)ips * (uint32_t)sizeof(C2<T>);
   const BufRsrc rin = buf_rsrc(BUF ? (const void*)in_c : nullptr,
-                               (BUF && valid) ? (uint32_t)d.in.len * (uint32_t)sizeof(C2<T>) : 0u);
+                               (BUF && valid && d.in.len > 0) ? ((uint32_t)(d.in.len - 1) * (uint32_t)ips + 1u) * (uint32_t)sizeof(C2<T>) : 0u);
   const BufRsrc rout = buf_rsrc(BUF ? (const void*)out_c : nullptr,
-                                (BUF && valid) ? (uint32_t)d.out.len * (uint32_t)sizeof(C2<T>) : 0u);
+                                (BUF && valid && d.out.len > 0) ? ((uint32_t)(d.out.len - 1) * (uint32_t)ops + 1u) * (uint32_t)sizeof(C2<T>) : 0u);
   if constexpr (MODE == PASS_FWD || CONV) {
     const int in_len = d.in.len;
     const int lim = in_len - 1;
@@ -383,7 +411,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
       const int p = t + TT * k;
       C2<T> a;
       if constexpr (BUF) {
-        a = buf_ld_c2<T>(rin, (uint32_t)t * (uint32_t)sizeof(C2<T>), (uint32_t)(TT * k * (int)sizeof(C2<T>)));
+        a = buf_ld_c2<T>(rin, (uint32_t)t * es, (uint32_t)(TT * k) * es);
       } else {
         a = load_in(p < in_len ? p : lim);
         if (p >= in_len) a = mk<T>(0, 0);
@@ -412,7 +440,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
 #pragma unroll
         for (int k = 0; k < P; ++k) {
           const int p = t + TT * k;
-          const int pp = (half == 0) ? ((H - p) & (H - 1)) : (H - 1 - p);
+          const int pp = (half == 0) ? herm_partner0<H>(p) : (H - 1 - p);
           const C2<T> zp = lds[lds_phys(lbase + pp)];
           const bool store = (half == 0) ? (p <= H / 2) : (p < H / 2);
           if (valid && store) {
@@ -525,7 +553,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
               }
             }
           } else if constexpr (BUF) {
-            buf_st_c2<T>(y, rout, (uint32_t)t * (uint32_t)sizeof(C2<T>), (uint32_t)((pp - t) * (int)sizeof(C2<T>)));
+            buf_st_c2<T>(y, rout, (uint32_t)t * es, (uint32_t)(pp - t) * es);
           } else {
             out_c[out_at(pp)] = y;
           }
@@ -538,7 +566,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
         if (t == 0 && valid) reinterpret_cast<T*>(d.partial)[(int64_t)q * d.Rn + r] = s;
       }
     }
-    if constexpr (MODE == PASS_CONV && LAY != LAY_STRIDED) {
+    if constexpr (MODE == PASS_CONV && LAY != LAY_STRIDED) {   // CONTIG / CONTIG_G / R1
       if (d.spart != nullptr) {     // uniform over the block
         const T s = line_sum<T, TT>(sdot, reinterpret_cast<T*>(smem_raw));
         if (t == 0 && valid) {

@@ -36,10 +36,15 @@ static hipError_t launch_h(int mode, int lay, const PassDesc& d, int64_t nblocks
     if (lay == LAY_STRIDED) return launch_one<T, H, PASS_CONV, LAY_STRIDED>(d, nblocks, s);
     if (lay == LAY_CONTIG) return launch_one<T, H, PASS_CONV, LAY_CONTIG>(d, nblocks, s);
     if (lay == LAY_R1) return launch_one<T, H, PASS_CONV, LAY_R1>(d, nblocks, s);
+    // the grouped-column intermediate of long fp32 rows (hgp_rows.hpp RowTCfg::G); any axis-0 H
+    if constexpr (std::is_same<T, float>::value)
+      if (lay == LAY_CONTIG_G) return launch_one<T, H, PASS_CONV, LAY_CONTIG_G>(d, nblocks, s);
   } else if (mode == PASS_CONVC) {
     if (lay == LAY_STRIDED) return launch_one<T, H, PASS_CONVC, LAY_STRIDED>(d, nblocks, s);
     if (lay == LAY_CONTIG) return launch_one<T, H, PASS_CONVC, LAY_CONTIG>(d, nblocks, s);
     if (lay == LAY_R1) return launch_one<T, H, PASS_CONVC, LAY_R1>(d, nblocks, s);
+    if constexpr (std::is_same<T, float>::value)
+      if (lay == LAY_CONTIG_G) return launch_one<T, H, PASS_CONVC, LAY_CONTIG_G>(d, nblocks, s);
   }
   return hipErrorInvalidValue;
 }
@@ -52,7 +57,7 @@ static PassGeom geom_one() {
 template <typename T, int H>
 static PassGeom geom_h(int lay) {
   if (lay == LAY_STRIDED) return geom_one<T, H, LAY_STRIDED>();
-  if (lay == LAY_CONTIG) return geom_one<T, H, LAY_CONTIG>();
+  if (lay == LAY_CONTIG || lay == LAY_CONTIG_G) return geom_one<T, H, LAY_CONTIG>();
   if (lay == LAY_RP) return geom_one<T, H, LAY_RP>();
   return geom_one<T, H, LAY_R1>();
 }
@@ -69,43 +74,61 @@ static PassGeom geom_h(int lay) {
     case 16384:   /* fp32 only: one 16384-point fp64 line exceeds one CU's LDS */                     \
       if constexpr (std::is_same<T, float>::value) return FN<T, 16384>(__VA_ARGS__);                 \
       break;                                                                                         \
+    /* 3 * 2^k (hgp_fft.hpp is_tri): the mixed-radix R / R^T lengths */                              \
+    case 12: return FN<T, 12>(__VA_ARGS__);     case 24: return FN<T, 24>(__VA_ARGS__);             \
+    case 48: return FN<T, 48>(__VA_ARGS__);     case 96: return FN<T, 96>(__VA_ARGS__);             \
+    case 192: return FN<T, 192>(__VA_ARGS__);   case 384: return FN<T, 384>(__VA_ARGS__);           \
+    case 768: return FN<T, 768>(__VA_ARGS__);   case 1536: return FN<T, 1536>(__VA_ARGS__);         \
+    case 3072: return FN<T, 3072>(__VA_ARGS__); case 6144: return FN<T, 6144>(__VA_ARGS__);         \
+    case 12288:   /* fp32 only, as 16384 */                                                          \
+      if constexpr (std::is_same<T, float>::value) return FN<T, 12288>(__VA_ARGS__);                 \
+      break;                                                                                         \
     default: break;                                                                                  \
   }
 
-template <typename T, int H, int EPI>
+template <typename T, int H, int EPI, int G>
 static hipError_t launch_rowt_inv(const PassDesc& d, int64_t nb, hipStream_t s) {
-  using Cfg = RowTCfg<T, H>;
+  using Cfg = RowTCfg<T, H, G>;
   static bool attr_set = false;   // opt in to > 64 KB dynamic LDS once per instance
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_row_inv_t<T, H, EPI>,
+    hipError_t e = hipFuncSetAttribute((const void*)k_row_inv_t<T, H, EPI, G>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  hipLaunchKernelGGL((k_row_inv_t<T, H, EPI>), dim3((unsigned)nb), dim3(Cfg::THREADS), Cfg::LDS, s, d);
+  hipLaunchKernelGGL((k_row_inv_t<T, H, EPI, G>), dim3((unsigned)nb), dim3(Cfg::THREADS), Cfg::LDS, s, d);
   return hipGetLastError();
 }
 
-template <typename T, int H>
-static hipError_t launch_rowt_h(int inv, int epi, const PassDesc& d, hipStream_t s) {
-  using Cfg = RowTCfg<T, H>;
+template <typename T, int H, int G>
+static hipError_t launch_rowt_g(int inv, int epi, const PassDesc& d, hipStream_t s) {
+  using Cfg = RowTCfg<T, H, G>;
   if constexpr (Cfg::LDS > LDS_CAP) return hipErrorNotSupported;   // e.g. fp64 rows of H = 8192
   const int64_t nb = (int64_t)d.Q * ((d.Rn + Cfg::C - 1) / Cfg::C);
   if (nb <= 0) return hipSuccess;
   if (inv) {
-    if (epi == EPI_XR) return launch_rowt_inv<T, H, EPI_XR>(d, nb, s);
-    if (epi == EPI_R) return launch_rowt_inv<T, H, EPI_R>(d, nb, s);
-    if (epi == EPI_XP) return launch_rowt_inv<T, H, EPI_XP>(d, nb, s);
-    return launch_rowt_inv<T, H, EPI_OUT>(d, nb, s);
+    if (epi == EPI_XR) return launch_rowt_inv<T, H, EPI_XR, G>(d, nb, s);
+    if (epi == EPI_R) return launch_rowt_inv<T, H, EPI_R, G>(d, nb, s);
+    if (epi == EPI_XP) return launch_rowt_inv<T, H, EPI_XP, G>(d, nb, s);
+    return launch_rowt_inv<T, H, EPI_OUT, G>(d, nb, s);
   }
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_row_fwd_t<T, H>, hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS);
+    hipError_t e = hipFuncSetAttribute((const void*)k_row_fwd_t<T, H, G>, hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  hipLaunchKernelGGL((k_row_fwd_t<T, H>), dim3((unsigned)nb), dim3(Cfg::THREADS), Cfg::LDS, s, d);
+  hipLaunchKernelGGL((k_row_fwd_t<T, H, G>), dim3((unsigned)nb), dim3(Cfg::THREADS), Cfg::LDS, s, d);
   return hipGetLastError();
+}
+
+// grouped: the 2-D operators' intermediate in the grouped-column layout (RowGroup<T, H>::G)
+template <typename T, int H>
+static hipError_t launch_rowt_h(int inv, int epi, const PassDesc& d, hipStream_t s, int grouped) {
+  constexpr int G = RowGroup<T, H>::G;
+  if constexpr (G > 1)
+    if (grouped) return launch_rowt_g<T, H, G>(inv, epi, d, s);
+  return launch_rowt_g<T, H, 1>(inv, epi, d, s);
 }
 
 template <typename T, int H>
@@ -144,36 +167,49 @@ hipError_t launch_linet(int H, int inv, const PassDesc& d, hipStream_t s) {
 }
 
 template <typename T, int H>
-static int rowt_pairs_h() { return RowTCfg<T, H>::C; }
+static int rowt_pairs_h(int grouped) { return grouped ? RowTCfg<T, H, RowGroup<T, H>::G>::C : RowTCfg<T, H>::C; }
 
 template <typename T, int H>
-static int rowt_threads_h() { return RowTCfg<T, H>::THREADS; }
+static int rowt_threads_h(int grouped) {
+  return grouped ? RowTCfg<T, H, RowGroup<T, H>::G>::THREADS : RowTCfg<T, H>::THREADS;
+}
 
 template <typename T, int H>
-static int rowt_fits_h() { return RowTCfg<T, H>::LDS <= LDS_CAP ? 1 : 0; }
+static int rowt_fits_h(int grouped) {
+  return (grouped ? RowTCfg<T, H, RowGroup<T, H>::G>::LDS : RowTCfg<T, H>::LDS) <= LDS_CAP ? 1 : 0;
+}
+
+template <typename T, int H>
+static int rowt_group_h() { return RowGroup<T, H>::G; }
 
 template <typename T>
-int rowt_fits(int H) {
-  HGP_H_SWITCH(rowt_fits_h)
+int rowt_fits(int H, int grouped) {
+  HGP_H_SWITCH(rowt_fits_h, grouped)
   return 0;
 }
 
 template <typename T>
-hipError_t launch_rowt(int H, int inv, int epi, const PassDesc& d, hipStream_t s) {
-  HGP_H_SWITCH(launch_rowt_h, inv, epi, d, s)
+hipError_t launch_rowt(int H, int inv, int epi, const PassDesc& d, hipStream_t s, int grouped) {
+  HGP_H_SWITCH(launch_rowt_h, inv, epi, d, s, grouped)
   return hipErrorInvalidValue;
 }
 
 template <typename T>
-int rowt_pairs(int H) {
-  HGP_H_SWITCH(rowt_pairs_h)
+int rowt_pairs(int H, int grouped) {
+  HGP_H_SWITCH(rowt_pairs_h, grouped)
   return 0;
 }
 
 template <typename T>
-int rowt_threads(int H) {
-  HGP_H_SWITCH(rowt_threads_h)
+int rowt_threads(int H, int grouped) {
+  HGP_H_SWITCH(rowt_threads_h, grouped)
   return 0;
+}
+
+template <typename T>
+int rowt_group(int H) {
+  HGP_H_SWITCH(rowt_group_h)
+  return 1;
 }
 
 template <typename T>

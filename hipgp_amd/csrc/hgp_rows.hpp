@@ -34,16 +34,41 @@
 
 namespace hgp {
 
-template <typename T, int H> struct RowTCfg {
-  static constexpr int P = (H < PMax<T>::v) ? H : PMax<T>::v;
+// Grouped columns (long fp32 rows).  A block's tile is 2C rows of every compact column; with the
+// plain column-major intermediate W[c][i0] its stores / loads are 2C x sizeof(complex) segments,
+// and at H = 4096 the LDS (four 4096-point exchange images, 139 KB) holds one 4-pair block per
+// CU: 64-B segments, no second block to overlap load, transform and store with (row passes
+// 0.37 of HBM at C4, PMC traffic 1.64x).  The grouped layout interleaves G consecutive compact
+// columns, element (c, i0) at ((c / G) S0 + i0) G + c % G, so 2C rows x G columns are one
+// contiguous 128-B segment with C = 8 / G pairs per block; the tile of each frequency half is
+// moved in NCH column chunks, and two such blocks fit a CU.  The axis-0 pass reads the layout
+// as LAY_CONTIG_G (hgp_pass.hpp).  G = 1 is the plain layout (the 3-D planes, the slab passes,
+// fp64 and rows of one wave or less).
+#ifndef HGP_ROWG_2048
+#define HGP_ROWG_2048 2           // G at H = 2048 (fp32): 4 pairs x 2 columns = 128 B
+#endif
+#ifndef HGP_ROWG_4096
+#define HGP_ROWG_4096 4           // G at H >= 4096 (fp32): 2 pairs x 4 columns = 128 B
+#endif
+template <typename T, int H> struct RowGroup {
+  static constexpr int G = (!std::is_same<T, float>::value || !is_pow2(H)) ? 1
+                         : H == 2048 ? HGP_ROWG_2048 : H >= 4096 ? HGP_ROWG_4096 : 1;
+};
+
+template <typename T, int H, int G = 1> struct RowTCfg {
+  static constexpr int P = PFor<T, H>::v;
   static constexpr int TT = H / P;
+  // tile chunks per frequency half (the grouped blocks keep a chunk of columns in LDS at a time)
+  static constexpr int NCH = G > 1 ? 2 : 1;
+  static constexpr int CHC = H / 2 / NCH;                        // nominal columns per chunk
   // exchange images: pair l owns logical elements [l*H, (l+1)*H), padded by lds_phys
   static constexpr int ex_elems(int c) { return c * H + (c * H) / 16; }
   static constexpr int TS(int c) { return 2 * c + 1; }           // tile row pitch (pad: banks)
-  static constexpr int tile_elems(int c) { return (H / 2 + 1) * TS(c); }
+  static constexpr int tile_elems(int c) { return (CHC + 1) * TS(c); }
   static constexpr int area(int c) { return ex_elems(c) > tile_elems(c) ? ex_elems(c) : tile_elems(c); }
   static constexpr int lds_bytes_for(int c) { return area(c) * (int)sizeof(C2<T>) + TwTab<T, H>::BYTES; }
   static constexpr int c_pairs() {
+    if (G > 1) return 8 / G;                                     // 2C rows x G columns = 128 B (fp32)
     int c = (TT > 64 ? HGP_ROWT_PAIRS_BIG : HGP_ROWT_PAIRS) * 64 / TT;   // 512 threads at the default
     if (c < 1) c = 1;
     if (c > 64) c = 64;                            // tiny rows: cap the tile height
@@ -59,10 +84,29 @@ template <typename T, int H> struct RowTCfg {
   static constexpr int BLOCKS_BY_LDS = LDS_CAP / LDS;
   static constexpr int MINW_LDS = (BLOCKS_BY_LDS * ((THREADS + 63) / 64)) / 4;
   static constexpr int MINW = MINW_LDS < 1 ? 1 : (MINW_LDS > 4 ? 4 : MINW_LDS);
-  static constexpr bool SHORT_SEG = 2 * C * (int)sizeof(C2<T>) < 128;
+  static constexpr bool SHORT_SEG = 2 * C * G * (int)sizeof(C2<T>) < 128;
   static constexpr bool XCD_INV = HGP_ROW_XCD >= 2 || (HGP_ROW_XCD == 1 && SHORT_SEG);
   static constexpr bool XCD_FWD = HGP_ROW_XCD == 3;
+  // one tile chunk as 128-B units: (column group, row, column in group), column fastest
+  static constexpr int SEG = 2 * C * G;                           // elements per group segment
+  static constexpr int MAXGRP = (CHC + 1 + G - 1) / G + 1;        // groups a chunk can touch
+  static constexpr int ITER = (MAXGRP * SEG + THREADS - 1) / THREADS;
 };
+
+// element offset of compact column c, row i0 of one RHS's intermediate (column pitch S0)
+template <int G>
+__device__ __forceinline__ uint32_t wg_off(int c, int i0, int64_t S0) {
+  if constexpr (G == 1) return (uint32_t)c * (uint32_t)S0 + (uint32_t)i0;
+  return ((uint32_t)(c / G) * (uint32_t)S0 + (uint32_t)i0) * (uint32_t)G + (uint32_t)(c % G);
+}
+
+// columns [a, b) of tile chunk j of frequency half `half`, relative to the half's first column
+template <int H, int NCH, int CHC>
+__device__ __forceinline__ void chunk_cols(int half, int j, int& a, int& b) {
+  const int ncol = half == 0 ? H / 2 + 1 : H / 2;
+  a = j * CHC;
+  b = (j == NCH - 1) ? ncol : (j + 1) * CHC;
+}
 
 template <bool REMAP>
 __device__ __forceinline__ int row_block_id() {
@@ -71,14 +115,14 @@ __device__ __forceinline__ int row_block_id() {
 
 // The forward row transform of a block's row pairs after their real values are in va (Re = row
 // 2l, Im = row 2l+1, positions t + TT k < H, zero padded): twiddled odd half, both halves' FFTs,
-// Hermitian split, and the transposed half spectra out to W[c][row0 + row] (column pitch S0).
-// Needs the twiddle table staged in `tab`; uses the LDS area from `lds` (exchange images, tile).
-template <typename T, int H, int P>
+// Hermitian split, and the transposed half spectra out to the intermediate (column pitch S0,
+// grouped by G).  Needs the twiddle table staged in `tab`; uses the LDS area from `lds`.
+template <typename T, int H, int P, int G>
 __device__ __forceinline__ void row_fwd_tail(C2<T> (&va)[P], C2<T> (&vb)[P],
                                              C2<T>* lds, const C2<T>* tab, const C2<T>* __restrict__ twg, int t,
                                              int l, int lbase, C2<T>* W, int64_t S0, int row0, int nrow_blk) {
-  using Cfg = RowTCfg<T, H>;
-  constexpr int TT = Cfg::TT, C = Cfg::C, PITCH = Cfg::PITCH;
+  using Cfg = RowTCfg<T, H, G>;
+  constexpr int TT = Cfg::TT, C = Cfg::C, PITCH = Cfg::PITCH, NCH = Cfg::NCH, CHC = Cfg::CHC, SEG = Cfg::SEG;
   static_assert(P == Cfg::P, "row_fwd_tail: P");
 #pragma unroll
   for (int k = 0; k < P; ++k) vb[k] = cmul<T>(va[k], tw_at<T, H>(tab, t + TT * k));
@@ -87,6 +131,7 @@ __device__ __forceinline__ void row_fwd_tail(C2<T> (&va)[P], C2<T> (&vb)[P],
   fft_line2<T, H, P, -1, 1, Cfg::WAVE>(va, vb, lds, lbase, t, tab);
   auto do_half = [&](auto half_c, C2<T>(&v)[P]) {
     constexpr int half = decltype(half_c)::value;
+    constexpr int C0 = (half == 0) ? 0 : H / 2 + 1;
     // Hermitian split through this group's exchange image
     xsync<Cfg::WAVE>();
 #pragma unroll
@@ -96,36 +141,40 @@ __device__ __forceinline__ void row_fwd_tail(C2<T> (&va)[P], C2<T> (&vb)[P],
 #pragma unroll
     for (int k = 0; k < P; ++k) {
       const int p = t + TT * k;
-      const int pp = (half == 0) ? ((H - p) & (H - 1)) : (H - 1 - p);
+      const int pp = (half == 0) ? herm_partner0<H>(p) : (H - 1 - p);
       const C2<T> zp = lds[lds_phys(lbase + pp)];
       herm_split<T>(v[k], zp, A[k], B[k]);
     }
     __syncthreads();   // every group done with its exchange image: the tile overlays them
-    // tile[col][row]: col = compact column - first column of the half, row = 2l + {0,1}
 #pragma unroll
-    for (int k = 0; k < P; ++k) {
-      const int p = t + TT * k;
-      const bool store = (half == 0) ? (p <= H / 2) : (p < H / 2);
-      if (store && l < C) {
-        lds[p * PITCH + 2 * l] = A[k];
-        lds[p * PITCH + 2 * l + 1] = B[k];
+    for (int j = 0; j < NCH; ++j) {
+      int ca, cb;
+      chunk_cols<H, NCH, CHC>(half, j, ca, cb);
+      // tile[col - ca][row]: col = compact column relative to the half, row = 2l + {0,1}
+#pragma unroll
+      for (int k = 0; k < P; ++k) {
+        const int p = t + TT * k;
+        if (p >= ca && p < cb && l < C) {
+          lds[(p - ca) * PITCH + 2 * l] = A[k];
+          lds[(p - ca) * PITCH + 2 * l + 1] = B[k];
+        }
       }
-    }
-    __syncthreads();
-    // column segments: rows-fast, 2C rows x sizeof(complex) contiguous per column
-    constexpr int NCOL = (half == 0) ? H / 2 + 1 : H / 2;
-    constexpr int C0 = (half == 0) ? 0 : H / 2 + 1;
-    constexpr int NE = NCOL * 2 * C;
-    constexpr int ITER = (NE + Cfg::THREADS - 1) / Cfg::THREADS;
+      __syncthreads();
+      // 128-B units: column group, row, column in the group (columns of other chunks / halves
+      // in a straddled group are left to them)
+      const int g0 = (C0 + ca) / G;
 #pragma unroll
-    for (int j = 0; j < ITER; ++j) {
-      const int e = threadIdx.x + j * Cfg::THREADS;
-      const int col = e / (2 * C);
-      const int row = e - col * (2 * C);
-      if (e < NE && row < nrow_blk)
-        buf_st_c2<T>(lds[col * PITCH + row], rW, ((uint32_t)(C0 + col) * (uint32_t)S0 + (uint32_t)(row0 + row)) * (uint32_t)sizeof(C2<T>));
+      for (int it = 0; it < Cfg::ITER; ++it) {
+        const int e = threadIdx.x + it * Cfg::THREADS;
+        const int gr = e / SEG;
+        const int rem = e - gr * SEG;
+        const int row = rem / G;
+        const int c = (g0 + gr) * G + (rem - row * G);     // absolute compact column
+        if (c >= C0 + ca && c < C0 + cb && row < nrow_blk)
+          buf_st_c2<T>(lds[(c - C0 - ca) * PITCH + row], rW, wg_off<G>(c, row0 + row, S0) * (uint32_t)sizeof(C2<T>));
+      }
+      __syncthreads();   // tile read before the next chunk / half reuses the area
     }
-    __syncthreads();   // tile read before the next half's FFT reuses the area
   };
   do_half(std::integral_constant<int, 0>{}, va);
   do_half(std::integral_constant<int, 1>{}, vb);
@@ -133,11 +182,11 @@ __device__ __forceinline__ void row_fwd_tail(C2<T> (&va)[P], C2<T> (&vb)[P],
 
 // Real row pairs -> column-major compact half spectra.
 //   in : View{x, q_stride (elements per RHS), r_stride (row pitch), 1, len = row length}
-//   out: View{W, q_stride (complex per RHS), r_stride = column pitch S0, 1, 0}
+//   out: View{W, q_stride (complex per RHS), r_stride = column pitch S0, 1, 0}  (grouped by G)
 //   Q RHS, Rn pairs per RHS (= ceil(nrows / 2)), grid = Q * ceil(Rn / C).
-template <typename T, int H>
-__global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) void k_row_fwd_t(const PassDesc d) {
-  using Cfg = RowTCfg<T, H>;
+template <typename T, int H, int G>
+__global__ __launch_bounds__((RowTCfg<T, H, G>::THREADS), (RowTCfg<T, H, G>::MINW)) void k_row_fwd_t(const PassDesc d) {
+  using Cfg = RowTCfg<T, H, G>;
   constexpr int P = Cfg::P, TT = Cfg::TT, C = Cfg::C;
   if (d.done != nullptr && *d.done) return;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
@@ -190,7 +239,7 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
   C2<T>* W = reinterpret_cast<C2<T>*>(d.out.ptr) + (int64_t)q * d.out.q_stride;
   const int row0 = 2 * rb * C;                     // first row of this block's tile
   const int nrow_blk = d.nrows - row0 < 2 * C ? d.nrows - row0 : 2 * C;
-  row_fwd_tail<T, H>(va, vb, lds, tab, twg, t, l, lbase, W, d.out.r_stride, row0, nrow_blk);
+  row_fwd_tail<T, H, P, G>(va, vb, lds, tab, twg, t, l, lbase, W, d.out.r_stride, row0, nrow_blk);
 }
 
 // Column-major compact half spectra -> real row pairs (crop), optional fused dot.
@@ -260,10 +309,11 @@ __device__ __forceinline__ void cg_fix_x(int nrow, int out_len, T* __restrict__ 
   }
 }
 
-template <typename T, int H, int EPI = EPI_OUT>
-__global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) void k_row_inv_t(const PassDesc d) {
-  using Cfg = RowTCfg<T, H>;
-  constexpr int P = Cfg::P, TT = Cfg::TT, C = Cfg::C, PITCH = Cfg::PITCH;
+template <typename T, int H, int EPI = EPI_OUT, int G = 1>
+__global__ __launch_bounds__((RowTCfg<T, H, G>::THREADS), (RowTCfg<T, H, G>::MINW)) void k_row_inv_t(const PassDesc d) {
+  using Cfg = RowTCfg<T, H, G>;
+  constexpr int P = Cfg::P, TT = Cfg::TT, C = Cfg::C, PITCH = Cfg::PITCH, NCH = Cfg::NCH, CHC = Cfg::CHC;
+  constexpr int SEG = Cfg::SEG;
   // staged rows (2C x out_len <= 2C x H values) + two wave-sum areas fit the LDS area
   static_assert((2 * C * H + 2 * (Cfg::THREADS / 64)) * (int)sizeof(T) <= Cfg::AREA * (int)sizeof(C2<T>), "epilogue LDS");
   const int nrb = (d.Rn + C - 1) / C;
@@ -306,43 +356,54 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
   const int nrow_blk = d.nrows - row0 < 2 * C ? d.nrows - row0 : 2 * C;
 
   C2<T> va[P], vb[P];
-  // Tiles of the two frequency halves (compact columns [0, H/2] and [H/2+1, H]) go through the
-  // same LDS area one after the other; the odd half's global loads are issued before the even
-  // half is rebuilt from LDS, so its memory latency overlaps that work.
-  constexpr int ITER = ((H / 2 + 1) * 2 * C + Cfg::THREADS - 1) / Cfg::THREADS;
+  // The tile chunks (frequency half, column chunk) go through the same LDS area one after the
+  // other; each chunk's global loads are issued before the previous chunk is rebuilt from LDS,
+  // so their memory latency overlaps that work.  Chunk u = half * NCH + j.
+  constexpr int NU = 2 * NCH;
+  constexpr int ITER = Cfg::ITER;
   C2<T> buf[ITER];
-  auto load_tile = [&](auto half_c) {
-    constexpr int half = decltype(half_c)::value;
-    constexpr int NCOL = (half == 0) ? H / 2 + 1 : H / 2;
-    constexpr int C0 = (half == 0) ? 0 : H / 2 + 1;
-    constexpr int NE = NCOL * 2 * C;
+  auto load_tile = [&](int u) {
+    const int half = u / NCH;
+    int ca, cb;
+    chunk_cols<H, NCH, CHC>(half, u - half * NCH, ca, cb);
+    const int C0 = half == 0 ? 0 : H / 2 + 1;
+    const int g0 = (C0 + ca) / G;
 #pragma unroll
-    for (int j = 0; j < ITER; ++j) {         // all global loads in flight at once
-      const int e = threadIdx.x + j * Cfg::THREADS;
-      const int ee = e < NE ? e : NE - 1;
-      const int col = ee / (2 * C);
-      const int row = ee - col * (2 * C);
-      const int rr = row < nrow_blk ? row : 0;
-      C2<T> val = buf_ld_c2<T>(rW, ((uint32_t)(C0 + col) * (uint32_t)S0 + (uint32_t)(row0 + rr)) * (uint32_t)sizeof(C2<T>));
-      if (row >= nrow_blk) val = mk<T>(0, 0);
-      buf[j] = val;
+    for (int it = 0; it < ITER; ++it) {         // all global loads in flight at once
+      const int e = threadIdx.x + it * Cfg::THREADS;
+      const int gr = e / SEG;
+      const int rem = e - gr * SEG;
+      const int row = rem / G;
+      int c = (g0 + gr) * G + (rem - row * G);
+      const bool ok = c >= C0 + ca && c < C0 + cb && row < nrow_blk;
+      if (!ok) c = C0 + ca;                      // clamped in-bounds address, zeroed below
+      C2<T> val = buf_ld_c2<T>(rW, wg_off<G>(c, row0 + (ok ? row : 0), S0) * (uint32_t)sizeof(C2<T>));
+      if (!ok) val = mk<T>(0, 0);
+      buf[it] = val;
     }
   };
-  auto park_tile = [&](auto half_c) {
-    constexpr int half = decltype(half_c)::value;
-    constexpr int NCOL = (half == 0) ? H / 2 + 1 : H / 2;
-    constexpr int NE = NCOL * 2 * C;
+  auto park_tile = [&](int u) {
+    const int half = u / NCH;
+    int ca, cb;
+    chunk_cols<H, NCH, CHC>(half, u - half * NCH, ca, cb);
+    const int C0 = half == 0 ? 0 : H / 2 + 1;
+    const int g0 = (C0 + ca) / G;
 #pragma unroll
-    for (int j = 0; j < ITER; ++j) {
-      const int e = threadIdx.x + j * Cfg::THREADS;
-      const int col = e / (2 * C);
-      const int row = e - col * (2 * C);
-      if (e < NE) lds[col * PITCH + row] = buf[j];
+    for (int it = 0; it < ITER; ++it) {
+      const int e = threadIdx.x + it * Cfg::THREADS;
+      const int gr = e / SEG;
+      const int rem = e - gr * SEG;
+      const int row = rem / G;
+      const int c = (g0 + gr) * G + (rem - row * G);
+      if (c >= C0 + ca && c < C0 + cb && row < 2 * C) lds[(c - C0 - ca) * PITCH + row] = buf[it];
     }
   };
-  // Hermitian rebuild Z = A + iB of the pair at frequency half `half`, position p
-  auto rebuild = [&](auto half_c, C2<T>(&v)[P]) {
-    constexpr int half = decltype(half_c)::value;
+  // Hermitian rebuild Z = A + iB of the pair at frequency half `half`, position p, for the
+  // positions whose compact column lies in the chunk [ca, cb) (relative to the half)
+  auto rebuild = [&](int u, C2<T>(&v)[P]) {
+    const int half = u / NCH;
+    int ca, cb;
+    chunk_cols<H, NCH, CHC>(half, u - half * NCH, ca, cb);
 #pragma unroll
     for (int k = 0; k < P; ++k) {
       const int p = t + TT * k;
@@ -350,17 +411,17 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
       int c;
       if (half == 0) { cj = p > H / 2; c = cj ? H - p : p; }
       else { cj = p >= H / 2; c = cj ? H - 1 - p : p; }
-      const int li = l < C ? l : 0;
-      C2<T> A = lds[c * PITCH + 2 * li];
-      C2<T> B = lds[c * PITCH + 2 * li + 1];
-      if (!has2) B = mk<T>(0, 0);
-      if (cj) { A.y = -A.y; B.y = -B.y; }
-      v[k] = herm_join<T>(A, B);
+      if (NCH == 1 || (c >= ca && c < cb)) {
+        const int li = l < C ? l : 0;
+        C2<T> A = lds[(c - ca) * PITCH + 2 * li];
+        C2<T> B = lds[(c - ca) * PITCH + 2 * li + 1];
+        if (!has2) B = mk<T>(0, 0);
+        if (cj) { A.y = -A.y; B.y = -B.y; }
+        v[k] = herm_join<T>(A, B);
+      }
     }
   };
-  using H0 = std::integral_constant<int, 0>;
-  using H1 = std::integral_constant<int, 1>;
-  load_tile(H0{});
+  load_tile(0);
   // in-kernel CG scalar: the RHS's spectral partials are loaded behind the first tile (their
   // latency hides under the tile's) and summed per thread and per wave right after it lands;
   // the wave sums are combined in the epilogue (cg_scalar)
@@ -384,15 +445,15 @@ __global__ __launch_bounds__((RowTCfg<T, H>::THREADS), (RowTCfg<T, H>::MINW)) vo
     }
   }
   __syncthreads();   // twiddles staged (the tile area is free)
-  park_tile(H0{});
-  __syncthreads();
-  load_tile(H1{});   // in flight during the even rebuild
-  rebuild(H0{}, va);
-  __syncthreads();   // even tile consumed
-  park_tile(H1{});
-  __syncthreads();
-  rebuild(H1{}, vb);
-  __syncthreads();   // tile consumed: the FFT exchange images overlay it
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    park_tile(u);
+    __syncthreads();
+    if (u + 1 < NU) load_tile(u + 1);            // in flight during this chunk's rebuild
+    if (u < NCH) rebuild(u, va);
+    else rebuild(u, vb);
+    __syncthreads();   // chunk consumed (the last: the FFT exchange images overlay the tile)
+  }
   fft_line2<T, H, P, +1, 1, Cfg::WAVE>(va, vb, lds, lbase, t, tab);
 
   // combine: y[p] = ye + conj(W_L^p) yo, y[p+H] = ye - conj(W_L^p) yo; real rows out

@@ -189,31 +189,45 @@ class SlabToeplitz:
 
     def pcg(self, b, maxiter=20, tol=1e-8, precond=True, callback=None):
         """conj_grad2 (`cg.py:44-80`) on the slabs: x0 = 0, per-RHS alpha / beta from all-reduced
-        dots, break when EVERY global sqrt(r.r) < tol.  Returns (x, iterations run)."""
+        dots, break when EVERY global sqrt(r.r) < tol.  Returns (x, iterations run).
+
+        The break is decided on the device: every rank holds the same reduced r.r, so a device
+        flag `done` (all sqrt(r.r) < tol after some iteration) is identical everywhere; the
+        iterations after it leave x unchanged (alpha masked to 0, the same x as the reference's
+        break) and the host queues all `maxiter` iterations without a synchronisation (RCCL: the
+        dots' all-reduces are stream-ordered).  The iteration count is read once at the end.
+        With a callback (`cg.py:77-78`, called after every iteration that did not break) the
+        host must look at the flag, so that form synchronises per iteration as the reference."""
         P = (lambda v: self.apply(_lib.OP_CINV, v)) if precond else (lambda v: v)
         x = torch.zeros_like(b)
         r = b.clone()
         z = P(r)
         p = z
         rs = self.dot(r, z)
-        it = 0
+        done = torch.zeros((), dtype=torch.bool, device=b.device)
+        its = torch.zeros((), dtype=torch.int64, device=b.device)
         for n in range(int(maxiter)):
-            it = n + 1
+            its += (~done).long()
             Ap = self.apply(_lib.OP_K, p)
-            alpha = rs / self.dot(p, Ap)
+            # after the break every update is masked out (alpha = 0), so x stays the iterate the
+            # reference returns; torch.where keeps the 0/0 of the masked iterations out
+            alpha = torch.where(done, torch.zeros_like(rs), rs / self.dot(p, Ap))
             x = x + alpha.unsqueeze(-1) * p
             r = r - alpha.unsqueeze(-1) * Ap
             rnew = self.dot(r, r)
-            if bool(torch.all(torch.sqrt(rnew) < tol)):
-                break
+            done = done | torch.all(torch.sqrt(rnew) < tol)
+            if callback is not None:
+                if bool(done):
+                    break
             z = P(r)
             zr = self.dot(z, r)
             beta = zr / rs
-            p = z + beta.unsqueeze(-1) * p
+            # p = 0 once done: the masked iterations then see Ap = 0 and finite x, r
+            p = torch.where(done, torch.zeros((), dtype=p.dtype, device=p.device), z + beta.unsqueeze(-1) * p)
             rs = zr                   # = sum(r * z) at the top of the next iteration (cg.py:64)
             if callback is not None:
                 callback(n, x)
-        return x, it
+        return x, int(its)
 
     def compute_kn(self, Knm_local, maxiter=20, tol=1e-8):
         """kn = R^T K^{-1} Knm^T (`hipgp.py:143-145`) with Knm's axis-0 rows on this rank;

@@ -42,7 +42,8 @@ def gen_case(zk, hg, dtype, case):
     y = np.sin(3 * x[:, :1]) * np.cos(2 * x[:, 1:]) + .1 * rs.randn(64, 1)
     s = np.full((64, 1), .1)
     out = {"grid0": _np(xgrids[0]), "grid1": _np(xgrids[1]), "x": x, "y": y, "s": s,
-           "theta1_init": _np(mod.global_theta1), "theta2_init": _np(mod.global_theta2)}
+           # copies: _np views the parameter's storage, which the fit updates in place
+           "theta1_init": _np(mod.global_theta1).copy(), "theta2_init": _np(mod.global_theta2).copy()}
     snaps = []
 
     def batch_cb(m, xb, yb, sb):

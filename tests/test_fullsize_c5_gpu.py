@@ -1,0 +1,97 @@
+"""BASELINE config C5 at full size on the GPU: the 3-D grid 256 x 256 x 128 (M = 8.4 M,
+M' = 66 M) with the per-GPU batch of 25 right-hand sides (200 split over 8 GPUs).
+
+* `_solve` (PCG, `toeplitz_tensor.py:54-68`) and `compute_kn` (`hipgp.py:117-146`) in fp32 --
+  the fused 3-D iteration: k_row_inv_t<float, 128, EPI_*> epilogues on 256 i0 planes per RHS,
+  k_fold_rows / k_cg_alpha, several RHS chunks over the two streams -- against the fp64 plan of
+  the same problem and the residual |K x - b|;
+* a mean-field `elbo_and_grad` with line-integral observations (`svi_gp.py:55-69`,
+  `hipgp.py:194-276`) on the C5 grid, fp32 against fp64, for the analytic SqExp Knm and the
+  Matern-5/2 MC estimator the C5 experiment uses (`run_domain_experiment.py:77-82`).
+Grid as config 5 (x, y in [-.25, .25], z in [-.05, .05]), Matern-5/2.  Config 5's own
+hyper-parameters (sig2 .1, ell .1 = 50 x-spacings, nugget 1e-3) leave K so ill-conditioned that
+20 PCG iterations stay far from the solution (fp64 residual 1.8 |b| measured), so fp32 and fp64
+iterates differ chaotically there; these tests use ell = 0.01 (5 x-spacings, 13 z-spacings) and a
+nugget of 0.1 sig2, where 20 iterations converge and fp32 must track fp64 (as tests/test_large_gpu.py
+does for C3 / C4)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+DIMS = (256, 256, 128)
+LO, HI = (-.25, -.25, -.05), (.25, .25, .05)
+
+
+def _grids(dt, device=DEV):
+    return [torch.linspace(lo, hi, m, device=device, dtype=dt) for m, lo, hi in zip(DIMS, LO, HI)]
+
+
+SIG2, ELL, JIT = 0.1, 0.01, 0.01
+
+
+def _tt(dt):
+    import ziggy.kernels as zk
+    from ziggy.misc.toeplitz_tensor import ToeplitzTensor
+    k = zk.Matern(nu=2.5, dtype=dt)
+    return ToeplitzTensor(_grids(dt), lambda x, y: k.forward(x, y, params=(SIG2, ELL)), jitter_val=JIT)
+
+
+def test_solve_compute_kn_C5_B25():
+    B = 25
+    M = int(np.prod(DIMS))
+    g = torch.Generator(device=DEV).manual_seed(31)
+    b64 = torch.randn(B, M, device=DEV, generator=g, dtype=torch.float64)
+    out = {}
+    for dt in (torch.float64, torch.float32):
+        T = _tt(dt)
+        b = b64.to(dt)
+        x = T._solve(b, do_precond=True, maxiter=20, tol=1e-8)
+        res = (T._matmul_by_K(x).double() - b64).norm(dim=1) / b64.norm(dim=1)
+        kn = T._matmul_by_RT(T.inv_matmul(b, do_precond=True, maxiter=20, tol=1e-8))
+        assert kn.shape == (B, 510 * 510 * 254)
+        out[dt] = (x.double(), res, kn)      # 288 GB of HBM: both runs' results stay resident
+        del T, b
+        torch.cuda.empty_cache()
+    x64, r64, kn64 = out[torch.float64]
+    x32, r32, kn32 = out[torch.float32]
+    print("C5 residuals fp64", float(r64.max()), "fp32", float(r32.max()))
+    assert float(r64.max()) < 0.05
+    assert float((r32 - r64).abs().max()) < 1e-3
+    rel_x = float(((x32 - x64).norm(dim=1) / x64.norm(dim=1)).max())
+    rel_kn = float(((kn32.double() - kn64).norm(dim=1) / kn64.norm(dim=1)).max())
+    print("C5 fp32 vs fp64: x", rel_x, "kn", rel_kn)
+    assert rel_x < 1e-3 and rel_kn < 1e-3, (rel_x, rel_kn)
+
+
+@pytest.mark.parametrize("estimator", ["analytic", "mc-biased"])
+def test_integrated_elbo_C5(estimator):
+    import ziggy.hipgp as hg
+    import ziggy.kernels as zk
+    rs = np.random.RandomState(7)
+    n = 25
+    x = (rs.rand(n, 3) - .5) * np.array([.5, .5, .1])
+    y = rs.randn(n, 1) * .1
+    res = {}
+    for dt in (torch.float64, torch.float32):
+        k = zk.SqExp(dtype=dt) if estimator == "analytic" else zk.Matern(nu=2.5, dtype=dt)
+        mod = hg.MeanFieldToeplitzGP(k, _grids(dt, "cpu"), num_obs=5000, sig2_init=SIG2, ell_init=ELL,
+                                     noise2_init=.01, dtype=dt, jitter_val=JIT)
+        torch.manual_seed(9)
+        with torch.no_grad():
+            mod.global_theta1.copy_((torch.randn(mod.Mprime, 1, dtype=torch.float64) * .01).to(dt))
+        mod = mod.cuda_params(0)
+        torch.manual_seed(11)           # the MC estimator's one offset draw (kernels.py:19-39)
+        elbo = mod.elbo_and_grad(torch.tensor(x, dtype=dt, device=DEV), torch.tensor(y, dtype=dt, device=DEV),
+                                 maxiter_cg=20, integrated_obs=True, semi_integrated_estimator=estimator,
+                                 semi_integrated_samps=10)
+        res[dt] = (float(elbo), mod.global_theta1.grad.double(), mod.global_theta2.grad.double())
+        del mod
+        torch.cuda.empty_cache()
+    e64, g1_64, g2_64 = res[torch.float64]
+    e32, g1_32, g2_32 = res[torch.float32]
+    print("C5 integrated ELBO", estimator, e64, e32)
+    assert np.isfinite(e64) and abs(e32 - e64) < 1e-4 * abs(e64), (e32, e64)
+    for a, b in ((g1_32, g1_64), (g2_32, g2_64)):
+        assert float((a - b).norm() / b.norm()) < 1e-3, float((a - b).norm() / b.norm())

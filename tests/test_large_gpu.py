@@ -24,7 +24,8 @@ def _tt(m, dtype, jitter=0.1):
     return ToeplitzTensor(grids, lambda x, y: k.forward(x, y, params=(1., 20. / m)), jitter_val=jitter)
 
 
-@pytest.mark.parametrize("m,B", [(2048, 16), (4096, 10)], ids=["C3_2048x2048_B16", "C4_4096x4096_B10"])
+@pytest.mark.parametrize("m,B", [(2048, 16), (4096, 10), (4096, 25)],
+                         ids=["C3_2048x2048_B16", "C4_4096x4096_B10", "C4_4096x4096_B25"])
 def test_pcg_compute_kn_fp32_vs_fp64(m, B):
     g = torch.Generator(device=DEV).manual_seed(21)
     b64 = torch.randn(B, m * m, device=DEV, generator=g, dtype=torch.float64)

@@ -313,8 +313,10 @@ def test_long_lines_accuracy_and_repeatability(dims, dtype):
             v64 = torch.tensor(v, device=DEV)
             refs = {op: _np(P64.apply(op, v64)) for op in (_lib.OP_K, _lib.OP_RT)}
             del P64, v64
+        # R^T: fp32 FFT rounding over the L_R grid (8192^2 at C4) grows with its size: 1e-6 at
+        # 4096 x 8, 7e-6 at 2048^2, 1.3e-5 at 4096^2 (measured); K stays within 5e-6
         for op, ref in refs.items():
-            assert rel_err(_np(P.apply(op, vt)), ref) < 5e-6, op
+            assert rel_err(_np(P.apply(op, vt)), ref) < (5e-6 if op == _lib.OP_K else 3e-5), op
     if dtype == torch.float64 and np.prod(dims) < 5e6:
         T = zo.ToeplitzOracle(col, dims)
         assert rel_err(P.spectrum(_lib.SPEC_D).cpu().numpy(), T.D) < 1e-12

@@ -16,7 +16,9 @@ pytestmark = pytest.mark.gpu
 
 CASES = {"2d_f32": ((128, 96), torch.float32), "2d_f64": ((96, 80), torch.float64),
          "3d_f32": ((32, 24, 20), torch.float32), "3d_f64": ((24, 20, 16), torch.float64),
-         "2d_C2_f32": ((1024, 1024), torch.float32)}
+         "2d_C2_f32": ((1024, 1024), torch.float32),
+         # full BASELINE sizes: C5's 3-D grid (256-plane folds, k_cg_alpha) and C4's 4096-point rows
+         "3d_C5_f32": ((256, 256, 128), torch.float32), "2d_C4_f32": ((4096, 4096), torch.float32)}
 
 
 def _plan(dims, dt):

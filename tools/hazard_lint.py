@@ -26,7 +26,10 @@ VALU = re.compile(r"^\s*v_\w+\s+(v\[(\d+):(\d+)\]|v(\d+))")
 def code_objects(lib, tmp):
     """The gfx950 code objects of every offload bundle in the library's .hip_fatbin."""
     fat = os.path.join(tmp, "fat.bin")
-    subprocess.run(["objcopy", f"--dump-section=.hip_fatbin={fat}", lib], check=True, capture_output=True)
+    # objcopy writes its output file even when only dumping: give it a scratch one (with the
+    # input alone it rewrites the library in place -- under a process that has it mapped)
+    subprocess.run(["objcopy", f"--dump-section=.hip_fatbin={fat}", lib, os.path.join(tmp, "scratch.so")],
+                   check=True, capture_output=True)
     data = open(fat, "rb").read()
     starts = []
     i = data.find(MAGIC)
