@@ -18,7 +18,7 @@ HGP_F32, HGP_F64 = 0, 1
 OP_K, OP_CINV, OP_RT, OP_R = 0, 1, 2, 3
 SPEC_D, SPEC_DSQRT, SPEC_DI = 0, 1, 2
 LAYOUT_ROWS, LAYOUT_COLS = 0, 1
-SLAB_FWD, SLAB_CONV, SLAB_INV = 0, 1, 2
+SLAB_FWD, SLAB_CONV, SLAB_INV, SLAB_CONV_A2A = 0, 1, 2, 3
 
 # every symbol include/hipgp.h declares (tests check the library exports all of them)
 EXPORTS = (

@@ -202,12 +202,12 @@ template <typename T>
 int launch(int H, int mode, int lay, const PassDesc& d, int64_t lines_contig, hipStream_t s) {
   const PassGeom g = pass_geom<T>(H, lay);
   if (g.C == 0) return fail(HGP_E_UNSUPPORTED, "transform half-length " + std::to_string(H) + " not supported");
-  // only the fp64 forward transforms fold an input longer than H (hgp_pass.hpp CAN_FOLD)
-  const bool can_fold = sizeof(T) == 8 && mode == PASS_FWD;
-  if (mode != PASS_INV && !can_fold && d.in.len > H)
+  // forward transforms and complex-spectrum conv passes fold an input longer than H (hgp_pass.hpp CAN_FOLD)
+  const bool can_fold = mode == PASS_FWD || mode == PASS_CONVC;
+  if (mode != PASS_INV && (can_fold ? d.in.len > 2 * H : d.in.len > H))
     return fail(HGP_E_ARG, "internal: pass input length " + std::to_string(d.in.len) + " > H = " + std::to_string(H));
   int64_t nb;
-  if (lay == LAY_STRIDED) nb = (int64_t)d.Q * d.Rn * ((d.In + g.C - 1) / g.C);
+  if (lay == LAY_STRIDED || lay == LAY_SEG_S) nb = (int64_t)d.Q * d.Rn * ((d.In + g.C - 1) / g.C);
   else nb = (lines_contig + g.C - 1) / g.C;
   if (nb <= 0) return 0;
   if (nb > 0x7fffffff) return fail(HGP_E_UNSUPPORTED, "grid too large");
@@ -847,10 +847,34 @@ int slab_pass_t(hgp_plan* P, int op, int stage, const void* in, void* out, int64
     return 0;
   };
   const int64_t rows_len = stage == HGP_SLAB_FWD ? g.in[0] : g.out[0];
-  if (stage != HGP_SLAB_CONV && (nrows < 1 || nrows > rows_len))
+  const bool conv = stage == HGP_SLAB_CONV || stage == HGP_SLAB_CONV_A2A;
+  if (!conv && (nrows < 1 || nrows > rows_len))
     return fail(HGP_E_ARG, "nrows must be in [1, " + std::to_string(rows_len) + "]");
-  if (stage == HGP_SLAB_CONV && (g0 < 0 || ng < 1 || g0 + ng > sg.NG))
+  if (conv && (g0 < 0 || ng < 1 || g0 + ng > sg.NG))
     return fail(HGP_E_ARG, "groups [g0, g0 + ng) must lie in [0, " + std::to_string(sg.NG) + ")");
+  if (stage == HGP_SLAB_CONV_A2A) {
+    // rank-block layouts of the two all-to-all buffers (hgp_pass.hpp LAY_SEG_*): nrows = ranks
+    if (nrows < 1) return fail(HGP_E_ARG, "HGP_SLAB_CONV_A2A: nrows is the world size (>= 1)");
+    if (in == out) return fail(HGP_E_ARG, "HGP_SLAB_CONV_A2A: in and out must differ");
+    const int64_t inner = d == 2 ? 1 : sg.inner;
+    const int64_t P0 = std::max(g.in[0], g.out[0]);
+    if (ng * nrhs * P0 * inner >= ((int64_t)1 << 31)) return fail(HGP_E_UNSUPPORTED, "slab too large");
+    PassDesc Sd = base_desc();
+    Sd.in = View{const_cast<void*>(in), 0, 0, inner, (int)g.in[0]};
+    Sd.out = View{out, 0, 0, inner, (int)g.out[0]};
+    Sd.seg_ws = (int)nrows;
+    const size_t se = g.spec_kind == SPEC_REAL ? sizeof(T) : cs;
+    Sd.spec = static_cast<const char*>(g.spec) + (size_t)(g0 * g.L[0]) * se;
+    Sd.spec_kind = g.spec_kind; Sd.spec_p = 1; Sd.spec_r = g.L[0];
+    Sd.tw = g.tw[0].ptr; Sd.Q = (int)nrhs; Sd.Rn = (int)ng;
+    if (d == 2) {     // lines (g, q), position-fast; spectrum [c1][k0]
+      Sd.spec_i = 0; Sd.In = 1;
+      return launch<T>((int)(g.L[0] / 2), conv_mode, LAY_SEG_C, Sd, nrhs * ng, st);
+    }
+    // d = 3: lines (g = k1, q) x c2 (adjacent); spectrum [c2][k1][k0]
+    Sd.spec_i = g.L[1] * g.L[0]; Sd.In = (int)(g.L[2] / 2 + 1);
+    return launch<T>((int)(g.L[0] / 2), conv_mode, LAY_SEG_S, Sd, 0, st);
+  }
   if (d == 2) {
     const int64_t H1 = g.L[1] / 2;
     if (stage == HGP_SLAB_FWD || stage == HGP_SLAB_INV) {

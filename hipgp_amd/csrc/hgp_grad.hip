@@ -140,12 +140,16 @@ struct LGeo {
 __device__ __forceinline__ int pos_of(int k, int L) { return (k & 1) ? (L >> 1) + (k >> 1) : (k >> 1); }
 __device__ __forceinline__ int freq_of(int s, int L) { return s < (L >> 1) ? 2 * s : 2 * (s - (L >> 1)) + 1; }
 
+// L is 2^k or 3 * 2^k (the mixed-radix R lengths): index arithmetic by division, not masks
 __device__ __forceinline__ void decodeL(int64_t f, const LGeo& G, int* c) {
   for (int a = G.d - 1; a >= 0; --a) {
-    c[a] = (int)(f & (G.L[a] - 1));
-    f >>= __ffs(G.L[a]) - 1;
+    const int64_t q = f / G.L[a];
+    c[a] = (int)(f - q * G.L[a]);
+    f = q;
   }
 }
+// t mod L for t in (-L, 2L)
+__device__ __forceinline__ int wrapL(int t, int L) { return t < 0 ? t + L : (t >= L ? t - L : t); }
 
 template <typename T>
 __global__ void k_pack_pair(const T* __restrict__ v, const T* __restrict__ h, int h_periodic, LGeo G,
@@ -181,7 +185,7 @@ __global__ void k_xspec_acc(const double2* __restrict__ Z, double2* __restrict__
   int64_t nf = 0, fn = 0;
   for (int a = 0; a < G.d; ++a) {
     const int k = freq_of(c[a], G.L[a]);
-    nf = nf * G.L[a] + pos_of((G.L[a] - k) & (G.L[a] - 1), G.L[a]);
+    nf = nf * G.L[a] + pos_of(wrapL(G.L[a] - k, G.L[a]), G.L[a]);
     fn = fn * G.L[a] + k;
   }
   const double2 zf = Z[f], zn = Z[nf];
@@ -222,7 +226,7 @@ __global__ void k_gather_n(const double2* __restrict__ F, LGeo G, int h_periodic
     for (int a = 0; a < G.d; ++a) {
       const int sel = (k >> a) & 1;
       if (sel >= nt[a]) { ok = false; break; }
-      idx = idx * G.L[a] + pos_of((t[a][sel] + G.L[a]) & (G.L[a] - 1), G.L[a]);
+      idx = idx * G.L[a] + pos_of(wrapL(t[a][sel], G.L[a]), G.L[a]);
     }
     if (ok) s += F[idx].x;
   }
@@ -257,8 +261,8 @@ __global__ void k_gather_flat(const double2* __restrict__ F, LGeo G, int64_t M, 
     dig[0] = (int)rem;
     int64_t ip = 0, in = 0;
     for (int a = 0; a < G.d; ++a) {
-      ip = ip * G.L[a] + pos_of((dig[a] + G.L[a]) & (G.L[a] - 1), G.L[a]);
-      in = in * G.L[a] + pos_of((G.L[a] - dig[a]) & (G.L[a] - 1), G.L[a]);
+      ip = ip * G.L[a] + pos_of(wrapL(dig[a], G.L[a]), G.L[a]);
+      in = in * G.L[a] + pos_of(wrapL(G.L[a] - dig[a], G.L[a]), G.L[a]);
     }
     s += i == 0 ? F[ip].x : F[ip].x + F[in].x;
   }

@@ -33,6 +33,15 @@
 //                 ((c / G) * S0 + p) * G + c % G; a block's C lines are the G columns of one group
 //                 (x C / G right-hand sides), so the 128-B segments a line touches are used whole
 //                 by the block.
+//   LAY_SEG_C / LAY_SEG_S: the axis-0 conv of the grid-block (slab) sharding reading the receive
+//                 buffer of the all-to-all and writing the send buffer of the return all-to-all
+//                 directly (hipgp_amd/slab.py): a line's rows are split over seg_ws ranks in
+//                 balanced blocks (rows [a_r, a_r + cnt_r) of rank r), stored per rank block
+//                 [r][line][row - a_r][c] (line = g * Q + q over the Rn groups and Q RHS, c < inner):
+//                 element (line, row p, c) at NL inner a_r + (line cnt_r + p - a_r) inner + c,
+//                 NL = Rn Q.  _C: position-fast lines (d = 2, inner = 1); _S: C adjacent c lines
+//                 per block as LAY_STRIDED (d = 3, In lines, inner = in.p_stride).  Input split
+//                 over in.len rows, output split over out.len rows.
 #pragma once
 #include <type_traits>
 
@@ -64,7 +73,9 @@
 namespace hgp {
 
 enum { PASS_FWD = 0, PASS_INV = 1, PASS_CONV = 2, PASS_CONVC = 3 };   // CONV: real spectrum, CONVC: complex
-enum { LAY_STRIDED = 0, LAY_CONTIG = 1, LAY_RP = 2, LAY_R1 = 3, LAY_CONTIG_G = 4 };
+enum { LAY_STRIDED = 0, LAY_CONTIG = 1, LAY_RP = 2, LAY_R1 = 3, LAY_CONTIG_G = 4, LAY_SEG_C = 5, LAY_SEG_S = 6 };
+// strided thread mapping (C adjacent lines, threads line-fast) vs position-fast lines
+constexpr bool lay_smap(int lay) { return lay == LAY_STRIDED || lay == LAY_SEG_S; }
 enum { SPEC_REAL = 0, SPEC_CPLX = 1, SPEC_CPLX_CONJ = 2 };
 // row-inverse epilogue (hgp_rows.hpp): EPI_XR x/r update (unpreconditioned PCG); with the
 // preconditioner the x update is deferred to the C^-1 pass: EPI_R r update, EPI_XP x and p
@@ -90,6 +101,7 @@ struct PassDesc {
   int Rn, In;                 // lines per RHS: r in [0,Rn) (outer), i in [0,In) (inner, strided)
   int nrows;                  // LAY_RP: real rows per RHS (the pair (2r, 2r+1) needs 2r+1 < nrows)
   int grp;                    // LAY_CONTIG_G: columns per group G (r_stride = S0, the group's pitch / G)
+  int seg_ws;                 // LAY_SEG_*: ranks the rows are split over
   const int* done;            // optional device flag: skip the pass when *done != 0
   // CONV passes: spectral dot of the transformed line with itself weighted by the real
   // spectrum, sum_k S_k |X_k|^2 = <x, op x> by Parseval (the crop is exact: x is zero outside
@@ -143,10 +155,10 @@ template <typename T, int H, int LAY> struct PassCfg {
     while (c > 1 && (c * TT > 1024 || lds_bytes_for(c) > LDS_CAP / 2)) c >>= 1;
     return c;
   }
-  static constexpr int C = (LAY == LAY_STRIDED) ? c_strided() : c_contig();
+  static constexpr int C = lay_smap(LAY) ? c_strided() : c_contig();
   // position-fast layouts keep each line inside one wavefront when TT <= 64: exchanges then
   // need no block barrier (hgp_fft.hpp xsync)
-  static constexpr bool WAVE = (LAY != LAY_STRIDED) && TT <= 64;
+  static constexpr bool WAVE = !lay_smap(LAY) && TT <= 64;
   static constexpr int THREADS = C * TT;
   static constexpr int EX_ELEMS = ex_elems(C);
   static constexpr int LDS = lds_bytes_for(C);
@@ -155,7 +167,7 @@ template <typename T, int H, int LAY> struct PassCfg {
   static constexpr int BLOCKS_BY_LDS = LDS_CAP / LDS;
   static constexpr int MINW_LDS = (BLOCKS_BY_LDS * WAVES_PER_BLOCK) / 4;
   static constexpr int MINW_AUTO = MINW_LDS < 1 ? 1 : (MINW_LDS > 4 ? 4 : MINW_LDS);
-  static constexpr int MINW_SET = (LAY == LAY_STRIDED) ? (TT >= 16 ? HGP_MINW_STRIDED : HGP_MINW_STRIDED_SMALL)
+  static constexpr int MINW_SET = lay_smap(LAY) ? (TT >= 16 ? HGP_MINW_STRIDED : HGP_MINW_STRIDED_SMALL)
                                  : (LAY == LAY_CONTIG || LAY == LAY_CONTIG_G) ? HGP_MINW_CONTIG : HGP_MINW_ROW;
   static constexpr int MINW = MINW_SET > 0 ? MINW_SET : MINW_AUTO;
 };
@@ -215,9 +227,10 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
   constexpr bool HERM_OUT = RP_IN;                                   // compact half spectra out
   constexpr bool R1 = (LAY == LAY_R1);
   constexpr bool REAL_OUT = RP_OUT || R1;
-  // inputs longer than H (folded x[p] +- x[p+H]) occur only in the fp64 setup grids' forward
-  // transforms; every other pass has in_len <= H (checked on the host), so no second load.
-  constexpr bool CAN_FOLD = std::is_same<T, double>::value && MODE == PASS_FWD;
+  // inputs longer than H (folded x[p] +- x[p+H]): the fp64 set-up grids' forward transforms,
+  // and the R operator's passes when L_R = 3 * 2^k < 2n (its input lives on the n-grid); the
+  // K / C^-1 column pass (PASS_CONV) never folds (in_len <= H, checked on the host)
+  constexpr bool CAN_FOLD = MODE == PASS_FWD || MODE == PASS_CONVC;
   if (d.done != nullptr && *d.done) return;                          // uniform: before any barrier
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   C2<T>* lds = reinterpret_cast<C2<T>*>(smem_raw);
@@ -227,8 +240,10 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
 
   const int tid = threadIdx.x;
   int l, t, lbase;
-  constexpr int LSTRIDE = (LAY == LAY_STRIDED) ? C : 1;
-  if constexpr (LAY == LAY_STRIDED) { t = tid / C; l = tid - t * C; lbase = l; }
+  constexpr bool SMAP = lay_smap(LAY);
+  constexpr bool SEG = (LAY == LAY_SEG_C || LAY == LAY_SEG_S);
+  constexpr int LSTRIDE = SMAP ? C : 1;
+  if constexpr (SMAP) { t = tid / C; l = tid - t * C; lbase = l; }
   else {
     // lines of whole waves: the line index is wave-uniform, kept in a scalar register so the
     // line's base pointers are scalar and every load/store is base + 32-bit lane offset
@@ -245,7 +260,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
   int q, r, i, i0 = 0, lc = 0;
   int64_t gbase = 0;          // LAY_CONTIG_G: element offset of the line in its RHS's slab
   bool valid;
-  if constexpr (LAY == LAY_STRIDED) {
+  if constexpr (SMAP) {
     // logical block = (q, g) with g fastest; the XCD remap keeps consecutive g (adjacent
     // column groups) of one RHS on one XCD.
     const int lb = xcd_remap(blockIdx.x, gridDim.x);
@@ -272,7 +287,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
     valid = r < d.Rn;
     if (!valid) { q = 0; r = 0; }
     gbase = (int64_t)(r / G) * d.in.r_stride * G + (r % G);
-  } else if constexpr (LAY == LAY_CONTIG) {
+  } else if constexpr (LAY == LAY_CONTIG || LAY == LAY_SEG_C) {
     // RHS-fastest: the C lines of a block are the same column r of C right-hand sides, so
     // they share one spectrum line; the XCD remap keeps the blocks of one column (all its
     // RHS) on one XCD, so the line is fetched into that L2 once
@@ -303,6 +318,8 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
   } else if constexpr (HERM_IN) {
     in_c = reinterpret_cast<const C2<T>*>(d.in.ptr) + (int64_t)q * d.in.q_stride + (int64_t)(2 * r) * d.in.r_stride;
     in_c2 = has2 ? in_c + d.in.r_stride : in_c;
+  } else if constexpr (SEG) {
+    in_c = reinterpret_cast<const C2<T>*>(d.in.ptr);   // positions by seg_off (the rank blocks)
   } else if constexpr (LAY == LAY_STRIDED) {
     in_c = reinterpret_cast<const C2<T>*>(d.in.ptr) + (int64_t)q * d.in.q_stride + (int64_t)r * d.in.r_stride + i0;
   } else if constexpr (LAY == LAY_CONTIG_G) {
@@ -320,6 +337,8 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
   } else if constexpr (HERM_OUT) {
     out_c = reinterpret_cast<C2<T>*>(d.out.ptr) + (int64_t)q * d.out.q_stride + (int64_t)(2 * r) * d.out.r_stride;
     out_c2 = out_c + d.out.r_stride;
+  } else if constexpr (SEG) {
+    out_c = reinterpret_cast<C2<T>*>(d.out.ptr);
   } else if constexpr (LAY == LAY_STRIDED) {
     out_c = reinterpret_cast<C2<T>*>(d.out.ptr) + (int64_t)q * d.out.q_stride + (int64_t)r * d.out.r_stride + i0;
   } else if constexpr (LAY == LAY_CONTIG_G) {
@@ -330,8 +349,28 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
   // element offset of position p in this lane's line (32-bit: one RHS slab < 2^31 elements)
   const int ips = (LAY == LAY_STRIDED) ? (int)d.in.p_stride : (LAY == LAY_CONTIG_G) ? d.grp : 1;
   const int ops = (LAY == LAY_STRIDED) ? (int)d.out.p_stride : (LAY == LAY_CONTIG_G) ? d.grp : 1;
-  auto in_at = [&](int p) -> int { return (LAY == LAY_STRIDED) ? lc + p * ips : (LAY == LAY_CONTIG_G) ? p * ips : p; };
-  auto out_at = [&](int p) -> int { return (LAY == LAY_STRIDED) ? lc + p * ops : (LAY == LAY_CONTIG_G) ? p * ops : p; };
+  // rank-block layouts: element offset of row p of this lane's line (balanced split of n rows)
+  const int s_inner = (LAY == LAY_SEG_S) ? (int)d.in.p_stride : 1;   // element pitch of c
+  const int64_t s_line = SEG ? (int64_t)r * d.Q + q : 0;
+  const int64_t s_nl = SEG ? (int64_t)d.Rn * d.Q : 0;
+  const int s_c = (LAY == LAY_SEG_S) ? i0 + lc : 0;
+  auto seg_off = [&](int p, int n) -> int64_t {
+    const int ws = d.seg_ws, base = n / ws, extra = n - base * ws;
+    const int big = extra * (base + 1);
+    const int rk = p < big ? p / (base + 1) : extra + (p - big) / (base > 0 ? base : 1);
+    const int a = rk * base + (rk < extra ? rk : extra);
+    const int cnt = base + (rk < extra ? 1 : 0);
+    return (s_nl * a + s_line * cnt + (p - a)) * s_inner + s_c;
+  };
+  using Off = std::conditional_t<SEG, int64_t, int>;   // 32-bit lane offsets on the fast layouts
+  auto in_at = [&](int p) -> Off {
+    if constexpr (SEG) return seg_off(p, d.in.len);
+    else return (LAY == LAY_STRIDED) ? lc + p * ips : (LAY == LAY_CONTIG_G) ? p * ips : p;
+  };
+  auto out_at = [&](int p) -> Off {
+    if constexpr (SEG) return seg_off(p, d.out.len);
+    else return (LAY == LAY_STRIDED) ? lc + p * ops : (LAY == LAY_CONTIG_G) ? p * ops : p;
+  };
 
   // Loads are unconditional on clamped (always in-bounds) addresses and zeroed afterwards:
   // a per-element branch around a load makes hipcc wait vmcnt(0) per element.
@@ -383,7 +422,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
   if constexpr (MODE == PASS_CONV) {
     sb = reinterpret_cast<const T*>(d.spec) + (int64_t)i0 * d.spec_i + (int64_t)r * d.spec_r;
     sp = (int)d.spec_p;
-    so = (LAY == LAY_STRIDED ? lc * (int)d.spec_i : 0) + t * sp;
+    so = (SMAP ? lc * (int)d.spec_i : 0) + t * sp;
   }
   // contiguous lines of whole waves: wave-uniform line bases -> raw buffer accesses (32-bit
   // lane offsets; the zero padding beyond in_len and the crop beyond out_len come from the
@@ -394,7 +433,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
 #define HGP_BUF_F64 1
 #endif
   constexpr bool CONTIG = (LAY == LAY_CONTIG || LAY == LAY_CONTIG_G);
-  constexpr bool BUF = (std::is_same<T, float>::value || HGP_BUF_F64) && CONTIG && (TT % 64 == 0) && !CAN_FOLD;
+  constexpr bool BUF = (std::is_same<T, float>::value || HGP_BUF_F64) && CONTIG && (TT % 64 == 0);
   // element stride of a line's positions: 1, or G in the grouped layout; the range then ends
   // one element past the line's last valid position ((len - 1) G + 1 elements)
   const uint32_t es = (uint32_t)ips * (uint32_t)sizeof(C2<T>);
@@ -418,7 +457,10 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
       }
       C2<T> c = mk<T>(0, 0);
       if constexpr (CAN_FOLD) {
-        if (fold) c = load_hi(p);
+        if (fold) {                 // uniform; beyond in_len the buffer range returns 0
+          if constexpr (BUF) c = buf_ld_c2<T>(rin, (uint32_t)t * es, (uint32_t)(TT * k + H) * es);
+          else c = load_hi(p);
+        }
       }
       va[k] = cadd<T>(a, c);
       vb[k] = cmul<T>(csub<T>(a, c), tw_at<T, H>(tab, p));
@@ -497,7 +539,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
       // complex spectrum at (i, r, kperm): block-uniform base + 32-bit lane offset
       const C2<T>* sbase = reinterpret_cast<const C2<T>*>(d.spec) + (int64_t)i0 * d.spec_i + (int64_t)r * d.spec_r;
       const int sp = (int)d.spec_p;
-      const int so0 = (LAY == LAY_STRIDED ? lc * (int)d.spec_i : 0) + t * sp;
+      const int so0 = (SMAP ? lc * (int)d.spec_i : 0) + t * sp;
 #pragma unroll
       for (int k = 0; k < P; ++k) {
         const C2<T> s0 = sbase[so0 + TT * k * sp];
@@ -531,7 +573,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
     // opaque copies: positions/offsets are recomputed here instead of being kept live (in
     // registers or scratch) from the loads at the top of the kernel
     asm volatile("" : "+v"(t));
-    if constexpr (LAY == LAY_STRIDED) asm volatile("" : "+v"(lc));
+    if constexpr (SMAP) asm volatile("" : "+v"(lc));
 #pragma unroll
     for (int k = 0; k < P; ++k) {
       const int p = t + TT * k;
@@ -566,7 +608,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
         if (t == 0 && valid) reinterpret_cast<T*>(d.partial)[(int64_t)q * d.Rn + r] = s;
       }
     }
-    if constexpr (MODE == PASS_CONV && LAY != LAY_STRIDED) {   // CONTIG / CONTIG_G / R1
+    if constexpr (MODE == PASS_CONV && !SMAP) {   // CONTIG / CONTIG_G / SEG_C / R1
       if (d.spart != nullptr) {     // uniform over the block
         const T s = line_sum<T, TT>(sdot, reinterpret_cast<T*>(smem_raw));
         if (t == 0 && valid) {

@@ -39,12 +39,16 @@ static hipError_t launch_h(int mode, int lay, const PassDesc& d, int64_t nblocks
     // the grouped-column intermediate of long fp32 rows (hgp_rows.hpp RowTCfg::G); any axis-0 H
     if constexpr (std::is_same<T, float>::value)
       if (lay == LAY_CONTIG_G) return launch_one<T, H, PASS_CONV, LAY_CONTIG_G>(d, nblocks, s);
+    if (lay == LAY_SEG_C) return launch_one<T, H, PASS_CONV, LAY_SEG_C>(d, nblocks, s);
+    if (lay == LAY_SEG_S) return launch_one<T, H, PASS_CONV, LAY_SEG_S>(d, nblocks, s);
   } else if (mode == PASS_CONVC) {
     if (lay == LAY_STRIDED) return launch_one<T, H, PASS_CONVC, LAY_STRIDED>(d, nblocks, s);
     if (lay == LAY_CONTIG) return launch_one<T, H, PASS_CONVC, LAY_CONTIG>(d, nblocks, s);
     if (lay == LAY_R1) return launch_one<T, H, PASS_CONVC, LAY_R1>(d, nblocks, s);
     if constexpr (std::is_same<T, float>::value)
       if (lay == LAY_CONTIG_G) return launch_one<T, H, PASS_CONVC, LAY_CONTIG_G>(d, nblocks, s);
+    if (lay == LAY_SEG_C) return launch_one<T, H, PASS_CONVC, LAY_SEG_C>(d, nblocks, s);
+    if (lay == LAY_SEG_S) return launch_one<T, H, PASS_CONVC, LAY_SEG_S>(d, nblocks, s);
   }
   return hipErrorInvalidValue;
 }
@@ -56,8 +60,8 @@ static PassGeom geom_one() {
 
 template <typename T, int H>
 static PassGeom geom_h(int lay) {
-  if (lay == LAY_STRIDED) return geom_one<T, H, LAY_STRIDED>();
-  if (lay == LAY_CONTIG || lay == LAY_CONTIG_G) return geom_one<T, H, LAY_CONTIG>();
+  if (lay == LAY_STRIDED || lay == LAY_SEG_S) return geom_one<T, H, LAY_STRIDED>();
+  if (lay == LAY_CONTIG || lay == LAY_CONTIG_G || lay == LAY_SEG_C) return geom_one<T, H, LAY_CONTIG>();
   if (lay == LAY_RP) return geom_one<T, H, LAY_RP>();
   return geom_one<T, H, LAY_R1>();
 }

@@ -113,8 +113,10 @@ __device__ __forceinline__ int row_block_id() {
   return REMAP ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
 }
 
-// The forward row transform of a block's row pairs after their real values are in va (Re = row
-// 2l, Im = row 2l+1, positions t + TT k < H, zero padded): twiddled odd half, both halves' FFTs,
+// The forward row transform of a block's row pairs after their even-half inputs are in va and
+// their odd-half inputs (before the twiddle) in vb (Re = row 2l, Im = row 2l+1, positions
+// t + TT k < H: va = x[p] + x[p+H], vb = x[p] - x[p+H], = x[p] both for rows of <= H values):
+// twiddled odd half, both halves' FFTs,
 // Hermitian split, and the transposed half spectra out to the intermediate (column pitch S0,
 // grouped by G).  Needs the twiddle table staged in `tab`; uses the LDS area from `lds`.
 template <typename T, int H, int P, int G>
@@ -125,7 +127,7 @@ __device__ __forceinline__ void row_fwd_tail(C2<T> (&va)[P], C2<T> (&vb)[P],
   constexpr int TT = Cfg::TT, C = Cfg::C, PITCH = Cfg::PITCH, NCH = Cfg::NCH, CHC = Cfg::CHC, SEG = Cfg::SEG;
   static_assert(P == Cfg::P, "row_fwd_tail: P");
 #pragma unroll
-  for (int k = 0; k < P; ++k) vb[k] = cmul<T>(va[k], tw_at<T, H>(tab, t + TT * k));
+  for (int k = 0; k < P; ++k) vb[k] = cmul<T>(vb[k], tw_at<T, H>(tab, t + TT * k));
   const BufRsrc rW = buf_rsrc(W, 0x7fffffffu);     // one RHS's slab: < 2 GiB (checked on the host)
   // both frequency halves' transforms, interleaved over the group's exchange image
   fft_line2<T, H, P, -1, 1, Cfg::WAVE>(va, vb, lds, lbase, t, tab);
@@ -212,6 +214,8 @@ __global__ __launch_bounds__((RowTCfg<T, H, G>::THREADS), (RowTCfg<T, H, G>::MIN
   const int in_len = d.in.len;
 
   C2<T> va[P], vb[P];
+  // rows longer than H (the R operator's n-grid input when L_R = 3 * 2^k < 2n): folded halves
+  const bool fold = in_len > H;                    // uniform
   if constexpr (TT % 64 == 0) {
     // raw buffer loads (the pair is wave-uniform): past the row length (zero padding) and for
     // absent rows they return 0
@@ -221,6 +225,13 @@ __global__ __launch_bounds__((RowTCfg<T, H, G>::THREADS), (RowTCfg<T, H, G>::MIN
     for (int k = 0; k < P; ++k) {
       const uint32_t lo = (uint32_t)t * (uint32_t)sizeof(T), so = (uint32_t)(TT * k * (int)sizeof(T));
       va[k] = mk<T>(buf_ld<T>(ra, lo, so), buf_ld<T>(rb_, lo, so));
+      vb[k] = va[k];
+      if (fold) {
+        const uint32_t sh = so + (uint32_t)(H * (int)sizeof(T));
+        const C2<T> hi = mk<T>(buf_ld<T>(ra, lo, sh), buf_ld<T>(rb_, lo, sh));
+        vb[k] = csub<T>(va[k], hi);
+        va[k] = cadd<T>(va[k], hi);
+      }
     }
   } else {
     // several pairs per wave: the row bases differ between lanes, and a buffer resource must be
@@ -233,6 +244,15 @@ __global__ __launch_bounds__((RowTCfg<T, H, G>::THREADS), (RowTCfg<T, H, G>::MIN
       const T a = in_a[ok ? p : 0];
       const T b = in_b[ok ? p : 0];
       va[k] = mk<T>(ok && pvalid ? a : (T)0, ok && has2 ? b : (T)0);
+      vb[k] = va[k];
+      if (fold) {
+        const bool ok2 = p + H < in_len;
+        const T a2 = in_a[ok2 ? p + H : 0];
+        const T b2 = in_b[ok2 ? p + H : 0];
+        const C2<T> hi = mk<T>(ok2 && pvalid ? a2 : (T)0, ok2 && has2 ? b2 : (T)0);
+        vb[k] = csub<T>(va[k], hi);
+        va[k] = cadd<T>(va[k], hi);
+      }
     }
   }
   __syncthreads();   // twiddle table staged

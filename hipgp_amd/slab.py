@@ -87,6 +87,9 @@ class HipSlabEngine:
     def conv(self, op, lines, g0, ng, nrhs):
         self._run(op, _lib.SLAB_CONV, lines, lines, nrhs, 0, g0, ng)
 
+    def conv_a2a(self, op, recv, send, g0, ng, nrhs, ws):
+        self._run(op, _lib.SLAB_CONV_A2A, recv, send, nrhs, ws, g0, ng)
+
     def inv(self, op, E, nrows, y):
         self._run(op, _lib.SLAB_INV, E, y, y.shape[0], nrows)
 
@@ -152,25 +155,20 @@ class SlabToeplitz:
         E = torch.empty((NG, nrhs, ni, inner), dtype=cd, device=dev)
         if ni > 0:
             e.fwd(op, x, ni, E)
-        # 2. all-to-all: my rows of every group -> all rows of my groups
+        # 2. all-to-all: my rows of every group -> all rows of my groups, received as rank blocks
+        #    [r][g][q][i - a_r][c] (rank r's rows [a_r, a_r + cnt_r))
         sizes_in = [(groups[s][1] - groups[s][0]) * nrhs * ni * inner for s in range(ws)]
-        recv = torch.empty(sum(ng * nrhs * (rows_in[r][1] - rows_in[r][0]) * inner for r in range(ws)),
-                           dtype=cd, device=dev)
         sizes_rx = [ng * nrhs * (rows_in[r][1] - rows_in[r][0]) * inner for r in range(ws)]
+        recv = torch.empty(sum(sizes_rx), dtype=cd, device=dev)
         _a2a(recv, E.reshape(-1), sizes_rx, sizes_in, self.group)
-        lines = torch.zeros((ng, nrhs, P0, inner), dtype=cd, device=dev)
-        off = 0
-        for r in range(ws):
-            a, b = rows_in[r]
-            cnt = ng * nrhs * (b - a) * inner
-            lines[:, :, a:b, :] = recv[off:off + cnt].view(ng, nrhs, b - a, inner)
-            off += cnt
-        # 3. the axis-0 convolution on my groups (whole lines)
-        if ng > 0:
-            e.conv(op, lines, gs0, ng, nrhs)
-        # 4. all-to-all back: all rows of my groups -> my output rows of every group
-        send = torch.cat([lines[:, :, rows_out[r][0]:rows_out[r][1], :].reshape(-1) for r in range(ws)])
+        # 3. the axis-0 convolution on my groups straight from the receive buffer into the send
+        #    buffer of the return all-to-all, rank blocks [r][g][q][o - b_r][c] of the output rows
+        #    (HGP_SLAB_CONV_A2A: no line buffer, no gather / scatter copies)
         sizes_tx = [ng * nrhs * (rows_out[r][1] - rows_out[r][0]) * inner for r in range(ws)]
+        send = torch.empty(sum(sizes_tx), dtype=cd, device=dev)
+        if ng > 0:
+            e.conv_a2a(op, recv, send, gs0, ng, nrhs, ws)
+        # 4. all-to-all back: all rows of my groups -> my output rows of every group
         back = torch.empty(NG * nrhs * no * inner, dtype=cd, device=dev)
         sizes_back = [(groups[s][1] - groups[s][0]) * nrhs * no * inner for s in range(ws)]
         _a2a(back, send, sizes_back, sizes_tx, self.group)

@@ -123,8 +123,15 @@ int hgp_pcg_iters(hgp_plan* plan, int* iters);
  * stage HGP_SLAB_CONV: E lines [ng][nrhs][P0][inner], P0 = max(in0, out0) rows per line, groups
  *                      [g0, g0 + ng) of the op's spectrum; in place allowed  (:80-82 etc.)
  * stage HGP_SLAB_INV : E over this rank's nrows output rows -> y (nrhs, nrows, rest) real, crop
+ * stage HGP_SLAB_CONV_A2A: the axis-0 convolution of groups [g0, g0 + ng) straight from the
+ *                      receive buffer of the first all-to-all to the send buffer of the second
+ *                      (no line buffer, no gather / scatter copies): `nrows` = the world size W,
+ *                      in  = [r][g][q][i - a_r][c] for the balanced split of the in0 input rows
+ *                            over the W ranks (rank r: rows [a_r, a_r + cnt_r)),
+ *                      out = [r][g][q][o - b_r][c] for the split of the out0 output rows,
+ *                      g < ng, q < nrhs, c < inner; in != out.
  * Partial dot products / PCG scalars are the caller's (all-reduced over ranks). */
-enum { HGP_SLAB_FWD = 0, HGP_SLAB_CONV = 1, HGP_SLAB_INV = 2 };
+enum { HGP_SLAB_FWD = 0, HGP_SLAB_CONV = 1, HGP_SLAB_INV = 2, HGP_SLAB_CONV_A2A = 3 };
 int hgp_slab_info(const hgp_plan* plan, int op, int64_t* ngroups, int64_t* inner);
 int hgp_slab_pass(hgp_plan* plan, int op, int stage, const void* in, void* out, int64_t nrhs,
                   int64_t nrows, int64_t g0, int64_t ng);

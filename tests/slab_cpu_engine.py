@@ -55,6 +55,36 @@ class CpuSlabEngine:
         Y = np.fft.ifft(F * s, axis=2)[:, :, :outs[0], :]
         lines[:, :, :outs[0], :] = torch.from_numpy(np.ascontiguousarray(Y))
 
+    @staticmethod
+    def _blocks(total, ws):
+        """The balanced row split of hipgp_amd.slab.split, as (start, count) per rank."""
+        base, rem = divmod(total, ws)
+        out, a = [], 0
+        for r in range(ws):
+            c = base + (1 if r < rem else 0)
+            out.append((a, c))
+            a += c
+        return out
+
+    def conv_a2a(self, op, recv, send, g0, ng, nrhs, ws):
+        """HGP_SLAB_CONV_A2A: lines read from the receive buffer's rank blocks
+        [r][g][q][i - a_r][c], results written to the send buffer's [r][g][q][o - b_r][c]."""
+        ins, outs = self._io(op)
+        _, inner = self.geometry(op)
+        lines = torch.zeros((ng, nrhs, max(ins[0], outs[0]), inner), dtype=self.cdtype)
+        R = recv.cpu()
+        off = 0
+        for a, c in self._blocks(ins[0], ws):
+            n = ng * nrhs * c * inner
+            lines[:, :, a:a + c, :] = R[off:off + n].view(ng, nrhs, c, inner)
+            off += n
+        self.conv(op, lines, g0, ng, nrhs)
+        off = 0
+        for b, c in self._blocks(outs[0], ws):
+            n = ng * nrhs * c * inner
+            send[off:off + n] = lines[:, :, b:b + c, :].reshape(-1).to(send.device)
+            off += n
+
     def inv(self, op, E, nrows, y):
         _, outs = self._io(op)
         A = E.cpu().numpy()
