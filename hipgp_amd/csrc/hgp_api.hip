@@ -106,6 +106,10 @@ struct hgp_plan {
   // R / R^T spectrum real (the filter embedded evenly: L_R >= 2n - 1 on every axis, d >= 2):
   // real-spectrum conv passes instead of complex ones, half the spectrum bytes
   bool r_real = false;
+  // fp64 plans whose L_R lines exceed one CU's LDS (L_R / 2 > 8192): R / R^T on the full fp64
+  // grid (run_op_grid: fwd_grid_f64's radix-2 step), spectrum in the transforms' stored order
+  bool grid_r = false;
+  DevBuf specRg, gridA, gridB;
   double clamp_min = 1e-6;                // of the last set_column (the clamp's gradient mask)
   DevBuf nclamp;
   // scratch
@@ -156,7 +160,7 @@ struct hgp_plan {
       twK[a].release(); twR[a].release(); tw64K[a].release(); tw64R[a].release(); tw64Rh[a].release();
       bsPre[a].release(); bsPost[a].release(); bsFilt[a].release();
     }
-    DevBuf* bufs[] = {&specK, &specI, &specR, &Dm3, &nclamp, &ws1, &ws2, &set1, &set2, &setM1, &setM2, &setC,
+    DevBuf* bufs[] = {&specK, &specI, &specR, &specRg, &gridA, &gridB, &Dm3, &nclamp, &ws1, &ws2, &set1, &set2, &setM1, &setM2, &setC,
                       &r, &z, &p, &Ap, &part_op, &part_u, &part_f, &scal, &flags, &bT, &xT};
     for (DevBuf* b : bufs) b->release();
     for (int i = 0; i < 3; ++i) {
@@ -168,6 +172,10 @@ struct hgp_plan {
 };
 
 namespace {
+
+#ifndef HGP_WS3_DEFAULT
+#define HGP_WS3_DEFAULT ((int64_t)4 << 30)   // 3-D operators' default workspace budget (bytes)
+#endif
 
 // op geometry: per-axis input/output lengths and transform length
 struct OpGeom {
@@ -278,10 +286,55 @@ using MidFn = std::function<void(int64_t, int, hipStream_t)>;
 // pass of the sequence (profiling).  2-D only: `spart` receives the column pass's spectral
 // dots <x, op x> per (RHS, compact column) [q][L_1/2 + 1]; `epi` replaces the output store by
 // the fused PCG update, `mid` runs between the column pass and the row-inverse pass.
+int fwd_grid_f64(hgp_plan* P, const int64_t* L, const DevBuf* tw64, double2* a, double2* b, double2** result);
+
+// R / R^T of a grid_r plan, one RHS at a time on the full fp64 L_R grid:
+// y = crop(IFFT(S' FFT(pad x))), S' = S (R^T) or conj(S) (R), the inverse as conj(FFT(conj Y)) / N.
+// Exact like the pass route (same spectrum, fp64 throughout); memory 2 prod(L_R) complex fp64.
+template <typename T>
+int run_op_grid(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs) {
+  hipStream_t s = P->stream;
+  const int d = P->d;
+  const int64_t N = P->prodLR;
+  HGP_TRY(P->gridA.ensure((size_t)N * sizeof(double2)));
+  HGP_TRY(P->gridB.ensure((size_t)N * sizeof(double2)));
+  double2* A = reinterpret_cast<double2*>(P->gridA.ptr);
+  double2* B = reinterpret_cast<double2*>(P->gridB.ptr);
+  GridDims gi, go;
+  gi.d = go.d = d;
+  int64_t inM = 1, outM = 1;
+  for (int a = 0; a < 3; ++a) {
+    gi.L[a] = go.L[a] = P->LR[a];
+    gi.n[a] = go.n[a] = P->n[a];
+    gi.m[a] = (op == HGP_OP_R) ? P->n[a] : P->m[a];
+    go.m[a] = (op == HGP_OP_RT) ? P->n[a] : P->m[a];
+    if (a < d) { inM *= gi.m[a]; outM *= go.m[a]; }
+  }
+  const double2* S = reinterpret_cast<const double2*>(P->specRg.ptr);
+  const size_t es = P->esz;
+  for (int64_t q = 0; q < nrhs; ++q) {
+    grid_embed(P->dtype, static_cast<const char*>(x) + (size_t)(q * inM) * es, gi, N, A, s);
+    double2* F = nullptr;
+    HGP_TRY(fwd_grid_f64(P, P->LR, P->tw64R, A, B, &F));
+    double2* other = (F == A) ? B : A;
+    grid_mul_unperm(F, S, gi, N, op == HGP_OP_R ? 1 : 0, other, s);
+    double2* Z = nullptr;
+    HGP_TRY(fwd_grid_f64(P, P->LR, P->tw64R, other, F, &Z));
+    grid_crop(P->dtype, Z, go, outM, static_cast<char*>(y) + (size_t)(q * outM) * es, s);
+  }
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
 template <typename T>
 int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void* dotv, void* partial,
            const int* done, int only_pass = -1, void* spart = nullptr, const RowEpi* epi = nullptr,
            const MidFn* mid = nullptr) {
+  if (P->grid_r && (op == HGP_OP_R || op == HGP_OP_RT)) {
+    if (dotv != nullptr || partial != nullptr || spart != nullptr || epi != nullptr || mid != nullptr || only_pass >= 0)
+      return fail(HGP_E_UNSUPPORTED, "internal: the full-grid R / R^T route has no fused dot or pass split");
+    return run_op_grid<T>(P, op, x, y, nrhs);
+  }
   const OpGeom g = op_geom(P, op);
   const int d = P->d;
   const int conv_mode = g.spec_kind == SPEC_REAL ? PASS_CONV : PASS_CONVC;
@@ -325,7 +378,10 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
   int64_t Qc = nrhs;
   if (B1 + B2 > 0) {
     const int64_t per = (B1 + B2) * (int64_t)cs;
-    Qc = std::max<int64_t>(1, std::min<int64_t>((nrhs + NS - 1) / NS, P->ws_budget / (per * NS)));
+    // 3-D: a larger default budget, so the axis-0 pass's spectrum lines (C5 R^T: 0.9 GB) are
+    // fetched once per chunk of several RHS instead of once per RHS
+    const int64_t budget = (d == 3 && !P->ws_explicit) ? std::max<int64_t>(P->ws_budget, HGP_WS3_DEFAULT) : P->ws_budget;
+    Qc = std::max<int64_t>(1, std::min<int64_t>((nrhs + NS - 1) / NS, budget / (per * NS)));
     // Infinity-Cache-resident chunks: where 8 RHS of a 2-D intermediate fit in ~72 MiB, each
     // stream works on 8 RHS at a time, so the intermediate a column pass writes is still in the
     // 256 MiB Infinity Cache when the row-inverse pass reads it (C2: row inverse 4.2 -> 5.0 TB/s,
@@ -428,7 +484,14 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
       }
       if (G2 > 1) {     // lines (column group, RHS, column in group): ceil(Rn / G2) G2 per RHS
         Bd.grp = G2;
-        HGP_TRY(run((int)(g.L[0] / 2), conv_mode, LAY_CONTIG_G, Bd, (int64_t)qn * ((H1 + G2) / G2) * G2));
+        // G2 position-fast blocks per group (LAY_CONTIG_G).  HGP_GRP_BLOCKS=1: one block per
+        // (group, RHS) with the columns interleaved over its threads (LAY_GRP*) -- coalesced
+        // 512-B accesses, but measured slower (C4 CONV 2.97 -> 3.85 ms, C3 0.765 -> 0.82 ms:
+        // 16-wave blocks / interleaved exchange images, profiles/r3_grouped_passtime.txt)
+        const int glay = G2 == 2 ? LAY_GRP2 : G2 == 4 ? LAY_GRP4 : -1;
+        static const bool grp_on = [] { const char* e = std::getenv("HGP_GRP_BLOCKS"); return e && std::atoi(e) == 1; }();
+        const bool use_grp = glay >= 0 && grp_on && pass_geom<T>((int)(g.L[0] / 2), glay).C == G2;
+        HGP_TRY(run((int)(g.L[0] / 2), conv_mode, use_grp ? glay : LAY_CONTIG_G, Bd, (int64_t)qn * ((H1 + G2) / G2) * G2));
       } else {
         HGP_TRY(run((int)(g.L[0] / 2), conv_mode, LAY_CONTIG, Bd, (int64_t)qn * Bd.Rn));
       }
@@ -789,6 +852,10 @@ int set_column_t(hgp_plan* P, const void* column, double jitter, double clamp_mi
     embed_R(sv, g1, gd, s);
     HGP_TRY(fwd_grid_f64(P, P->LR, P->tw64R, g1, g2, &F));
     extract_cplx<T>(F, P->specR.ptr, nR, LRl, SR, compact, 1.0 / (double)P->prodLR, s);
+    if (P->grid_r) {
+      HGP_TRY(P->specRg.ensure((size_t)P->prodLR * sizeof(double2)));
+      scale_copy(F, reinterpret_cast<double2*>(P->specRg.ptr), P->prodLR, 1.0 / (double)P->prodLR, s);
+    }
   } else if (!long_r) {
     // the R filter is real: real row-pair transform of the last axis, compact columns only after
     embed_R_real(sv, reinterpret_cast<double*>(g1), gd, sym ? 1 : 0, s);
@@ -805,6 +872,10 @@ int set_column_t(hgp_plan* P, const void* column, double jitter, double clamp_mi
     HGP_TRY(fwd_grid_f64(P, P->LR, P->tw64R, g1, g2, &F));
     extract_t<T>(F, P->specR.ptr, nullptr, P->LR[0], d == 3 ? P->LR[1] : 1, LRl / 2, LRl, 0,
                  1.0 / (double)P->prodLR, s);
+    if (P->grid_r) {
+      HGP_TRY(P->specRg.ensure((size_t)P->prodLR * sizeof(double2)));
+      scale_copy(F, reinterpret_cast<double2*>(P->specRg.ptr), P->prodLR, 1.0 / (double)P->prodLR, s);
+    }
   }
   HIP_TRY(hipGetLastError());
   P->have_spec = true;
@@ -833,6 +904,8 @@ SlabGeom slab_geom(const hgp_plan* P, int op) {
 template <typename T>
 int slab_pass_t(hgp_plan* P, int op, int stage, const void* in, void* out, int64_t nrhs, int64_t nrows, int64_t g0,
                 int64_t ng) {
+  if (P->grid_r && (op == HGP_OP_R || op == HGP_OP_RT))
+    return fail(HGP_E_UNSUPPORTED, "grid-block sharding of R / R^T with fp64 lines of more than 16384 points");
   const OpGeom g = op_geom(P, op);
   const int d = P->d;
   const SlabGeom sg = slab_geom(P, op);
@@ -1217,11 +1290,12 @@ int hgp_plan_create(int device, int ndim, const int64_t* m, int dtype, int64_t m
     // L_R / 2 = 16384 (axes of 4098..8192 points): fp32 operator passes hold one such line per
     // block; fp64 lines of 16384 points exceed one CU's LDS (the set-up's fp64 transforms of
     // them take fft_lines_f64's radix-2 step)
-    if (P->LR[a] / 2 > 16384 || P->LK[a] / 2 > 8192 || (dtype == HGP_F64 && P->LR[a] / 2 > 8192)) {
+    if (P->LR[a] / 2 > 16384 || P->LK[a] / 2 > 8192) {
       delete P;
-      return fail(HGP_E_UNSUPPORTED, dtype == HGP_F64 ? "fp64 plans support grid axes of up to 4097 points (fp32: 8192)"
-                                                      : "grid axis longer than 8192 points is not supported");
+      return fail(HGP_E_UNSUPPORTED, "grid axis longer than 8192 points is not supported");
     }
+    // fp64 lines of L_R / 2 > 8192 points exceed one CU's LDS: R / R^T take the full-grid route
+    if (dtype == HGP_F64 && P->LR[a] / 2 > 8192) P->grid_r = true;
     P->M *= P->m[a];
     P->Mp *= P->n[a];
     P->prodLK *= P->LK[a];
@@ -1717,7 +1791,7 @@ int hgp_slab_pass(hgp_plan* plan, int op, int stage, const void* in, void* out, 
   if (!plan->have_spec) return fail(HGP_E_STATE, "hgp_plan_set_column has not been called");
   if (op < HGP_OP_K || op > HGP_OP_R) return fail(HGP_E_ARG, "bad op");
   if (plan->d < 2) return fail(HGP_E_UNSUPPORTED, "slab sharding needs a 2-D or 3-D grid");
-  if (stage < HGP_SLAB_FWD || stage > HGP_SLAB_INV) return fail(HGP_E_ARG, "bad slab stage");
+  if (stage < HGP_SLAB_FWD || stage > HGP_SLAB_CONV_A2A) return fail(HGP_E_ARG, "bad slab stage");
   if (nrhs < 0 || (nrhs > 0 && (in == nullptr || out == nullptr))) return fail(HGP_E_ARG, "bad in/out/nrhs");
   if (stage != HGP_SLAB_CONV && in == out) return fail(HGP_E_ARG, "in and out must not alias (row stages)");
   if (nrhs == 0) return 0;
@@ -1767,7 +1841,7 @@ int hgp_plan_trim(hgp_plan* plan) {
     if (plan->side[i]) HIP_TRY(hipStreamSynchronize(plan->side[i]));
   DevBuf* bufs[] = {&plan->ws1, &plan->ws2, &plan->set1, &plan->set2, &plan->setM1, &plan->setM2, &plan->setC,
                     &plan->r, &plan->z, &plan->p, &plan->Ap, &plan->part_op, &plan->part_u, &plan->part_f,
-                    &plan->scal, &plan->bT, &plan->xT};
+                    &plan->scal, &plan->bT, &plan->xT, &plan->gridA, &plan->gridB};
   for (DevBuf* b : bufs) b->release();
   plan->drop_graph();                               // its kernels addressed the freed workspaces
   plan->last_apply = hgp_plan::ApplyKey();

@@ -269,6 +269,59 @@ __global__ void k_gather_flat(const double2* __restrict__ F, LGeo G, int64_t M, 
   out[i] = (T)(s * invL);
 }
 
+
+// ---- fp64 full-grid route of R / R^T (plans whose L_R lines exceed one CU's LDS in fp64) ------
+// y = crop(IFFT(S' . FFT(pad x))) with the forward transforms of fwd_grid_f64 (stored order,
+// pos_of per axis) and the inverse as conj(FFT(conj Y)) / N (the 1/N is in the stored S).
+// z[f] = x at natural grid point f when inside the input extents (G.m), else 0
+template <typename T>
+__global__ void k_grid_embed(const T* __restrict__ x, LGeo G, int64_t prodL, double2* __restrict__ z) {
+  const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= prodL) return;
+  int c[3];
+  decodeL(f, G, c);
+  bool in = true;
+  int64_t ix = 0;
+  for (int a = 0; a < G.d; ++a) {
+    in = in && c[a] < G.m[a];
+    ix = ix * G.m[a] + c[a];
+  }
+  z[f] = make_double2(in ? (double)x[ix] : 0.0, 0.0);
+}
+
+// out[f] (natural order) = conj(F[pos(f)] S'[pos(f)]), S' = S or conj(S)
+__global__ void k_grid_mul_unperm(const double2* __restrict__ F, const double2* __restrict__ S, LGeo G,
+                                  int64_t prodL, int conj_spec, double2* __restrict__ out) {
+  const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= prodL) return;
+  int c[3];
+  decodeL(f, G, c);
+  int64_t p = 0;
+  for (int a = 0; a < G.d; ++a) p = p * G.L[a] + pos_of(c[a], G.L[a]);
+  const double2 a = F[p];
+  double2 w = S[p];
+  if (conj_spec) w.y = -w.y;
+  out[f] = make_double2(a.x * w.x - a.y * w.y, -(a.x * w.y + a.y * w.x));
+}
+
+// y[j] (j over the output extents G.m) = Re Z[pos(j)]
+template <typename T>
+__global__ void k_grid_crop(const double2* __restrict__ Z, LGeo G, int64_t outM, T* __restrict__ y) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= outM) return;
+  int c[3] = {0, 0, 0};
+  int64_t r = j;
+  for (int a = G.d - 1; a >= 0; --a) { c[a] = (int)(r % G.m[a]); r /= G.m[a]; }
+  int64_t p = 0;
+  for (int a = 0; a < G.d; ++a) p = p * G.L[a] + pos_of(c[a], G.L[a]);
+  y[j] = (T)Z[p].x;
+}
+
+__global__ void k_scale_copy(const double2* __restrict__ a, double2* __restrict__ b, int64_t n, double sc) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) b[i] = make_double2(a[i].x * sc, a[i].y * sc);
+}
+
 LGeo make_lgeo(const GridDims& g) {
   LGeo G;
   G.d = g.d;
@@ -330,6 +383,27 @@ void gather_flat(int dtype, const double2* F, const GridDims& gd, int64_t M, dou
   const LGeo G = make_lgeo(gd);
   if (dtype == 1) k_gather_flat<double><<<nblk(M, 256), 256, 0, s>>>(F, G, M, invL, (double*)out);
   else k_gather_flat<float><<<nblk(M, 256), 256, 0, s>>>(F, G, M, invL, (float*)out);
+}
+
+void grid_embed(int dtype, const void* x, const GridDims& gd, int64_t prodL, double2* z, hipStream_t s) {
+  const LGeo G = make_lgeo(gd);
+  if (dtype == 1) k_grid_embed<double><<<nblk(prodL, 256), 256, 0, s>>>((const double*)x, G, prodL, z);
+  else k_grid_embed<float><<<nblk(prodL, 256), 256, 0, s>>>((const float*)x, G, prodL, z);
+}
+
+void grid_mul_unperm(const double2* F, const double2* S, const GridDims& gd, int64_t prodL, int conj_spec,
+                     double2* out, hipStream_t s) {
+  k_grid_mul_unperm<<<nblk(prodL, 256), 256, 0, s>>>(F, S, make_lgeo(gd), prodL, conj_spec, out);
+}
+
+void grid_crop(int dtype, const double2* Z, const GridDims& gd, int64_t outM, void* y, hipStream_t s) {
+  const LGeo G = make_lgeo(gd);
+  if (dtype == 1) k_grid_crop<double><<<nblk(outM, 256), 256, 0, s>>>(Z, G, outM, (double*)y);
+  else k_grid_crop<float><<<nblk(outM, 256), 256, 0, s>>>(Z, G, outM, (float*)y);
+}
+
+void scale_copy(const double2* a, double2* b, int64_t n, double sc, hipStream_t s) {
+  k_scale_copy<<<nblk(n, 256), 256, 0, s>>>(a, b, n, sc);
 }
 
 }  // namespace hgp

@@ -98,6 +98,12 @@ void pack_pair(int dtype, const void* v, const void* h, int h_periodic, const Gr
                hipStream_t s);
 void xspec_acc(const double2* Z, double2* S, const GridDims& gd, int64_t prodL, int first, hipStream_t s);
 void conj_inplace(double2* S, int64_t n, hipStream_t s);
+// fp64 full-grid route of R / R^T (hgp_grad.hip): gd.m = the input / output extents, gd.L = L_R
+void grid_embed(int dtype, const void* x, const GridDims& gd, int64_t prodL, double2* z, hipStream_t s);
+void grid_mul_unperm(const double2* F, const double2* S, const GridDims& gd, int64_t prodL, int conj_spec,
+                     double2* out, hipStream_t s);
+void grid_crop(int dtype, const double2* Z, const GridDims& gd, int64_t outM, void* y, hipStream_t s);
+void scale_copy(const double2* a, double2* b, int64_t n, double sc, hipStream_t s);
 void gather_n(const double2* F, const GridDims& gd, int h_periodic, int64_t Mp, double invL, double* X, hipStream_t s);
 void gather_flat(int dtype, const double2* F, const GridDims& gd, int64_t M, double invL, void* out, hipStream_t s);
 // CG

@@ -42,6 +42,11 @@
 //                 NL = Rn Q.  _C: position-fast lines (d = 2, inner = 1); _S: C adjacent c lines
 //                 per block as LAY_STRIDED (d = 3, In lines, inner = in.p_stride).  Input split
 //                 over in.len rows, output split over out.len rows.
+//   LAY_GRP2 / LAY_GRP4: the grouped-column intermediate as LAY_CONTIG_G, but a block holds the
+//                 G = 2 / 4 columns of one group of one RHS with threads column-fast (the strided
+//                 mapping, C = G): every load / store instruction of a wave covers one contiguous
+//                 64 / G-position run of the group (512 B), instead of G blocks each taking one
+//                 column out of every 8 G bytes.
 #pragma once
 #include <type_traits>
 
@@ -69,13 +74,19 @@
 #ifndef HGP_MINW_CONTIG
 #define HGP_MINW_CONTIG 4
 #endif
+#ifndef HGP_MINW_CONTIG_LONG
+#define HGP_MINW_CONTIG_LONG HGP_MINW_CONTIG   // lines of H >= 2048 (multi-wave, two-level twiddles)
+#endif
 
 namespace hgp {
 
 enum { PASS_FWD = 0, PASS_INV = 1, PASS_CONV = 2, PASS_CONVC = 3 };   // CONV: real spectrum, CONVC: complex
-enum { LAY_STRIDED = 0, LAY_CONTIG = 1, LAY_RP = 2, LAY_R1 = 3, LAY_CONTIG_G = 4, LAY_SEG_C = 5, LAY_SEG_S = 6 };
+enum { LAY_STRIDED = 0, LAY_CONTIG = 1, LAY_RP = 2, LAY_R1 = 3, LAY_CONTIG_G = 4, LAY_SEG_C = 5, LAY_SEG_S = 6,
+       LAY_GRP2 = 7, LAY_GRP4 = 8 };
+// columns per block of the interleaved grouped layouts (0: not one)
+constexpr int lay_grp(int lay) { return lay == LAY_GRP2 ? 2 : lay == LAY_GRP4 ? 4 : 0; }
 // strided thread mapping (C adjacent lines, threads line-fast) vs position-fast lines
-constexpr bool lay_smap(int lay) { return lay == LAY_STRIDED || lay == LAY_SEG_S; }
+constexpr bool lay_smap(int lay) { return lay == LAY_STRIDED || lay == LAY_SEG_S || lay_grp(lay) > 0; }
 enum { SPEC_REAL = 0, SPEC_CPLX = 1, SPEC_CPLX_CONJ = 2 };
 // row-inverse epilogue (hgp_rows.hpp): EPI_XR x/r update (unpreconditioned PCG); with the
 // preconditioner the x update is deferred to the C^-1 pass: EPI_R r update, EPI_XP x and p
@@ -155,7 +166,7 @@ template <typename T, int H, int LAY> struct PassCfg {
     while (c > 1 && (c * TT > 1024 || lds_bytes_for(c) > LDS_CAP / 2)) c >>= 1;
     return c;
   }
-  static constexpr int C = lay_smap(LAY) ? c_strided() : c_contig();
+  static constexpr int C = lay_grp(LAY) ? lay_grp(LAY) : lay_smap(LAY) ? c_strided() : c_contig();
   // position-fast layouts keep each line inside one wavefront when TT <= 64: exchanges then
   // need no block barrier (hgp_fft.hpp xsync)
   static constexpr bool WAVE = !lay_smap(LAY) && TT <= 64;
@@ -167,8 +178,12 @@ template <typename T, int H, int LAY> struct PassCfg {
   static constexpr int BLOCKS_BY_LDS = LDS_CAP / LDS;
   static constexpr int MINW_LDS = (BLOCKS_BY_LDS * WAVES_PER_BLOCK) / 4;
   static constexpr int MINW_AUTO = MINW_LDS < 1 ? 1 : (MINW_LDS > 4 ? 4 : MINW_LDS);
-  static constexpr int MINW_SET = lay_smap(LAY) ? (TT >= 16 ? HGP_MINW_STRIDED : HGP_MINW_STRIDED_SMALL)
-                                 : (LAY == LAY_CONTIG || LAY == LAY_CONTIG_G) ? HGP_MINW_CONTIG : HGP_MINW_ROW;
+  static constexpr int MINW_CL = H >= 2048 ? HGP_MINW_CONTIG_LONG : HGP_MINW_CONTIG;
+  // a block's waves must fit the SIMDs' share at once: >= WAVES_PER_BLOCK / 4 waves per SIMD
+  static constexpr int MINW_BLK = (WAVES_PER_BLOCK + 3) / 4;
+  static constexpr int MINW_SET = lay_grp(LAY) ? (MINW_CL > MINW_BLK ? MINW_CL : MINW_BLK)
+                                 : lay_smap(LAY) ? (TT >= 16 ? HGP_MINW_STRIDED : HGP_MINW_STRIDED_SMALL)
+                                 : (LAY == LAY_CONTIG || LAY == LAY_CONTIG_G) ? MINW_CL : HGP_MINW_ROW;
   static constexpr int MINW = MINW_SET > 0 ? MINW_SET : MINW_AUTO;
 };
 
@@ -258,9 +273,22 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
   // adds a 32-bit element offset lc + p*stride to uniform base pointers, so no 64-bit address
   // is held per position across the FFT.
   int q, r, i, i0 = 0, lc = 0;
-  int64_t gbase = 0;          // LAY_CONTIG_G: element offset of the line in its RHS's slab
+  int64_t gbase = 0;          // LAY_CONTIG_G / GRP: element offset of the line's group in its RHS's slab
   bool valid;
-  if constexpr (SMAP) {
+  constexpr bool GRP = lay_grp(LAY) > 0;
+  if constexpr (GRP) {
+    // logical block = (column group, RHS) with the RHS fastest: the XCD remap keeps every RHS of
+    // a group (one set of spectrum lines) on one XCD
+    const int lb = xcd_remap(blockIdx.x, gridDim.x);
+    const int cg = lb / d.Q;
+    q = lb - cg * d.Q;
+    i0 = cg * C;                    // the group's first column
+    r = i0 + l;
+    i = 0;
+    valid = r < d.Rn;               // the last group's padding columns: computed, never stored
+    lc = l;
+    gbase = (int64_t)i0 * d.in.r_stride;
+  } else if constexpr (SMAP) {
     // logical block = (q, g) with g fastest; the XCD remap keeps consecutive g (adjacent
     // column groups) of one RHS on one XCD.
     const int lb = xcd_remap(blockIdx.x, gridDim.x);
@@ -322,7 +350,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
     in_c = reinterpret_cast<const C2<T>*>(d.in.ptr);   // positions by seg_off (the rank blocks)
   } else if constexpr (LAY == LAY_STRIDED) {
     in_c = reinterpret_cast<const C2<T>*>(d.in.ptr) + (int64_t)q * d.in.q_stride + (int64_t)r * d.in.r_stride + i0;
-  } else if constexpr (LAY == LAY_CONTIG_G) {
+  } else if constexpr (LAY == LAY_CONTIG_G || GRP) {
     in_c = reinterpret_cast<const C2<T>*>(d.in.ptr) + (int64_t)q * d.in.q_stride + gbase;
   } else {
     in_c = reinterpret_cast<const C2<T>*>(d.in.ptr) + (int64_t)q * d.in.q_stride + (int64_t)r * d.in.r_stride;
@@ -341,14 +369,14 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
     out_c = reinterpret_cast<C2<T>*>(d.out.ptr);
   } else if constexpr (LAY == LAY_STRIDED) {
     out_c = reinterpret_cast<C2<T>*>(d.out.ptr) + (int64_t)q * d.out.q_stride + (int64_t)r * d.out.r_stride + i0;
-  } else if constexpr (LAY == LAY_CONTIG_G) {
+  } else if constexpr (LAY == LAY_CONTIG_G || GRP) {
     out_c = reinterpret_cast<C2<T>*>(d.out.ptr) + (int64_t)q * d.out.q_stride + gbase;
   } else {
     out_c = reinterpret_cast<C2<T>*>(d.out.ptr) + (int64_t)q * d.out.q_stride + (int64_t)r * d.out.r_stride;
   }
   // element offset of position p in this lane's line (32-bit: one RHS slab < 2^31 elements)
-  const int ips = (LAY == LAY_STRIDED) ? (int)d.in.p_stride : (LAY == LAY_CONTIG_G) ? d.grp : 1;
-  const int ops = (LAY == LAY_STRIDED) ? (int)d.out.p_stride : (LAY == LAY_CONTIG_G) ? d.grp : 1;
+  const int ips = (LAY == LAY_STRIDED) ? (int)d.in.p_stride : (LAY == LAY_CONTIG_G) ? d.grp : GRP ? C : 1;
+  const int ops = (LAY == LAY_STRIDED) ? (int)d.out.p_stride : (LAY == LAY_CONTIG_G) ? d.grp : GRP ? C : 1;
   // rank-block layouts: element offset of row p of this lane's line (balanced split of n rows)
   const int s_inner = (LAY == LAY_SEG_S) ? (int)d.in.p_stride : 1;   // element pitch of c
   const int64_t s_line = SEG ? (int64_t)r * d.Q + q : 0;
@@ -365,11 +393,11 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
   using Off = std::conditional_t<SEG, int64_t, int>;   // 32-bit lane offsets on the fast layouts
   auto in_at = [&](int p) -> Off {
     if constexpr (SEG) return seg_off(p, d.in.len);
-    else return (LAY == LAY_STRIDED) ? lc + p * ips : (LAY == LAY_CONTIG_G) ? p * ips : p;
+    else return (LAY == LAY_STRIDED || GRP) ? lc + p * ips : (LAY == LAY_CONTIG_G) ? p * ips : p;
   };
   auto out_at = [&](int p) -> Off {
     if constexpr (SEG) return seg_off(p, d.out.len);
-    else return (LAY == LAY_STRIDED) ? lc + p * ops : (LAY == LAY_CONTIG_G) ? p * ops : p;
+    else return (LAY == LAY_STRIDED || GRP) ? lc + p * ops : (LAY == LAY_CONTIG_G) ? p * ops : p;
   };
 
   // Loads are unconditional on clamped (always in-bounds) addresses and zeroed afterwards:
@@ -420,9 +448,14 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
   const T* sb = nullptr;
   int so = 0, sp = 0;
   if constexpr (MODE == PASS_CONV) {
-    sb = reinterpret_cast<const T*>(d.spec) + (int64_t)i0 * d.spec_i + (int64_t)r * d.spec_r;
     sp = (int)d.spec_p;
-    so = (SMAP ? lc * (int)d.spec_i : 0) + t * sp;
+    if constexpr (GRP) {            // columns i0 + lc (the padding columns read column i0's)
+      sb = reinterpret_cast<const T*>(d.spec) + (int64_t)i0 * d.spec_r;
+      so = (valid ? lc : 0) * (int)d.spec_r + t * sp;
+    } else {
+      sb = reinterpret_cast<const T*>(d.spec) + (int64_t)i0 * d.spec_i + (int64_t)r * d.spec_r;
+      so = (SMAP ? lc * (int)d.spec_i : 0) + t * sp;
+    }
   }
   // contiguous lines of whole waves: wave-uniform line bases -> raw buffer accesses (32-bit
   // lane offsets; the zero padding beyond in_len and the crop beyond out_len come from the
@@ -537,9 +570,10 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
     } else if constexpr (MODE == PASS_CONVC) {
       fft_line2<T, H, P, -1, LSTRIDE, Cfg::WAVE>(va, vb, lds, lbase, t, tab);
       // complex spectrum at (i, r, kperm): block-uniform base + 32-bit lane offset
-      const C2<T>* sbase = reinterpret_cast<const C2<T>*>(d.spec) + (int64_t)i0 * d.spec_i + (int64_t)r * d.spec_r;
+      const C2<T>* sbase = reinterpret_cast<const C2<T>*>(d.spec) +
+                           (GRP ? (int64_t)i0 * d.spec_r : (int64_t)i0 * d.spec_i + (int64_t)r * d.spec_r);
       const int sp = (int)d.spec_p;
-      const int so0 = (SMAP ? lc * (int)d.spec_i : 0) + t * sp;
+      const int so0 = (GRP ? (valid ? lc : 0) * (int)d.spec_r : SMAP ? lc * (int)d.spec_i : 0) + t * sp;
 #pragma unroll
       for (int k = 0; k < P; ++k) {
         const C2<T> s0 = sbase[so0 + TT * k * sp];

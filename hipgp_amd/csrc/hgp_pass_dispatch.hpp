@@ -23,6 +23,21 @@ static hipError_t launch_one(const PassDesc& d, int64_t nblocks, hipStream_t s) 
   return hipGetLastError();
 }
 
+// the interleaved grouped layouts exist where one group's G lines fit a block
+template <typename T, int H, int LAY>
+constexpr bool grp_ok() {
+  return std::is_same<T, float>::value && PassCfg<T, H, LAY>::THREADS <= 1024 && PassCfg<T, H, LAY>::LDS <= LDS_CAP;
+}
+
+template <typename T, int H, int MODE>
+static hipError_t launch_grp(int lay, const PassDesc& d, int64_t nblocks, hipStream_t s) {
+  if constexpr (grp_ok<T, H, LAY_GRP2>())
+    if (lay == LAY_GRP2) return launch_one<T, H, MODE, LAY_GRP2>(d, nblocks, s);
+  if constexpr (grp_ok<T, H, LAY_GRP4>())
+    if (lay == LAY_GRP4) return launch_one<T, H, MODE, LAY_GRP4>(d, nblocks, s);
+  return hipErrorInvalidValue;
+}
+
 template <typename T, int H>
 static hipError_t launch_h(int mode, int lay, const PassDesc& d, int64_t nblocks, hipStream_t s) {
   if (mode == PASS_FWD) {
@@ -41,6 +56,7 @@ static hipError_t launch_h(int mode, int lay, const PassDesc& d, int64_t nblocks
       if (lay == LAY_CONTIG_G) return launch_one<T, H, PASS_CONV, LAY_CONTIG_G>(d, nblocks, s);
     if (lay == LAY_SEG_C) return launch_one<T, H, PASS_CONV, LAY_SEG_C>(d, nblocks, s);
     if (lay == LAY_SEG_S) return launch_one<T, H, PASS_CONV, LAY_SEG_S>(d, nblocks, s);
+    if (lay_grp(lay)) return launch_grp<T, H, PASS_CONV>(lay, d, nblocks, s);
   } else if (mode == PASS_CONVC) {
     if (lay == LAY_STRIDED) return launch_one<T, H, PASS_CONVC, LAY_STRIDED>(d, nblocks, s);
     if (lay == LAY_CONTIG) return launch_one<T, H, PASS_CONVC, LAY_CONTIG>(d, nblocks, s);
@@ -49,6 +65,7 @@ static hipError_t launch_h(int mode, int lay, const PassDesc& d, int64_t nblocks
       if (lay == LAY_CONTIG_G) return launch_one<T, H, PASS_CONVC, LAY_CONTIG_G>(d, nblocks, s);
     if (lay == LAY_SEG_C) return launch_one<T, H, PASS_CONVC, LAY_SEG_C>(d, nblocks, s);
     if (lay == LAY_SEG_S) return launch_one<T, H, PASS_CONVC, LAY_SEG_S>(d, nblocks, s);
+    if (lay_grp(lay)) return launch_grp<T, H, PASS_CONVC>(lay, d, nblocks, s);
   }
   return hipErrorInvalidValue;
 }
@@ -63,6 +80,8 @@ static PassGeom geom_h(int lay) {
   if (lay == LAY_STRIDED || lay == LAY_SEG_S) return geom_one<T, H, LAY_STRIDED>();
   if (lay == LAY_CONTIG || lay == LAY_CONTIG_G || lay == LAY_SEG_C) return geom_one<T, H, LAY_CONTIG>();
   if (lay == LAY_RP) return geom_one<T, H, LAY_RP>();
+  if (lay == LAY_GRP2) return grp_ok<T, H, LAY_GRP2>() ? geom_one<T, H, LAY_GRP2>() : PassGeom{0, 0, 0};
+  if (lay == LAY_GRP4) return grp_ok<T, H, LAY_GRP4>() ? geom_one<T, H, LAY_GRP4>() : PassGeom{0, 0, 0};
   return geom_one<T, H, LAY_R1>();
 }
 

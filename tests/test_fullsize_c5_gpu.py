@@ -11,9 +11,10 @@ M' = 66 M) with the per-GPU batch of 25 right-hand sides (200 split over 8 GPUs)
 Grid as config 5 (x, y in [-.25, .25], z in [-.05, .05]), Matern-5/2.  Config 5's own
 hyper-parameters (sig2 .1, ell .1 = 50 x-spacings, nugget 1e-3) leave K so ill-conditioned that
 20 PCG iterations stay far from the solution (fp64 residual 1.8 |b| measured), so fp32 and fp64
-iterates differ chaotically there; these tests use ell = 0.01 (5 x-spacings, 13 z-spacings) and a
-nugget of 0.1 sig2, where 20 iterations converge and fp32 must track fp64 (as tests/test_large_gpu.py
-does for C3 / C4)."""
+iterates differ chaotically there; these tests use ell = 0.005 (2.5 x-spacings, 6 z-spacings) and
+a nugget of 0.5 sig2, where 20 iterations converge (oracle, one RHS: residual 5.2e-4; ell = 0.01
+with a 0.1 sig2 nugget leaves 0.35, ell = 0.005 with 0.1 sig2 0.028) and fp32 must track fp64 (as
+tests/test_large_gpu.py does for C3 / C4)."""
 import numpy as np
 import pytest
 import torch
@@ -28,7 +29,7 @@ def _grids(dt, device=DEV):
     return [torch.linspace(lo, hi, m, device=device, dtype=dt) for m, lo, hi in zip(DIMS, LO, HI)]
 
 
-SIG2, ELL, JIT = 0.1, 0.01, 0.01
+SIG2, ELL, JIT = 0.1, 0.005, 0.05
 
 
 def _tt(dt):
@@ -57,7 +58,7 @@ def test_solve_compute_kn_C5_B25():
     x64, r64, kn64 = out[torch.float64]
     x32, r32, kn32 = out[torch.float32]
     print("C5 residuals fp64", float(r64.max()), "fp32", float(r32.max()))
-    assert float(r64.max()) < 0.05
+    assert float(r64.max()) < 0.01
     assert float((r32 - r64).abs().max()) < 1e-3
     rel_x = float(((x32 - x64).norm(dim=1) / x64.norm(dim=1)).max())
     rel_kn = float(((kn32.double() - kn64).norm(dim=1) / kn64.norm(dim=1)).max())

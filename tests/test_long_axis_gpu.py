@@ -1,11 +1,13 @@
 """Grid axes longer than 4097 points (the reference has no length limit, `toeplitz_tensor.py:85-97`).
 
-An axis of m in 4098..8192 points needs L_R = 32768-point transforms for R / R^T: fp32 plans run
-them as one-line-per-block passes (H = 16384), and the fp64 set-up of every plan transforms
-the L_R grid with fft_lines_f64's radix-2 step (two 16384-point halves + k_r2_combine).  Here
-the fp32 operators and PCG of 1-D / 2-D / 3-D grids with such an axis (any position) are checked
-against the fp64 oracle of the same column; fp64 plans of those sizes are refused cleanly
-(one 16384-point fp64 line exceeds a CU's LDS), as are axes beyond 8192 points."""
+An axis of m in 4098..8192 points needs L_R >= 3m - 3 > 12288-point transforms for R / R^T:
+fp32 plans run them as one-line-per-block passes (H up to 16384), and the fp64 set-up of every
+plan transforms the L_R grid with fft_lines_f64's radix-2 step (two half-length transforms +
+k_r2_combine).  fp64 plans run K / C^-1 lines of up to 8192 points per half (one line per block)
+and R / R^T either as passes (L_R / 2 <= 8192: axes up to 5462 points with the 3 * 2^k or
+power-of-two L_R <= 16384) or, beyond that, on the full fp64 L_R grid (run_op_grid).  Here the
+operators and PCG of 1-D / 2-D / 3-D grids with such an axis (any position) are checked against
+the fp64 oracle of the same column, in both dtypes; axes beyond 8192 points are refused."""
 import numpy as np
 import pytest
 import torch
@@ -61,11 +63,46 @@ def test_long_axis_ops_and_pcg_fp32(case):
     assert float(np.abs(rr - kv).max() / np.abs(kv).max()) < 3e-5
 
 
+# fp64: pass route (L_R / 2 <= 8192) and full-grid R / R^T route (6000-point axes)
+CASES64 = {"1d_5000": (5000,), "2d_4200x12": (4200, 12), "2d_10x4500": (10, 4500), "3d_3x5x4300": (3, 5, 4300),
+           "2d_6000x10": (6000, 10), "3d_4x6000x3": (4, 6000, 3), "2d_8x8192": (8, 8192)}
+
+
+@pytest.mark.parametrize("case", sorted(CASES64))
+def test_long_axis_ops_and_pcg_fp64(case):
+    from hipgp_amd import _lib
+    from hipgp_amd.plan import ToeplitzPlan
+    dims = CASES64[case]
+    col = _column(dims)
+    O = zo.ToeplitzOracle(col, dims)
+    P = ToeplitzPlan(dims, torch.float64, DEV)
+    P.set_column(torch.tensor(col, device=DEV, dtype=torch.float64))
+    M, Mp = O.M, O.Mp
+    rs = np.random.RandomState(5)
+    v = rs.randn(2, M)
+    w = rs.randn(2, Mp)
+    for name, op, x, ref in (("K", _lib.OP_K, v, O.matmul_K(v)), ("Cinv", _lib.OP_CINV, v, O.matmul_Cinv(v)),
+                             ("RT", _lib.OP_RT, v, O.matmul_RT(v)), ("R", _lib.OP_R, w, O.matmul_R(w))):
+        got = P.apply(op, torch.tensor(x, device=DEV, dtype=torch.float64)).cpu().numpy()
+        assert got.shape == ref.shape, name
+        err = float(np.abs(got - ref).max() / np.abs(ref).max())
+        assert err < 1e-10, (name, err)
+    b = rs.randn(2, M)
+    x_ref = O.solve(b, do_precond=True, maxiter=10, tol=1e-30)
+    x = P.pcg(torch.tensor(b, device=DEV), 10, 1e-30, precond=True).cpu().numpy()
+    assert np.linalg.norm(x - x_ref) / np.linalg.norm(x_ref) < 1e-9
+    vt = torch.tensor(v, device=DEV)
+    rr = P.apply(_lib.OP_R, P.apply(_lib.OP_RT, vt)).cpu().numpy()
+    kv = O.matmul_K(v)
+    assert float(np.abs(rr - kv).max() / np.abs(kv).max()) < 1e-10
+
+
 def test_long_axis_refusals():
     from hipgp_amd import _lib
     from hipgp_amd.plan import ToeplitzPlan
-    with pytest.raises(_lib.HipgpError, match="fp64 plans support grid axes of up to 4097"):
-        ToeplitzPlan((4200, 12), torch.float64, DEV)
-    with pytest.raises(_lib.HipgpError, match="longer than 8192"):
-        ToeplitzPlan((8193,), torch.float32, DEV)
-    ToeplitzPlan((4097, 3), torch.float64, DEV)        # the fp64 limit itself is accepted
+    for dt in (torch.float32, torch.float64):
+        with pytest.raises(_lib.HipgpError, match="longer than 8192"):
+            ToeplitzPlan((8193,), dt, DEV)
+        with pytest.raises(_lib.HipgpError, match="longer than 8192"):
+            ToeplitzPlan((3, 8193), dt, DEV)
+    ToeplitzPlan((8192, 3), torch.float64, DEV)        # the limit itself is accepted in fp64 too

@@ -324,18 +324,23 @@ def test_long_lines_accuracy_and_repeatability(dims, dtype):
             assert rel_err(_np(P.apply(op, vt)), ref) < 1e-11, op
 
 
+@pytest.mark.parametrize("lr", ["pow2", "short"])
 @pytest.mark.parametrize("dims", [(700, 2100), (40, 4096)], ids=["700x2100", "40x4096"])
-def test_generic_2d_sequence_fp64(dims):
+def test_generic_2d_sequence_fp64(dims, lr, monkeypatch):
     """fp64 rows whose row-pair kernels do not fit one CU's LDS (R / R^T with L_R >= 16384 along
-    axis 1) run the generic 2-D sequence; against the oracle, and the fp64 PCG through it."""
+    axis 1: the power-of-two L_R, HGP_LR=pow2) run the generic 2-D sequence; against the oracle,
+    and the fp64 PCG through it.  "short": the plan's own choice (3 * 2^k or 2^k >= 3m - 3)."""
     from hipgp_amd import _lib
     from hipgp_amd.plan import ToeplitzPlan
     grids = [np.linspace(-1, 1, m) for m in dims]
     col = zo.toeplitz_column(grids, lambda x, y: zo.kernel_eval("matern", x, y, (1., .05), nu=1.5), 0.1)
     T = zo.ToeplitzOracle(col, dims)
+    if lr == "pow2":
+        monkeypatch.setenv("HGP_LR", "pow2")
     P = ToeplitzPlan(dims, torch.float64, DEV)
     P.set_column(torch.tensor(col, device=DEV))
-    assert P.L_R[1] >= 16384
+    if lr == "pow2":
+        assert P.L_R[1] >= 16384
     rs = np.random.RandomState(1)
     v = rs.randn(2, T.M)
     w = rs.randn(2, T.Mp)
