@@ -160,7 +160,8 @@ template <typename T, int H, int LAY> struct PassCfg {
     while (c > 1 && (c * TT > 1024 || lds_bytes_for(c) > LDS_CAP)) c >>= 1;
     return c;
   }
-  static constexpr int ROWT = (LAY == LAY_CONTIG || LAY == LAY_CONTIG_G) ? HGP_CONTIG_THREADS : HGP_ROW_THREADS;
+  static constexpr int ROWT = (LAY == LAY_CONTIG || LAY == LAY_CONTIG_G || LAY == LAY_SEG_C) ? HGP_CONTIG_THREADS
+                                                                                          : HGP_ROW_THREADS;
   static constexpr int c_contig() {
     int c = (TT >= ROWT) ? 1 : ROWT / TT;
     while (c > 1 && (c * TT > 1024 || lds_bytes_for(c) > LDS_CAP / 2)) c >>= 1;
@@ -183,7 +184,8 @@ template <typename T, int H, int LAY> struct PassCfg {
   static constexpr int MINW_BLK = (WAVES_PER_BLOCK + 3) / 4;
   static constexpr int MINW_SET = lay_grp(LAY) ? (MINW_CL > MINW_BLK ? MINW_CL : MINW_BLK)
                                  : lay_smap(LAY) ? (TT >= 16 ? HGP_MINW_STRIDED : HGP_MINW_STRIDED_SMALL)
-                                 : (LAY == LAY_CONTIG || LAY == LAY_CONTIG_G) ? MINW_CL : HGP_MINW_ROW;
+                                 : (LAY == LAY_CONTIG || LAY == LAY_CONTIG_G || LAY == LAY_SEG_C) ? MINW_CL
+                                                                                                  : HGP_MINW_ROW;
   static constexpr int MINW = MINW_SET > 0 ? MINW_SET : MINW_AUTO;
 };
 

@@ -77,8 +77,12 @@ static PassGeom geom_one() {
 
 template <typename T, int H>
 static PassGeom geom_h(int lay) {
-  if (lay == LAY_STRIDED || lay == LAY_SEG_S) return geom_one<T, H, LAY_STRIDED>();
-  if (lay == LAY_CONTIG || lay == LAY_CONTIG_G || lay == LAY_SEG_C) return geom_one<T, H, LAY_CONTIG>();
+  // the geometry of the very instantiation launch_h runs (block shape and lines per block)
+  if (lay == LAY_STRIDED) return geom_one<T, H, LAY_STRIDED>();
+  if (lay == LAY_SEG_S) return geom_one<T, H, LAY_SEG_S>();
+  if (lay == LAY_CONTIG) return geom_one<T, H, LAY_CONTIG>();
+  if (lay == LAY_CONTIG_G) return geom_one<T, H, LAY_CONTIG_G>();
+  if (lay == LAY_SEG_C) return geom_one<T, H, LAY_SEG_C>();
   if (lay == LAY_RP) return geom_one<T, H, LAY_RP>();
   if (lay == LAY_GRP2) return grp_ok<T, H, LAY_GRP2>() ? geom_one<T, H, LAY_GRP2>() : PassGeom{0, 0, 0};
   if (lay == LAY_GRP4) return grp_ok<T, H, LAY_GRP4>() ? geom_one<T, H, LAY_GRP4>() : PassGeom{0, 0, 0};

@@ -47,8 +47,12 @@ namespace hgp {
 #ifndef HGP_ROWG_2048
 #define HGP_ROWG_2048 2           // G at H = 2048 (fp32): 4 pairs x 2 columns = 128 B
 #endif
+// H >= 4096: G = 4 (2 pairs x 4 columns = 128 B) speeds both row passes (C4: 1.41 -> 1.16 ms,
+// 1.71 -> 1.63 ms) but the axis-0 pass reading one column of every 32 B loses more (2.52 -> 2.97
+// ms; the interleaved LAY_GRP4 blocks 3.85 ms): C4 K matvec 5.64 (G = 1) vs 5.78 ms (G = 4),
+// profiles/r3_grouped_passtime.txt.  Plain layout there; G = 2 at H = 2048 (C3 1.71 -> 1.63 ms).
 #ifndef HGP_ROWG_4096
-#define HGP_ROWG_4096 4           // G at H >= 4096 (fp32): 2 pairs x 4 columns = 128 B
+#define HGP_ROWG_4096 1
 #endif
 template <typename T, int H> struct RowGroup {
   static constexpr int G = (!std::is_same<T, float>::value || !is_pow2(H)) ? 1

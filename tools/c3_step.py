@@ -1,9 +1,9 @@
 """C3 minibatch step timing (GPU box): one `svigp_fit` minibatch (`svi_gp.py:172-442` via
 hipgp_amd/ziggy/svi_gp.py) on the C3 shape -- 2048 x 2048 inducing grid on [-1, 1]^2, Matern-3/2
-(ell 0.1), N = 100k synthetic observations, batch 1000 (`experiment_util.py:44-50`), PCG
-maxiter 20: zero grads, elbo_and_grad (fused Kuf + compute_kn + statistics), with learned
-kernel the hyper backward + Adam step, the natural-gradient SGD step.  Both model classes.
-One JSON line per (model, learn_kernel).
+(ell 0.02, nugget 1e-2), N = 100k synthetic observations, batch 1000 (`experiment_util.py:44-50`),
+PCG maxiter 20: zero grads, elbo_and_grad (fused Kuf + compute_kn + statistics), with learned
+kernel the hyper backward + Adam step, the natural-gradient SGD step (lr 0.01, the svi_gp.py
+default).  One JSON line per (model, learn_kernel, batch).
 
     python tools/c3_step.py > gpurun_out/c3_step.jsonl
 """
@@ -32,8 +32,8 @@ def main():
     # (model, learned kernel, batch): the learned-kernel step keeps autograd graphs of several
     # (batch, M) tensors (16 GB each at batch 1000), so it runs at the fit default batch 256
     for cls, learn_kernel, bsz in (("MeanFieldToeplitzGP", False, 1000), ("MeanFieldToeplitzGP", True, 256)):
-        mod = getattr(hg, cls)(zk.Matern(nu=1.5, dtype=dt), grids, num_obs=N, sig2_init=1., ell_init=.1,
-                                noise2_init=.01, learn_kernel=learn_kernel, dtype=dt).cuda_params(0)
+        mod = getattr(hg, cls)(zk.Matern(nu=1.5, dtype=dt), grids, num_obs=N, sig2_init=1., ell_init=.02,
+                                jitter_val=1e-2, noise2_init=.01, learn_kernel=learn_kernel, dtype=dt).cuda_params(0)
         X = torch.tensor(x, dtype=dt, device=dev)
         Y = torch.tensor(y, dtype=dt, device=dev)
         S = torch.tensor(s, dtype=dt, device=dev)
