@@ -323,6 +323,36 @@ __device__ __forceinline__ C2<T> tw_at(const C2<T>* __restrict__ tab, int q) {
   return w;
 }
 
+// Stage twiddles: a[r] *= w^r (forward) / conj(w)^r (inverse), r = 1..R-1, w = W_H^{kk H/(NS R)}.
+// Default: powers by binary powering (at most 4 products deep, ~4 ulp), all R-1 live at once.
+// HGP_TW_CHAIN: a running product (one live power: fewer VGPRs, up to R-2 products deep).
+#ifndef HGP_TW_CHAIN
+#define HGP_TW_CHAIN 0
+#endif
+template <typename T, int H, int R, int DIR, int NS>
+__device__ __forceinline__ void stage_twiddle(C2<T>* a, int kk, const C2<T>* __restrict__ tab) {
+  const C2<T> w = tw_at<T, H>(tab, (2 * (H / (NS * R))) * kk);
+  if constexpr (HGP_TW_CHAIN) {
+    C2<T> wr = w;
+#pragma unroll
+    for (int r = 1; r < R; ++r) {
+      if (r > 1) wr = cmul<T>(wr, w);
+      a[r] = (DIR < 0) ? cmul<T>(a[r], wr) : cmulc<T>(a[r], wr);
+    }
+  } else {
+    C2<T> wp[R];
+    wp[1] = w;
+#pragma unroll
+    for (int r = 2; r < R; ++r) {
+      const int hi = (r & (r - 1)) == 0 ? r / 2 : (1 << (31 - __builtin_clz(r)));   // r = hi + lo
+      const int lo = r - hi;
+      wp[r] = cmul<T>(wp[hi], wp[lo]);
+    }
+#pragma unroll
+    for (int r = 1; r < R; ++r) a[r] = (DIR < 0) ? cmul<T>(a[r], wp[r]) : cmulc<T>(a[r], wp[r]);
+  }
+}
+
 // Hermitian partner of position p in the even frequency half: (H - p) mod H
 template <int H>
 __device__ __forceinline__ int herm_partner0(int p) {
@@ -362,19 +392,8 @@ __device__ __forceinline__ void fft_stage(C2<T> (&v)[P], C2<T>* lds, int base, i
       for (int r = 0; r < R; ++r) a[b][r] = v[b + r * NB];
       if constexpr (NS > 1) {
         const int j = t + b * TT;
-        const int kk = j & (NS - 1);
-        // w^r with w = W_H^{kk*H/(NS*R)}: one LDS lookup, powers by binary powering
-        // (at most 4 products deep, ~4 ulp) -- few LDS reads and few live registers.
-        C2<T> wp[R];
-        wp[1] = tw_at<T, H>(tab, (2 * (H / (NS * R))) * kk);
-#pragma unroll
-        for (int r = 2; r < R; ++r) {
-          const int hi = (r & (r - 1)) == 0 ? r / 2 : (1 << (31 - __builtin_clz(r)));   // r = hi + lo
-          const int lo = r - hi;
-          wp[r] = cmul<T>(wp[hi], wp[lo]);
-        }
-#pragma unroll
-        for (int r = 1; r < R; ++r) a[b][r] = (DIR < 0) ? cmul<T>(a[b][r], wp[r]) : cmulc<T>(a[b][r], wp[r]);
+        // w = W_H^{kk*H/(NS*R)}: one LDS lookup, its powers in registers (stage_twiddle)
+        stage_twiddle<T, H, R, DIR, NS>(a[b], j & (NS - 1), tab);
       }
       dft<T, R, DIR>(a[b]);
     }
@@ -435,18 +454,7 @@ __device__ __forceinline__ void fft_bfly(const C2<T> (&v)[P], C2<T> (&a)[P], int
     for (int r = 0; r < R; ++r) a[b * R + r] = v[b + r * NB];
     if constexpr (NS > 1) {
       const int j = t + b * TT;
-      const int kk = j & (NS - 1);
-      C2<T> wp[R];
-      wp[1] = tw_at<T, H>(tab, (2 * (H / (NS * R))) * kk);
-#pragma unroll
-      for (int r = 2; r < R; ++r) {
-        const int hi = (r & (r - 1)) == 0 ? r / 2 : (1 << (31 - __builtin_clz(r)));   // r = hi + lo
-        const int lo = r - hi;
-        wp[r] = cmul<T>(wp[hi], wp[lo]);
-      }
-#pragma unroll
-      for (int r = 1; r < R; ++r)
-        a[b * R + r] = (DIR < 0) ? cmul<T>(a[b * R + r], wp[r]) : cmulc<T>(a[b * R + r], wp[r]);
+      stage_twiddle<T, H, R, DIR, NS>(&a[b * R], j & (NS - 1), tab);
     }
     dft<T, R, DIR>(&a[b * R]);
   }

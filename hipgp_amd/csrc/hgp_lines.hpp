@@ -81,22 +81,26 @@ __global__ __launch_bounds__((LineTCfg<T, H>::THREADS), (LineTCfg<T, H>::MINW)) 
   const C2<T>* in = reinterpret_cast<const C2<T>*>(d.in.ptr) + (int64_t)B.q * d.in.q_stride +
                     (int64_t)B.r * d.in.r_stride + (int64_t)(valid ? B.i0 + l : 0) * d.in.p_stride;
   const int in_len = d.in.len;     // <= 2H; > H (folded halves) for the R operator's n-grid input
-  const bool fold = in_len > H;    // when L_R = 3 * 2^k < 2n
   C2<T> va[P], vb[P];
+  // fold (when L_R = 3 * 2^k < 2n) as a compile-time branch of its own straight-line loads
+  auto load_lines = [&](auto fold_c) {
 #pragma unroll
-  for (int k = 0; k < P; ++k) {
-    const int p = t + TT * k;
-    C2<T> a = in[p < in_len ? p : 0];
-    if (!valid || p >= in_len) a = mk<T>(0, 0);
-    va[k] = a;
-    vb[k] = a;
-    if (fold) {
-      C2<T> hi = in[p + H < in_len ? p + H : 0];
-      if (!valid || p + H >= in_len) hi = mk<T>(0, 0);
-      va[k] = cadd<T>(a, hi);
-      vb[k] = csub<T>(a, hi);
+    for (int k = 0; k < P; ++k) {
+      const int p = t + TT * k;
+      C2<T> a = in[p < in_len ? p : 0];
+      if (!valid || p >= in_len) a = mk<T>(0, 0);
+      va[k] = a;
+      vb[k] = a;
+      if constexpr (decltype(fold_c)::value) {
+        C2<T> hi = in[p + H < in_len ? p + H : 0];
+        if (!valid || p + H >= in_len) hi = mk<T>(0, 0);
+        va[k] = cadd<T>(a, hi);
+        vb[k] = csub<T>(a, hi);
+      }
     }
-  }
+  };
+  if (in_len > H) load_lines(std::true_type{});
+  else load_lines(std::false_type{});
   __syncthreads();   // twiddle table staged
 #pragma unroll
   for (int k = 0; k < P; ++k) vb[k] = cmul<T>(vb[k], tw_at<T, H>(tab, t + TT * k));

@@ -479,26 +479,33 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
   if constexpr (MODE == PASS_FWD || CONV) {
     const int in_len = d.in.len;
     const int lim = in_len - 1;
-    const bool fold = CAN_FOLD && in_len > H;
+    // the (uniform) fold test picks one of two straight-line load sequences
+    auto load_line = [&](auto fold_c) {
+      constexpr bool FOLD = decltype(fold_c)::value;
 #pragma unroll
-    for (int k = 0; k < P; ++k) {
-      const int p = t + TT * k;
-      C2<T> a;
-      if constexpr (BUF) {
-        a = buf_ld_c2<T>(rin, (uint32_t)t * es, (uint32_t)(TT * k) * es);
-      } else {
-        a = load_in(p < in_len ? p : lim);
-        if (p >= in_len) a = mk<T>(0, 0);
-      }
-      C2<T> c = mk<T>(0, 0);
-      if constexpr (CAN_FOLD) {
-        if (fold) {                 // uniform; beyond in_len the buffer range returns 0
+      for (int k = 0; k < P; ++k) {
+        const int p = t + TT * k;
+        C2<T> a;
+        if constexpr (BUF) {
+          a = buf_ld_c2<T>(rin, (uint32_t)t * es, (uint32_t)(TT * k) * es);
+        } else {
+          a = load_in(p < in_len ? p : lim);
+          if (p >= in_len) a = mk<T>(0, 0);
+        }
+        C2<T> c = mk<T>(0, 0);
+        if constexpr (FOLD) {       // beyond in_len the buffer range returns 0
           if constexpr (BUF) c = buf_ld_c2<T>(rin, (uint32_t)t * es, (uint32_t)(TT * k + H) * es);
           else c = load_hi(p);
         }
+        va[k] = cadd<T>(a, c);
+        vb[k] = cmul<T>(csub<T>(a, c), tw_at<T, H>(tab, p));
       }
-      va[k] = cadd<T>(a, c);
-      vb[k] = cmul<T>(csub<T>(a, c), tw_at<T, H>(tab, p));
+    };
+    if constexpr (CAN_FOLD) {
+      if (in_len > H) load_line(std::true_type{});
+      else load_line(std::false_type{});
+    } else {
+      load_line(std::false_type{});
     }
   }
 
