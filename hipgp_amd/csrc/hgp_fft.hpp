@@ -512,9 +512,19 @@ __device__ __forceinline__ void fft_stage2(C2<T> (&va)[P], C2<T> (&vb)[P], C2<T>
 
 // Two H-point FFTs (same direction) of the lines whose values this thread holds in va and vb,
 // through one exchange image at `base` (fft_line semantics for each).
-template <typename T, int H, int P, int DIR, int STRIDE, bool WAVE = false>
+// HGP_SEQ_MULTIWAVE: lines of several waves (block barriers at every exchange) run the two
+// transforms one after the other instead (32 fewer live VGPRs: no `a` array in flight).
+#ifndef HGP_SEQ_MULTIWAVE
+#define HGP_SEQ_MULTIWAVE 0
+#endif
+template <typename T, int H, int P, int DIR, int STRIDE, bool WAVE = false, bool SEQ = (HGP_SEQ_MULTIWAVE && !WAVE)>
 __device__ __forceinline__ void fft_line2(C2<T> (&va)[P], C2<T> (&vb)[P], C2<T>* lds, int base, int t,
                                           const C2<T>* __restrict__ tab) {
+  if constexpr (SEQ) {
+    fft_line<T, H, P, DIR, STRIDE, WAVE>(va, lds, base, t, tab);
+    fft_line<T, H, P, DIR, STRIDE, WAVE>(vb, lds, base, t, tab);
+    return;
+  }
   int tt = t;
   asm volatile("" : "+v"(tt));
   C2<T> a[P];

@@ -71,11 +71,28 @@
 #ifndef HGP_CONTIG_THREADS
 #define HGP_CONTIG_THREADS 512   // complex contiguous lines (2-D column CONV, setup grids)
 #endif
+// the same for lines of several waves (TT >= 128): one 4096-point line (or two 2048-point lines)
+// per block, so that a CU's blocks are small enough for the occupancy chosen below
+// (profiles/r3_h_variants_passtime.txt: C4 column pass 2.47 -> 2.00 ms with MINW 3, C3 0.745 -> 0.69 ms)
+#ifndef HGP_CONTIG_THREADS_LONG
+#define HGP_CONTIG_THREADS_LONG 256
+#endif
+// the column passes' two half-length transforms one after the other on lines of several waves
+// (instead of interleaved over one exchange image, hgp_fft.hpp fft_line2)
+#ifndef HGP_SEQ_PASS
+#define HGP_SEQ_PASS 0
+#endif
 #ifndef HGP_MINW_CONTIG
 #define HGP_MINW_CONTIG 4
 #endif
 #ifndef HGP_MINW_CONTIG_LONG
-#define HGP_MINW_CONTIG_LONG HGP_MINW_CONTIG   // lines of H >= 2048 (multi-wave, two-level twiddles)
+#define HGP_MINW_CONTIG_LONG HGP_MINW_CONTIG   // lines of H = 2048 (multi-wave, two-level twiddles)
+#endif
+// lines of H = 4096 (4 waves): 3 waves per SIMD (up to 168 VGPRs).  At 4 the 4096-point column kernel
+// spilled 23 VGPRs, and every spill went to HBM (PMC: 5.8 of the C4 K op's 24 GB were scratch),
+// column pass 2.47 ms; at 3 (1-line blocks, 3 per CU) it spills none: 2.00 ms, traffic 1.15x.
+#ifndef HGP_MINW_CONTIG_4096
+#define HGP_MINW_CONTIG_4096 3
 #endif
 
 namespace hgp {
@@ -160,8 +177,9 @@ template <typename T, int H, int LAY> struct PassCfg {
     while (c > 1 && (c * TT > 1024 || lds_bytes_for(c) > LDS_CAP)) c >>= 1;
     return c;
   }
-  static constexpr int ROWT = (LAY == LAY_CONTIG || LAY == LAY_CONTIG_G || LAY == LAY_SEG_C) ? HGP_CONTIG_THREADS
-                                                                                          : HGP_ROW_THREADS;
+  static constexpr int ROWT = (LAY == LAY_CONTIG || LAY == LAY_CONTIG_G || LAY == LAY_SEG_C)
+                                  ? (TT >= 128 ? HGP_CONTIG_THREADS_LONG : HGP_CONTIG_THREADS)
+                                  : HGP_ROW_THREADS;
   static constexpr int c_contig() {
     int c = (TT >= ROWT) ? 1 : ROWT / TT;
     while (c > 1 && (c * TT > 1024 || lds_bytes_for(c) > LDS_CAP / 2)) c >>= 1;
@@ -179,7 +197,9 @@ template <typename T, int H, int LAY> struct PassCfg {
   static constexpr int BLOCKS_BY_LDS = LDS_CAP / LDS;
   static constexpr int MINW_LDS = (BLOCKS_BY_LDS * WAVES_PER_BLOCK) / 4;
   static constexpr int MINW_AUTO = MINW_LDS < 1 ? 1 : (MINW_LDS > 4 ? 4 : MINW_LDS);
-  static constexpr int MINW_CL = H >= 2048 ? HGP_MINW_CONTIG_LONG : HGP_MINW_CONTIG;
+  // (3 waves per SIMD only for lines of 4 waves: 3 whole blocks per CU)
+  static constexpr int MINW_CL = (H >= 4096 && TT == 256) ? HGP_MINW_CONTIG_4096
+                                 : H >= 2048 ? HGP_MINW_CONTIG_LONG : HGP_MINW_CONTIG;
   // a block's waves must fit the SIMDs' share at once: >= WAVES_PER_BLOCK / 4 waves per SIMD
   static constexpr int MINW_BLK = (WAVES_PER_BLOCK + 3) / 4;
   static constexpr int MINW_SET = lay_grp(LAY) ? (MINW_CL > MINW_BLK ? MINW_CL : MINW_BLK)
@@ -511,7 +531,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
 
   if constexpr (MODE == PASS_FWD) {
     // both halves' transforms interleaved over one exchange image (hgp_fft.hpp fft_line2)
-    fft_line2<T, H, P, -1, LSTRIDE, Cfg::WAVE>(va, vb, lds, lbase, t, tab);
+    fft_line2<T, H, P, -1, LSTRIDE, Cfg::WAVE, (HGP_SEQ_PASS || HGP_SEQ_MULTIWAVE) && !Cfg::WAVE>(va, vb, lds, lbase, t, tab);
     auto fwd_half = [&](auto half_c, C2<T>(&v)[P]) {
       constexpr int half = decltype(half_c)::value;
       if constexpr (HERM_OUT) {
@@ -546,7 +566,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
     // va ends as the even half's inverse (ye), vb as the odd half's (yo); the two halves'
     // transforms run interleaved over one exchange image (hgp_fft.hpp fft_line2)
     if constexpr (MODE == PASS_CONV) {
-      fft_line2<T, H, P, -1, LSTRIDE, Cfg::WAVE>(va, vb, lds, lbase, t, tab);
+      fft_line2<T, H, P, -1, LSTRIDE, Cfg::WAVE, (HGP_SEQ_PASS || HGP_SEQ_MULTIWAVE) && !Cfg::WAVE>(va, vb, lds, lbase, t, tab);
       // the line's real spectrum, loaded after the forward transforms (no registers held across
       // them); L2-resident: every line of a block shares it (RHS-fastest map, XCD-grouped)
       T sre1[P];
@@ -577,7 +597,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
         vb[k] = mk<T>(vb[k].x * sre1[k], vb[k].y * sre1[k]);
       }
     } else if constexpr (MODE == PASS_CONVC) {
-      fft_line2<T, H, P, -1, LSTRIDE, Cfg::WAVE>(va, vb, lds, lbase, t, tab);
+      fft_line2<T, H, P, -1, LSTRIDE, Cfg::WAVE, (HGP_SEQ_PASS || HGP_SEQ_MULTIWAVE) && !Cfg::WAVE>(va, vb, lds, lbase, t, tab);
       // complex spectrum at (i, r, kperm): block-uniform base + 32-bit lane offset
       const C2<T>* sbase = reinterpret_cast<const C2<T>*>(d.spec) +
                            (GRP ? (int64_t)i0 * d.spec_r : (int64_t)i0 * d.spec_i + (int64_t)r * d.spec_r);
@@ -602,7 +622,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
         }
       }
     }
-    fft_line2<T, H, P, +1, LSTRIDE, Cfg::WAVE>(va, vb, lds, lbase, t, tab);
+    fft_line2<T, H, P, +1, LSTRIDE, Cfg::WAVE, (HGP_SEQ_PASS || HGP_SEQ_MULTIWAVE) && !Cfg::WAVE>(va, vb, lds, lbase, t, tab);
     // combine in registers: y[p] = ye + conj(W_L^p) yo, y[p+H] = ye - conj(W_L^p) yo; crop.
     const int out_len = d.out.len;
     const T* dot_re = nullptr; const T* dot_im = nullptr;

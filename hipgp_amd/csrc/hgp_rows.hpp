@@ -54,6 +54,11 @@ namespace hgp {
 #ifndef HGP_ROWG_4096
 #define HGP_ROWG_4096 1
 #endif
+// pairs per block of the grouped 4096-point rows (0: 8 / G, i.e. 128-B segments).  2 with G = 2:
+// 64-B segments but a 70 KB block, two per CU.
+#ifndef HGP_ROWG_PAIRS_LONG
+#define HGP_ROWG_PAIRS_LONG 0
+#endif
 template <typename T, int H> struct RowGroup {
   static constexpr int G = (!std::is_same<T, float>::value || !is_pow2(H)) ? 1
                          : H == 2048 ? HGP_ROWG_2048 : H >= 4096 ? HGP_ROWG_4096 : 1;
@@ -72,7 +77,8 @@ template <typename T, int H, int G = 1> struct RowTCfg {
   static constexpr int area(int c) { return ex_elems(c) > tile_elems(c) ? ex_elems(c) : tile_elems(c); }
   static constexpr int lds_bytes_for(int c) { return area(c) * (int)sizeof(C2<T>) + TwTab<T, H>::BYTES; }
   static constexpr int c_pairs() {
-    if (G > 1) return 8 / G;                                     // 2C rows x G columns = 128 B (fp32)
+    if (G > 1) return (H >= 4096 && HGP_ROWG_PAIRS_LONG > 0) ? HGP_ROWG_PAIRS_LONG
+                                                              : 8 / G;   // 2C rows x G columns = 128 B (fp32)
     int c = (TT > 64 ? HGP_ROWT_PAIRS_BIG : HGP_ROWT_PAIRS) * 64 / TT;   // 512 threads at the default
     if (c < 1) c = 1;
     if (c > 64) c = 64;                            // tiny rows: cap the tile height

@@ -18,12 +18,14 @@ if stats:
     for r in rows[:12]:
         print(f"  {r['Name'][:70]:70s} calls {r['Calls']:>5} avg_us {float(r['AverageNs']) / 1e3:9.1f} pct {float(r['Percentage']):5.1f}")
 tot = collections.defaultdict(float)
+per = collections.defaultdict(float)     # (kernel, counter) -> KB over the run
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
     for f in glob.glob(os.path.join(root, c, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 if any(k in row.get("Kernel_Name", "") for k in OP_KERNELS):
                     tot[c] += float(row["Counter_Value"])
+                    per[(row["Kernel_Name"][:60], c)] += float(row["Counter_Value"])
 d = len(shape)
 M = 1
 for m in shape:
@@ -35,3 +37,6 @@ res = {"shape": shape, "rhs": rhs, "ops": nops, "fetch_kb_per_op_raw": tot["FETC
        "write_kb_per_op": tot["WRITE_SIZE"] / nops, "traffic_bytes_per_op": traffic,
        "algorithmic_bytes_per_op": rhs * bk, "traffic_over_algorithmic": traffic / (rhs * bk)}
 print(json.dumps(res))
+for name in sorted({k for k, _ in per}):
+    f, w = 2 * per[(name, "FETCH_SIZE")] * 1024 / nops / 1e9, per[(name, "WRITE_SIZE")] * 1024 / nops / 1e9
+    print(f"  per op: {name:60s} fetch(x2) {f:8.3f} GB  write {w:8.3f} GB")
