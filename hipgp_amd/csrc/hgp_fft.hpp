@@ -126,15 +126,16 @@ template <typename T, int H> struct PFor {
 // exchange index math of fft_xchg needs.
 template <int H, int P> struct Stages {
   static constexpr bool TRI = !is_pow2(H);
+  static constexpr int RMAX = P < 16 ? P : 16;   // in-register DFTs up to 16 points (P = 32: two per stage)
   static constexpr int last_tri() { return 3 * (H / 3 >= 4 ? 4 : H / 3); }
   static constexpr int count() {
-    if (!TRI) { int n = 0, rem = H; while (rem > 1) { int r = rem >= P ? P : rem; rem /= r; ++n; } return n; }
+    if (!TRI) { int n = 0, rem = H; while (rem > 1) { int r = rem >= RMAX ? RMAX : rem; rem /= r; ++n; } return n; }
     int n = 1, rem = H / last_tri();
     while (rem > 1) { rem /= (rem >= 4 ? 4 : rem); ++n; }
     return n;
   }
   static constexpr int radix(int s) {
-    if (!TRI) { int rem = H; for (int i = 0; i < s; ++i) rem /= (rem >= P ? P : rem); return rem >= P ? P : rem; }
+    if (!TRI) { int rem = H; for (int i = 0; i < s; ++i) rem /= (rem >= RMAX ? RMAX : rem); return rem >= RMAX ? RMAX : rem; }
     int rem = H / last_tri(), i = 0;
     while (rem > 1) { const int r = rem >= 4 ? 4 : rem; if (i == s) return r; rem /= r; ++i; }
     return last_tri();

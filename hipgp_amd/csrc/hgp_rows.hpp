@@ -64,8 +64,15 @@ template <typename T, int H> struct RowGroup {
                          : H == 2048 ? HGP_ROWG_2048 : H >= 4096 ? HGP_ROWG_4096 : 1;
 };
 
+// points per thread of the fp32 row passes at H >= 4096 (0: PFor's 16).  32: a pair's line is two
+// waves instead of four, a 4-pair block 8 waves, 2 waves per SIMD with up to 256 VGPRs (no spills;
+// the P = 16 row inverse spilled 13 VGPRs to HBM scratch at C4).
+#ifndef HGP_ROW_P_LONG
+#define HGP_ROW_P_LONG 0
+#endif
 template <typename T, int H, int G = 1> struct RowTCfg {
-  static constexpr int P = PFor<T, H>::v;
+  static constexpr int P = (std::is_same<T, float>::value && is_pow2(H) && H >= 4096 && HGP_ROW_P_LONG > 0)
+                               ? HGP_ROW_P_LONG : PFor<T, H>::v;
   static constexpr int TT = H / P;
   // tile chunks per frequency half (the grouped blocks keep a chunk of columns in LDS at a time)
   static constexpr int NCH = G > 1 ? 2 : 1;
@@ -574,20 +581,62 @@ __global__ __launch_bounds__((RowTCfg<T, H, G>::THREADS), (RowTCfg<T, H, G>::MIN
   T dsum = 0;
   int tt = t;
   asm volatile("" : "+v"(tt));
+  if constexpr (TT % 64 == 0) {
+    // the pair is wave-uniform: raw buffer stores from the rows' scalar bases with 32-bit lane
+    // offsets; the resource ranges crop (pp >= out_len) and drop an absent pair / second row, so
+    // no per-position branch or 64-bit address is formed.  (Plain stores here held a 64-bit
+    // address per position under per-position exec branches: the 4096-point kernel spilled 13
+    // VGPRs, and its scratch traffic went to HBM.)
+    const uint32_t rowb = (uint32_t)out_len * (uint32_t)sizeof(T);
+    const BufRsrc ra = buf_rsrc(out_a, pvalid ? rowb : 0u);
+    const BufRsrc rb2 = buf_rsrc(out_b, has2 ? rowb : 0u);
+    const uint32_t lo = (uint32_t)tt * (uint32_t)sizeof(T);
+    auto put = [&](auto dot_c) {
+      constexpr bool DOT = decltype(dot_c)::value;
+      BufRsrc da, db;
+      if constexpr (DOT) {
+        da = buf_rsrc(dot_a, pvalid ? rowb : 0u);
+        db = buf_rsrc(dot_b, has2 ? rowb : 0u);
+      }
 #pragma unroll
-  for (int k = 0; k < P; ++k) {
-    const int p = tt + TT * k;
-    const C2<T> wo = cmulc<T>(vb[k], tw_at<T, H>(tab, p));
+      for (int k = 0; k < P; ++k) {
+        const int p = tt + TT * k;
+        const C2<T> wo = cmulc<T>(vb[k], tw_at<T, H>(tab, p));
 #pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
-      const C2<T> y = hh == 0 ? cadd<T>(va[k], wo) : csub<T>(va[k], wo);
-      const int pp = p + hh * H;
-      if (pvalid && pp < out_len) {
-        out_a[pp] = y.x;
-        if (dot_a != nullptr) dsum += y.x * dot_a[pp];
-        if (has2) {
-          out_b[pp] = y.y;
-          if (dot_a != nullptr) dsum += y.y * dot_b[pp];
+        for (int hh = 0; hh < 2; ++hh) {
+          if (hh * H < out_len) {               // uniform: does this half reach the output at all
+            const C2<T> y = hh == 0 ? cadd<T>(va[k], wo) : csub<T>(va[k], wo);
+            const uint32_t so = (uint32_t)(TT * k + hh * H) * (uint32_t)sizeof(T);
+            buf_st<T>(y.x, ra, lo, so);
+            buf_st<T>(y.y, rb2, lo, so);
+            if constexpr (DOT) {                // loads past the range return 0; the select keeps
+              const bool in = p + hh * H < out_len;   // a cropped (never stored) value out of the sum
+              const T xa = buf_ld<T>(da, lo, so), xb = buf_ld<T>(db, lo, so);
+              dsum += in ? y.x * xa : (T)0;      // the plain path's order: row a, then row b
+              dsum += in ? y.y * xb : (T)0;
+            }
+          }
+        }
+      }
+    };
+    if (dot_a != nullptr) put(std::true_type{});
+    else put(std::false_type{});
+  } else {
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+      const int p = tt + TT * k;
+      const C2<T> wo = cmulc<T>(vb[k], tw_at<T, H>(tab, p));
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const C2<T> y = hh == 0 ? cadd<T>(va[k], wo) : csub<T>(va[k], wo);
+        const int pp = p + hh * H;
+        if (pvalid && pp < out_len) {
+          out_a[pp] = y.x;
+          if (dot_a != nullptr) dsum += y.x * dot_a[pp];
+          if (has2) {
+            out_b[pp] = y.y;
+            if (dot_a != nullptr) dsum += y.y * dot_b[pp];
+          }
         }
       }
     }
