@@ -27,6 +27,10 @@
 
 namespace hgp {
 
+// occupancy of the line-inverse pass (0: from the LDS footprint)
+#ifndef HGP_MINW_LINE_INV
+#define HGP_MINW_LINE_INV 0
+#endif
 template <typename T, int H> struct LineTCfg {
   static constexpr int P = PFor<T, H>::v;
   static constexpr int TT = H / P;
@@ -48,6 +52,7 @@ template <typename T, int H> struct LineTCfg {
   static constexpr int BLOCKS_BY_LDS = LDS_CAP / LDS;
   static constexpr int MINW_LDS = (BLOCKS_BY_LDS * ((THREADS + 63) / 64)) / 4;
   static constexpr int MINW = MINW_LDS < 1 ? 1 : (MINW_LDS > 4 ? 4 : MINW_LDS);
+  static constexpr int MINW_INV = HGP_MINW_LINE_INV > 0 ? HGP_MINW_LINE_INV : MINW;
 };
 
 // block -> (q, r, first line i0); l = line of this thread group, t = position index
@@ -131,7 +136,7 @@ __global__ __launch_bounds__((LineTCfg<T, H>::THREADS), (LineTCfg<T, H>::MINW)) 
 }
 
 template <typename T, int H>
-__global__ __launch_bounds__((LineTCfg<T, H>::THREADS), (LineTCfg<T, H>::MINW)) void k_line_inv_t(const PassDesc d) {
+__global__ __launch_bounds__((LineTCfg<T, H>::THREADS), (LineTCfg<T, H>::MINW_INV)) void k_line_inv_t(const PassDesc d) {
   using Cfg = LineTCfg<T, H>;
   constexpr int P = Cfg::P, TT = Cfg::TT, C = Cfg::C, PITCH = Cfg::PITCH;
   if (d.done != nullptr && *d.done) return;
@@ -191,8 +196,14 @@ __global__ __launch_bounds__((LineTCfg<T, H>::THREADS), (LineTCfg<T, H>::MINW)) 
   __syncthreads();   // tile consumed: the exchange images overlay it
   fft_line2<T, H, P, +1, 1, Cfg::WAVE>(va, vb, lds, l * H, t, tab);
   // y[p] = ye + conj(W_L^p) yo, y[p + H] = ye - conj(W_L^p) yo; crop to out.len
-  C2<T>* out = reinterpret_cast<C2<T>*>(d.out.ptr) + (int64_t)B.q * d.out.q_stride + (int64_t)B.r * d.out.r_stride +
-               (int64_t)(valid ? B.i0 + l : 0) * d.out.p_stride;
+  // one buffer resource from the block's first line (uniform; its C lines lie within 2 GiB of it,
+  // checked on the host), per-lane 32-bit offsets, masked positions sent past the range (dropped)
+  // instead of per-position exec branches with 64-bit addresses
+  C2<T>* outb0 = reinterpret_cast<C2<T>*>(d.out.ptr) + (int64_t)B.q * d.out.q_stride + (int64_t)B.r * d.out.r_stride +
+                 (int64_t)B.i0 * d.out.p_stride;
+  const BufRsrc ro = buf_rsrc(outb0, 0x7fffffffu);
+  constexpr uint32_t DROP = 0x80000000u;
+  const uint32_t lo = (uint32_t)l * (uint32_t)d.out.p_stride;
   const int out_len = d.out.len;
   int tt = t;
   asm volatile("" : "+v"(tt));
@@ -200,8 +211,10 @@ __global__ __launch_bounds__((LineTCfg<T, H>::THREADS), (LineTCfg<T, H>::MINW)) 
   for (int k = 0; k < P; ++k) {
     const int p = tt + TT * k;
     const C2<T> wo = cmulc<T>(vb[k], tw_at<T, H>(tab, p));
-    if (valid && p < out_len) out[p] = cadd<T>(va[k], wo);
-    if (valid && p + H < out_len) out[p + H] = csub<T>(va[k], wo);
+    const uint32_t o = (lo + (uint32_t)p) * (uint32_t)sizeof(C2<T>);
+    buf_st_c2<T>(cadd<T>(va[k], wo), ro, (valid && p < out_len) ? o : DROP);
+    if (H < out_len)   // uniform: the second half reaches the output (R^T's n-grid lines)
+      buf_st_c2<T>(csub<T>(va[k], wo), ro, (valid && p + H < out_len) ? o + (uint32_t)(H * (int)sizeof(C2<T>)) : DROP);
   }
 }
 

@@ -85,6 +85,15 @@
 #ifndef HGP_MINW_CONTIG
 #define HGP_MINW_CONTIG 4
 #endif
+// lines of H <= 512 (several lines per wave: the 3-D axis-0 passes): 256-thread blocks at 3 waves
+// per SIMD (the 256-point column kernel spilled 16 VGPRs at 4; C5 K op column pass 2.13 -> 1.74 ms,
+// R^T's 384-point one 8.41 -> 7.56 ms, profiles/r3_k_c5_passtime.txt)
+#ifndef HGP_MINW_CONTIG_SHORT
+#define HGP_MINW_CONTIG_SHORT 3
+#endif
+#ifndef HGP_CONTIG_THREADS_SHORT
+#define HGP_CONTIG_THREADS_SHORT 256
+#endif
 #ifndef HGP_MINW_CONTIG_LONG
 #define HGP_MINW_CONTIG_LONG HGP_MINW_CONTIG   // lines of H = 2048 (multi-wave, two-level twiddles)
 #endif
@@ -178,7 +187,7 @@ template <typename T, int H, int LAY> struct PassCfg {
     return c;
   }
   static constexpr int ROWT = (LAY == LAY_CONTIG || LAY == LAY_CONTIG_G || LAY == LAY_SEG_C)
-                                  ? (TT >= 128 ? HGP_CONTIG_THREADS_LONG : HGP_CONTIG_THREADS)
+                                  ? (TT >= 128 ? HGP_CONTIG_THREADS_LONG : H <= 512 ? HGP_CONTIG_THREADS_SHORT : HGP_CONTIG_THREADS)
                                   : HGP_ROW_THREADS;
   static constexpr int c_contig() {
     int c = (TT >= ROWT) ? 1 : ROWT / TT;
@@ -199,7 +208,7 @@ template <typename T, int H, int LAY> struct PassCfg {
   static constexpr int MINW_AUTO = MINW_LDS < 1 ? 1 : (MINW_LDS > 4 ? 4 : MINW_LDS);
   // (3 waves per SIMD only for lines of 4 waves: 3 whole blocks per CU)
   static constexpr int MINW_CL = (H >= 4096 && TT == 256) ? HGP_MINW_CONTIG_4096
-                                 : H >= 2048 ? HGP_MINW_CONTIG_LONG : HGP_MINW_CONTIG;
+                                 : H >= 2048 ? HGP_MINW_CONTIG_LONG : H <= 512 ? HGP_MINW_CONTIG_SHORT : HGP_MINW_CONTIG;
   // a block's waves must fit the SIMDs' share at once: >= WAVES_PER_BLOCK / 4 waves per SIMD
   static constexpr int MINW_BLK = (WAVES_PER_BLOCK + 3) / 4;
   static constexpr int MINW_SET = lay_grp(LAY) ? (MINW_CL > MINW_BLK ? MINW_CL : MINW_BLK)
@@ -531,7 +540,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
 
   if constexpr (MODE == PASS_FWD) {
     // both halves' transforms interleaved over one exchange image (hgp_fft.hpp fft_line2)
-    fft_line2<T, H, P, -1, LSTRIDE, Cfg::WAVE, (HGP_SEQ_PASS || HGP_SEQ_MULTIWAVE) && !Cfg::WAVE>(va, vb, lds, lbase, t, tab);
+    fft_line2<T, H, P, -1, LSTRIDE, Cfg::WAVE, (HGP_SEQ_PASS == 2 || ((HGP_SEQ_PASS || HGP_SEQ_MULTIWAVE) && !Cfg::WAVE))>(va, vb, lds, lbase, t, tab);
     auto fwd_half = [&](auto half_c, C2<T>(&v)[P]) {
       constexpr int half = decltype(half_c)::value;
       if constexpr (HERM_OUT) {
@@ -566,7 +575,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
     // va ends as the even half's inverse (ye), vb as the odd half's (yo); the two halves'
     // transforms run interleaved over one exchange image (hgp_fft.hpp fft_line2)
     if constexpr (MODE == PASS_CONV) {
-      fft_line2<T, H, P, -1, LSTRIDE, Cfg::WAVE, (HGP_SEQ_PASS || HGP_SEQ_MULTIWAVE) && !Cfg::WAVE>(va, vb, lds, lbase, t, tab);
+      fft_line2<T, H, P, -1, LSTRIDE, Cfg::WAVE, (HGP_SEQ_PASS == 2 || ((HGP_SEQ_PASS || HGP_SEQ_MULTIWAVE) && !Cfg::WAVE))>(va, vb, lds, lbase, t, tab);
       // the line's real spectrum, loaded after the forward transforms (no registers held across
       // them); L2-resident: every line of a block shares it (RHS-fastest map, XCD-grouped)
       T sre1[P];
@@ -597,7 +606,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
         vb[k] = mk<T>(vb[k].x * sre1[k], vb[k].y * sre1[k]);
       }
     } else if constexpr (MODE == PASS_CONVC) {
-      fft_line2<T, H, P, -1, LSTRIDE, Cfg::WAVE, (HGP_SEQ_PASS || HGP_SEQ_MULTIWAVE) && !Cfg::WAVE>(va, vb, lds, lbase, t, tab);
+      fft_line2<T, H, P, -1, LSTRIDE, Cfg::WAVE, (HGP_SEQ_PASS == 2 || ((HGP_SEQ_PASS || HGP_SEQ_MULTIWAVE) && !Cfg::WAVE))>(va, vb, lds, lbase, t, tab);
       // complex spectrum at (i, r, kperm): block-uniform base + 32-bit lane offset
       const C2<T>* sbase = reinterpret_cast<const C2<T>*>(d.spec) +
                            (GRP ? (int64_t)i0 * d.spec_r : (int64_t)i0 * d.spec_i + (int64_t)r * d.spec_r);
@@ -622,7 +631,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
         }
       }
     }
-    fft_line2<T, H, P, +1, LSTRIDE, Cfg::WAVE, (HGP_SEQ_PASS || HGP_SEQ_MULTIWAVE) && !Cfg::WAVE>(va, vb, lds, lbase, t, tab);
+    fft_line2<T, H, P, +1, LSTRIDE, Cfg::WAVE, (HGP_SEQ_PASS == 2 || ((HGP_SEQ_PASS || HGP_SEQ_MULTIWAVE) && !Cfg::WAVE))>(va, vb, lds, lbase, t, tab);
     // combine in registers: y[p] = ye + conj(W_L^p) yo, y[p+H] = ye - conj(W_L^p) yo; crop.
     const int out_len = d.out.len;
     const T* dot_re = nullptr; const T* dot_im = nullptr;

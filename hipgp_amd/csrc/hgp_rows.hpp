@@ -621,6 +621,30 @@ __global__ __launch_bounds__((RowTCfg<T, H, G>::THREADS), (RowTCfg<T, H, G>::MIN
     };
     if (dot_a != nullptr) put(std::true_type{});
     else put(std::false_type{});
+  } else if (dot_a == nullptr) {
+    // several pairs per wave (TT < 64): one buffer resource from the block's first row (uniform;
+    // the block's 2C rows lie within 2 GiB of it, checked on the host), per-lane 32-bit offsets,
+    // and masked positions sent past the range (dropped) instead of per-position exec branches
+    T* blk = reinterpret_cast<T*>(d.out.ptr) + (int64_t)q * d.out.q_stride + (int64_t)(2 * rb * C) * d.out.r_stride;
+    const BufRsrc ro = buf_rsrc(blk, 0x7fffffffu);
+    const uint32_t rowa = (uint32_t)(2 * l) * (uint32_t)d.out.r_stride, rowp = (uint32_t)d.out.r_stride;
+    constexpr uint32_t DROP = 0x80000000u;
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+      const int p = tt + TT * k;
+      const C2<T> wo = cmulc<T>(vb[k], tw_at<T, H>(tab, p));
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        if (hh * H < out_len) {
+          const C2<T> y = hh == 0 ? cadd<T>(va[k], wo) : csub<T>(va[k], wo);
+          const int pp = p + hh * H;
+          const bool in = pvalid && pp < out_len;
+          const uint32_t oa = (rowa + (uint32_t)pp) * (uint32_t)sizeof(T);
+          buf_st<T>(y.x, ro, in ? oa : DROP);
+          buf_st<T>(y.y, ro, (in && has2) ? oa + rowp * (uint32_t)sizeof(T) : DROP);
+        }
+      }
+    }
   } else {
 #pragma unroll
     for (int k = 0; k < P; ++k) {

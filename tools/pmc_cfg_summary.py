@@ -9,7 +9,7 @@ import os
 import sys
 
 root, nops, shape, rhs = sys.argv[1], int(sys.argv[2]), [int(v) for v in sys.argv[3].split(",")], int(sys.argv[4])
-OP_KERNELS = ("k_row_fwd_t", "k_row_inv_t", "k_pass<float")
+OP_KERNELS = ("k_row_fwd_t", "k_row_inv_t", "k_line_fwd_t", "k_line_inv_t", "k_pass<float")
 stats = glob.glob(os.path.join(root, "stats", "**", "*kernel_stats.csv"), recursive=True)
 if stats:
     with open(stats[0]) as fh:
