@@ -57,7 +57,8 @@ def parse():
     return ap.parse_args()
 
 
-PMC_FILE = os.path.join(ROOT, "profiles", "r2_pmc_kop_C2.json")   # tools/pmc_kop.sh, this round
+# tools/pmc_kop.sh summaries, newest round first (the kernels of the op change between rounds)
+PMC_FILES = [os.path.join(ROOT, "profiles", f) for f in ("r3_pmc_kop_C2.json", "r2_pmc_kop_C2.json")]
 
 
 def pmc_traffic(M, B):
@@ -65,14 +66,15 @@ def pmc_traffic(M, B):
     (tools/pmc_kop.sh): (2 x FETCH_SIZE + WRITE_SIZE) x 1 KiB summed over the op's kernels —
     FETCH_SIZE counts half the bytes of wide streaming reads on gfx950 (MI355X_MICROARCH.md
     §HBM).  None when no summary for this workload is committed."""
-    try:
-        with open(PMC_FILE) as fh:
-            d = json.load(fh)
-    except (OSError, ValueError):
-        return None
-    if d.get("M") != M or d.get("rhs") != B:
-        return None
-    return d.get("traffic_bytes_per_op")
+    for f in PMC_FILES:
+        try:
+            with open(f) as fh:
+                d = json.load(fh)
+        except (OSError, ValueError):
+            continue
+        if d.get("M") == M and d.get("rhs") == B:
+            return d.get("traffic_bytes_per_op"), os.path.relpath(f, ROOT)
+    return None, None
 
 
 def make_problem(m, B, device, seed):
@@ -294,6 +296,7 @@ def main():
     kernels = [{"pass": i, "ms": round(pass_ms[i], 4),
                 "gbs": round(pass_bytes[i] / (pass_ms[i] * 1e-3) / 1e9, 1)} for i in range(npass)]
     pcg_ms = reduce_max(float(np.median(pcg_times) * 1e3))
+    traffic, traffic_src = pmc_traffic(M, B)
 
     out = {
         "metric": "Toeplitz-FFT Kuu matvecs/sec + PCG wall-clock at M=1M inducing",
@@ -315,9 +318,9 @@ def main():
         "pcg": {"what": "compute_kn: setup + PCG(maxiter=20, tol=1e-8, precond) + R^T, B RHS",
                 "median_ms": pcg_ms, "setup_ms": setup_s * 1e3, "pcg_plus_rt_ms": solve_s * 1e3},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(M, B),
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "achieved_note": "bytes_per_launch / ms_per_step (the timed steps' own clock)",
-                     "traffic_note": "HBM bytes per batched K matvec from profiles/r2_pmc_kop_C2.json "
+                     "traffic_note": f"HBM bytes per batched K matvec from {traffic_src} "
                                      "(rocprofv3 --pmc, 2*FETCH_SIZE + WRITE_SIZE); algorithmic "
                                      "bytes per launch = bytes_per_launch",
                      "kernel": "batched K matvec = 3 pass kernels (FWD rows, CONV cols, INV rows)",

@@ -27,9 +27,11 @@
 
 namespace hgp {
 
-// occupancy of the line-inverse pass (0: from the LDS footprint)
+// occupancy of the line-inverse pass with 4-wave blocks (0: from the LDS footprint).  3 waves per
+// SIMD: the 256-point kernel (C5 axis 1) no longer spills 15 VGPRs, 1.12 -> 1.07 ms
+// (profiles/r3_l_passtime.txt)
 #ifndef HGP_MINW_LINE_INV
-#define HGP_MINW_LINE_INV 0
+#define HGP_MINW_LINE_INV 3
 #endif
 template <typename T, int H> struct LineTCfg {
   static constexpr int P = PFor<T, H>::v;
@@ -52,7 +54,7 @@ template <typename T, int H> struct LineTCfg {
   static constexpr int BLOCKS_BY_LDS = LDS_CAP / LDS;
   static constexpr int MINW_LDS = (BLOCKS_BY_LDS * ((THREADS + 63) / 64)) / 4;
   static constexpr int MINW = MINW_LDS < 1 ? 1 : (MINW_LDS > 4 ? 4 : MINW_LDS);
-  static constexpr int MINW_INV = HGP_MINW_LINE_INV > 0 ? HGP_MINW_LINE_INV : MINW;
+  static constexpr int MINW_INV = (HGP_MINW_LINE_INV > 0 && THREADS == 256) ? HGP_MINW_LINE_INV : MINW;
 };
 
 // block -> (q, r, first line i0); l = line of this thread group, t = position index
@@ -83,8 +85,14 @@ __global__ __launch_bounds__((LineTCfg<T, H>::THREADS), (LineTCfg<T, H>::MINW)) 
   const int l = (TT % 64 == 0) ? __builtin_amdgcn_readfirstlane(threadIdx.x / TT) : threadIdx.x / TT;
   const int t = threadIdx.x & (TT - 1);
   const bool valid = B.i0 + l < d.In;
-  const C2<T>* in = reinterpret_cast<const C2<T>*>(d.in.ptr) + (int64_t)B.q * d.in.q_stride +
-                    (int64_t)B.r * d.in.r_stride + (int64_t)(valid ? B.i0 + l : 0) * d.in.p_stride;
+  // one buffer resource from the block's first line (uniform; its C lines lie within 2 GiB of it,
+  // checked on the host), per-lane 32-bit offsets; positions past the line and invalid lines read
+  // at an offset past the range, which returns 0 (no clamped 64-bit addresses, no zeroing selects)
+  const C2<T>* inb0 = reinterpret_cast<const C2<T>*>(d.in.ptr) + (int64_t)B.q * d.in.q_stride +
+                      (int64_t)B.r * d.in.r_stride + (int64_t)B.i0 * d.in.p_stride;
+  const BufRsrc rin = buf_rsrc(inb0, 0x7fffffffu);
+  constexpr uint32_t DROP = 0x80000000u;
+  const uint32_t li = (uint32_t)l * (uint32_t)d.in.p_stride;
   const int in_len = d.in.len;     // <= 2H; > H (folded halves) for the R operator's n-grid input
   C2<T> va[P], vb[P];
   // fold (when L_R = 3 * 2^k < 2n) as a compile-time branch of its own straight-line loads
@@ -92,13 +100,11 @@ __global__ __launch_bounds__((LineTCfg<T, H>::THREADS), (LineTCfg<T, H>::MINW)) 
 #pragma unroll
     for (int k = 0; k < P; ++k) {
       const int p = t + TT * k;
-      C2<T> a = in[p < in_len ? p : 0];
-      if (!valid || p >= in_len) a = mk<T>(0, 0);
+      const C2<T> a = buf_ld_c2<T>(rin, (valid && p < in_len) ? (li + (uint32_t)p) * (uint32_t)sizeof(C2<T>) : DROP);
       va[k] = a;
       vb[k] = a;
       if constexpr (decltype(fold_c)::value) {
-        C2<T> hi = in[p + H < in_len ? p + H : 0];
-        if (!valid || p + H >= in_len) hi = mk<T>(0, 0);
+        const C2<T> hi = buf_ld_c2<T>(rin, (valid && p + H < in_len) ? (li + (uint32_t)(p + H)) * (uint32_t)sizeof(C2<T>) : DROP);
         va[k] = cadd<T>(a, hi);
         vb[k] = csub<T>(a, hi);
       }

@@ -256,20 +256,26 @@ __global__ __launch_bounds__((RowTCfg<T, H, G>::THREADS), (RowTCfg<T, H, G>::MIN
     } else {
       // several pairs per wave: the row bases differ between lanes, and a buffer resource must be
       // wave-uniform (a per-lane base costs a readfirstlane loop per load: 2x the VALU of the
-      // whole kernel at H = 128); plain loads at clamped positions, zeroed after
+      // whole kernel at H = 128).  One resource from the block's first row instead (its 2C rows
+      // lie within 2 GiB of it, checked on the host), per-lane 32-bit offsets; positions past the
+      // row, absent pairs and absent second rows read at an offset past the range (returns 0)
+      const T* blk = reinterpret_cast<const T*>(d.in.ptr) + (int64_t)q * d.in.q_stride + (int64_t)(2 * rb * C) * d.in.r_stride;
+      const BufRsrc rbk = buf_rsrc(blk, 0x7fffffffu);
+      constexpr uint32_t DROP = 0x80000000u;
+      const uint32_t oa = (uint32_t)(2 * l) * (uint32_t)d.in.r_stride, ob = oa + (uint32_t)d.in.r_stride;
 #pragma unroll
       for (int k = 0; k < P; ++k) {
         const int p = t + TT * k;
         const bool ok = p < in_len;
-        const T a = in_a[ok ? p : 0];
-        const T b = in_b[ok ? p : 0];
-        va[k] = mk<T>(ok && pvalid ? a : (T)0, ok && has2 ? b : (T)0);
+        const T a = buf_ld<T>(rbk, (ok && pvalid) ? (oa + (uint32_t)p) * (uint32_t)sizeof(T) : DROP);
+        const T b = buf_ld<T>(rbk, (ok && has2) ? (ob + (uint32_t)p) * (uint32_t)sizeof(T) : DROP);
+        va[k] = mk<T>(a, b);
         vb[k] = va[k];
         if constexpr (FOLD) {
           const bool ok2 = p + H < in_len;
-          const T a2 = in_a[ok2 ? p + H : 0];
-          const T b2 = in_b[ok2 ? p + H : 0];
-          const C2<T> hi = mk<T>(ok2 && pvalid ? a2 : (T)0, ok2 && has2 ? b2 : (T)0);
+          const T a2 = buf_ld<T>(rbk, (ok2 && pvalid) ? (oa + (uint32_t)(p + H)) * (uint32_t)sizeof(T) : DROP);
+          const T b2 = buf_ld<T>(rbk, (ok2 && has2) ? (ob + (uint32_t)(p + H)) * (uint32_t)sizeof(T) : DROP);
+          const C2<T> hi = mk<T>(a2, b2);
           vb[k] = csub<T>(va[k], hi);
           va[k] = cadd<T>(va[k], hi);
         }
