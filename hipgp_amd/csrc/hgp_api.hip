@@ -124,6 +124,7 @@ struct hgp_plan {
   int cg_rs_par = 0;                      // which of the two rs buffers the next step reads
   int cg_step = 0;                        // steps queued since hgp_pcg_begin
   int64_t ws_budget = (int64_t)1 << 30;
+  int64_t ws3_budget = (int64_t)4 << 30;  // 3-D default (hgp_plan_create: from the device's memory)
   bool ws_explicit = false;               // HGP_WS_MB given: the byte budget alone sets the chunks
   // 2-D operators run their RHS chunks on `nstreams` streams (the plan's own + side streams),
   // so one chunk's compute-heavy column pass overlaps another's memory-heavy row passes
@@ -173,8 +174,13 @@ struct hgp_plan {
 
 namespace {
 
-#ifndef HGP_WS3_DEFAULT
-#define HGP_WS3_DEFAULT ((int64_t)4 << 30)   // 3-D operators' default workspace budget (bytes)
+// 3-D operators' default workspace budget: an eighth of the device's memory, at most 32 GiB (36 GB
+// of a 288 GB MI355X).  The R / R^T intermediates of a C5 grid are 1 GB per RHS; with this budget
+// each of the two streams takes its whole half of the 25 RHS in one chunk, so the axis-0 pass
+// fetches the complex spectrum (0.9 GB) twice per op instead of 13 times, and each pass launches
+// twice instead of 13 times: C5 R^T 20.8 -> 19.6 ms (4 GiB -> 26 GB, profiles/r3_m_rt_ws.txt).
+#ifndef HGP_WS3_MAX
+#define HGP_WS3_MAX ((int64_t)32 << 30)
 #endif
 
 // op geometry: per-axis input/output lengths and transform length
@@ -380,7 +386,7 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
     const int64_t per = (B1 + B2) * (int64_t)cs;
     // 3-D: a larger default budget, so the axis-0 pass's spectrum lines (C5 R^T: 0.9 GB) are
     // fetched once per chunk of several RHS instead of once per RHS
-    const int64_t budget = (d == 3 && !P->ws_explicit) ? std::max<int64_t>(P->ws_budget, HGP_WS3_DEFAULT) : P->ws_budget;
+    const int64_t budget = (d == 3 && !P->ws_explicit) ? std::max<int64_t>(P->ws_budget, P->ws3_budget) : P->ws_budget;
     Qc = std::max<int64_t>(1, std::min<int64_t>((nrhs + NS - 1) / NS, budget / (per * NS)));
     // Infinity-Cache-resident chunks: where 8 RHS of a 2-D intermediate fit in ~72 MiB, each
     // stream works on 8 RHS at a time, so the intermediate a column pass writes is still in the
@@ -1300,6 +1306,11 @@ int hgp_plan_create(int device, int ndim, const int64_t* m, int dtype, int64_t m
     P->Mp *= P->n[a];
     P->prodLK *= P->LK[a];
     P->prodLR *= P->LR[a];
+  }
+  {
+    size_t tot = 0;
+    if (hipDeviceTotalMem(&tot, device) == hipSuccess && tot > 0)
+      P->ws3_budget = std::max<int64_t>((int64_t)4 << 30, std::min<int64_t>(HGP_WS3_MAX, (int64_t)(tot / 8)));
   }
   const char* wb = std::getenv("HGP_WS_MB");
   if (wb) { P->ws_budget = (int64_t)std::atoll(wb) << 20; P->ws_explicit = true; }

@@ -514,17 +514,34 @@ __global__ __launch_bounds__((RowTCfg<T, H, G>::THREADS), (RowTCfg<T, H, G>::MIN
     __syncthreads();   // every group is done with its exchange image
     int tt = t;
     asm volatile("" : "+v"(tt));
+    if (out_len == H) {
+      // rows of exactly H outputs (every power-of-two grid): the even half's positions are all
+      // outputs and the odd half's none, so the only tests left are uniform (pair / second row
+      // present) -- no per-position exec branches (the 4096-point kernels spilled 9-17 VGPRs with
+      // them, to HBM scratch)
+      T* ya = ys + (2 * l) * H;
 #pragma unroll
-    for (int k = 0; k < P; ++k) {
-      const int p = tt + TT * k;
-      const C2<T> wo = cmulc<T>(vb[k], tw_at<T, H>(tab, p));
+      for (int k = 0; k < P; ++k) {
+        const int p = tt + TT * k;
+        const C2<T> y = cadd<T>(va[k], cmulc<T>(vb[k], tw_at<T, H>(tab, p)));
+        if (pvalid) {
+          ya[p] = y.x;
+          if (has2) ya[H + p] = y.y;
+        }
+      }
+    } else {
 #pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {
-        const C2<T> y = hh == 0 ? cadd<T>(va[k], wo) : csub<T>(va[k], wo);
-        const int pp = p + hh * H;
-        if (pvalid && pp < out_len) {
-          ys[(2 * l) * out_len + pp] = y.x;
-          if (has2) ys[(2 * l + 1) * out_len + pp] = y.y;
+      for (int k = 0; k < P; ++k) {
+        const int p = tt + TT * k;
+        const C2<T> wo = cmulc<T>(vb[k], tw_at<T, H>(tab, p));
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          const C2<T> y = hh == 0 ? cadd<T>(va[k], wo) : csub<T>(va[k], wo);
+          const int pp = p + hh * H;
+          if (pvalid && pp < out_len) {
+            ys[(2 * l) * out_len + pp] = y.x;
+            if (has2) ys[(2 * l + 1) * out_len + pp] = y.y;
+          }
         }
       }
     }

@@ -22,12 +22,14 @@ def expanded_dims(dims):
 # compute_kn call (`hipgp.py:143`); re-using an idle plan of the same grid keeps its twiddle /
 # DCT tables, so only the spectrum is recomputed (hgp_plan_set_column).  Idle plans also keep
 # their scratch (workspaces, CG vectors: the next solve needs the same sizes) while all idle
-# scratch stays under HGP_POOL_MB (default 6 GiB of the 288 GB); beyond that a plan is trimmed to its
+# scratch stays under HGP_POOL_MB (default 40 GiB of the 288 GB: one C5 plan's R^T workspace is 26 GB,
+# hgp_api.hip HGP_WS3_MAX, and re-allocating it per compute_kn would cost more than it saves);
+# beyond that a plan is trimmed to its
 # tables when it goes idle (hgp_plan_trim).  release_pool() frees every idle plan, e.g. before
 # a large torch allocation (this memory is outside torch's caching allocator).
 _POOL = {}
 _POOL_MAX = 2
-_POOL_BYTES = int(os.environ.get("HGP_POOL_MB", "6144")) << 20
+_POOL_BYTES = int(os.environ.get("HGP_POOL_MB", "40960")) << 20
 
 
 def _scratch_bytes(h):
