@@ -59,8 +59,16 @@ namespace hgp {
 #ifndef HGP_ROWG_PAIRS_LONG
 #define HGP_ROWG_PAIRS_LONG 0
 #endif
+// G for the fp32 3 * 2^k rows of >= 6144 points (the 2-D R / R^T of 4096-point axes, L_R = 12288):
+// their row-pair blocks hold 2 pairs (123 KB of LDS), i.e. 32-B column segments with G = 1; G = 4
+// makes them 128 B (C4 R^T 21.0 -> 17.8 ms, R 21.6 -> 18.1 ms: row forward 5.3 -> 2.7 ms, row
+// inverse 7.2 -> 6.1 ms, the column pass 9.1 -> 9.8 ms; profiles/r3_p_tri_rows.txt)
+#ifndef HGP_ROWG_TRI
+#define HGP_ROWG_TRI 4
+#endif
 template <typename T, int H> struct RowGroup {
-  static constexpr int G = (!std::is_same<T, float>::value || !is_pow2(H)) ? 1
+  static constexpr int G = !std::is_same<T, float>::value ? 1
+                         : !is_pow2(H) ? (H >= 6144 ? HGP_ROWG_TRI : 1)
                          : H == 2048 ? HGP_ROWG_2048 : H >= 4096 ? HGP_ROWG_4096 : 1;
 };
 
