@@ -82,6 +82,10 @@
 #ifndef HGP_SEQ_PASS
 #define HGP_SEQ_PASS 0
 #endif
+// the same for the 2048-point lines (2 waves) only
+#ifndef HGP_SEQ_PASS_2048
+#define HGP_SEQ_PASS_2048 0
+#endif
 #ifndef HGP_MINW_CONTIG
 #define HGP_MINW_CONTIG 4
 #endif
@@ -540,7 +544,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
 
   if constexpr (MODE == PASS_FWD) {
     // both halves' transforms interleaved over one exchange image (hgp_fft.hpp fft_line2)
-    fft_line2<T, H, P, -1, LSTRIDE, Cfg::WAVE, (HGP_SEQ_PASS == 2 || ((HGP_SEQ_PASS || HGP_SEQ_MULTIWAVE) && !Cfg::WAVE))>(va, vb, lds, lbase, t, tab);
+    fft_line2<T, H, P, -1, LSTRIDE, Cfg::WAVE, (HGP_SEQ_PASS == 2 || ((HGP_SEQ_PASS || HGP_SEQ_MULTIWAVE || (HGP_SEQ_PASS_2048 && TT == 128)) && !Cfg::WAVE))>(va, vb, lds, lbase, t, tab);
     auto fwd_half = [&](auto half_c, C2<T>(&v)[P]) {
       constexpr int half = decltype(half_c)::value;
       if constexpr (HERM_OUT) {
@@ -575,7 +579,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
     // va ends as the even half's inverse (ye), vb as the odd half's (yo); the two halves'
     // transforms run interleaved over one exchange image (hgp_fft.hpp fft_line2)
     if constexpr (MODE == PASS_CONV) {
-      fft_line2<T, H, P, -1, LSTRIDE, Cfg::WAVE, (HGP_SEQ_PASS == 2 || ((HGP_SEQ_PASS || HGP_SEQ_MULTIWAVE) && !Cfg::WAVE))>(va, vb, lds, lbase, t, tab);
+      fft_line2<T, H, P, -1, LSTRIDE, Cfg::WAVE, (HGP_SEQ_PASS == 2 || ((HGP_SEQ_PASS || HGP_SEQ_MULTIWAVE || (HGP_SEQ_PASS_2048 && TT == 128)) && !Cfg::WAVE))>(va, vb, lds, lbase, t, tab);
       // the line's real spectrum, loaded after the forward transforms (no registers held across
       // them); L2-resident: every line of a block shares it (RHS-fastest map, XCD-grouped)
       T sre1[P];
@@ -606,7 +610,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
         vb[k] = mk<T>(vb[k].x * sre1[k], vb[k].y * sre1[k]);
       }
     } else if constexpr (MODE == PASS_CONVC) {
-      fft_line2<T, H, P, -1, LSTRIDE, Cfg::WAVE, (HGP_SEQ_PASS == 2 || ((HGP_SEQ_PASS || HGP_SEQ_MULTIWAVE) && !Cfg::WAVE))>(va, vb, lds, lbase, t, tab);
+      fft_line2<T, H, P, -1, LSTRIDE, Cfg::WAVE, (HGP_SEQ_PASS == 2 || ((HGP_SEQ_PASS || HGP_SEQ_MULTIWAVE || (HGP_SEQ_PASS_2048 && TT == 128)) && !Cfg::WAVE))>(va, vb, lds, lbase, t, tab);
       // complex spectrum at (i, r, kperm): block-uniform base + 32-bit lane offset
       const C2<T>* sbase = reinterpret_cast<const C2<T>*>(d.spec) +
                            (GRP ? (int64_t)i0 * d.spec_r : (int64_t)i0 * d.spec_i + (int64_t)r * d.spec_r);
@@ -631,7 +635,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
         }
       }
     }
-    fft_line2<T, H, P, +1, LSTRIDE, Cfg::WAVE, (HGP_SEQ_PASS == 2 || ((HGP_SEQ_PASS || HGP_SEQ_MULTIWAVE) && !Cfg::WAVE))>(va, vb, lds, lbase, t, tab);
+    fft_line2<T, H, P, +1, LSTRIDE, Cfg::WAVE, (HGP_SEQ_PASS == 2 || ((HGP_SEQ_PASS || HGP_SEQ_MULTIWAVE || (HGP_SEQ_PASS_2048 && TT == 128)) && !Cfg::WAVE))>(va, vb, lds, lbase, t, tab);
     // combine in registers: y[p] = ye + conj(W_L^p) yo, y[p+H] = ye - conj(W_L^p) yo; crop.
     const int out_len = d.out.len;
     const T* dot_re = nullptr; const T* dot_im = nullptr;
