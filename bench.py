@@ -19,7 +19,16 @@ The compute_kn timing and the per-pass event timing run BEFORE the timed steps (
 the metric), so the timed steps see the GPU at its steady clock.
 
 Multi-GPU: one process per GPU (torchrun); RHS are sharded (each rank its own 32), no
-collective inside the timed region apart from the barriers; max-over-ranks timing.
+collective inside the timed region apart from the barriers; max-over-ranks timing.  Beside the
+weak K-matvec line, two legs measured at every N (untimed for the metric, max over ranks) that
+CAN fail to scale:
+  strong        = compute_kn for a FIXED global batch (C2's 32 RHS split 32/N per rank,
+                  hipgp_amd.dist.sharded_compute_kn with the reference's all-RHS break rule:
+                  one all-reduce(MIN) of a device flag per PCG iteration, RCCL on GPUs)
+  elbo_step     = one mean-field `elbo_and_grad` minibatch of 32 observations sharded 32/N
+                  (hipgp_amd.dist.sharded_elbo_and_grad: fused Kuf + compute_kn + statistics and
+                  the all-reduce of the 2 M' natural-gradient sums, hipgp.py:234-266), and that
+                  all-reduce (33.5 MB at C2) timed alone
 """
 import argparse
 import json
@@ -54,6 +63,8 @@ def parse():
                     help="rehearsal on a 1-GPU box: every rank uses cuda:0 (with --backend gloo)")
     ap.add_argument("--kop-only", action="store_true",
                     help="only the timed K matvec steps (for rocprofv3 --pmc passes)")
+    ap.add_argument("--no-legs", action="store_true", help="skip the strong-scaling / ELBO-step legs")
+    ap.add_argument("--legs-reps", type=int, default=3)
     return ap.parse_args()
 
 
@@ -170,6 +181,61 @@ def cpu_baseline(m, B, grids_np, seed, threads=None):
             "pcg_s": pcg_s, "pcg_rhs": B}
 
 
+def multi_gpu_legs(args, m, grids, kf, device, dist, world, rank, reps):
+    """The fixed-global-batch legs (see the module docstring); every timing is a barrier +
+    synchronise on both sides, max over ranks, median of `reps`."""
+    import torch.distributed as tdist
+    import ziggy.hipgp as hg
+    import ziggy.kernels as zk
+    from hipgp_amd import dist as hdist
+    G = args.rhs                                              # C2's global batch
+    sl = hdist.rhs_shard(G, world, rank)
+    g = torch.Generator(device="cpu").manual_seed(4321)       # the SAME minibatch on every rank
+    x = (torch.rand(G, 2, generator=g, dtype=torch.float32) * 2 - 1).to(device)
+    y = (torch.sin(3 * x[:, :1]) * torch.cos(2 * x[:, 1:]) + 0.1 * torch.randn(G, 1, generator=g).to(device))
+    s = torch.full((G, 1), 0.1, device=device)
+    mod = hg.MeanFieldToeplitzGP(zk.SqExp(dtype=torch.float32), grids, num_obs=100_000, sig2_init=1.,
+                                 ell_init=.01, learn_kernel=False, jitter_val=1e-3, dtype=torch.float32)
+    mod = mod.cuda_params(device.index)
+    Knm_local, _ = mod._make_grams(x[sl])
+
+    def timed(fn):
+        out = []
+        fn()
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            if dist:
+                tdist.barrier()
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            if dist:
+                tdist.barrier()
+            out.append(time.perf_counter() - t0)
+        v = float(np.median(out))
+        if dist:
+            tt = torch.tensor([v], device=device if args.backend == "nccl" else "cpu", dtype=torch.float64)
+            tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
+            v = float(tt.item())
+        return v * 1e3
+
+    grp = None
+    # N = 1: the plan's own break test is the all-RHS rule (no process group to reduce over)
+    kn_ms = timed(lambda: hdist.sharded_compute_kn(mod, Knm_local, maxiter_cg=20, tol=1e-8, exact_break=dist))
+    elbo_ms = timed(lambda: hdist.sharded_elbo_and_grad(mod, x, y, s, maxiter_cg=20, tol=1e-8, exact_break=dist))
+    Mp = mod.Mprime
+    stats = [torch.zeros(Mp, device=device), torch.zeros(Mp, device=device)]
+    ar_ms = timed(lambda: [hdist._allreduce_(t, grp) for t in stats]) if dist else 0.0
+    return {"strong": {"what": "compute_kn (set-up + PCG(20, tol 1e-8, precond, all-RHS break over ranks) + R^T) "
+                                "for a fixed global batch split over the ranks",
+                       "global_rhs": G, "rhs_per_rank": sl.stop - sl.start, "ms": kn_ms,
+                       "rhs_per_s": G / (kn_ms * 1e-3), "scaling": "strong"},
+            "elbo_step": {"what": "mean-field elbo_and_grad minibatch (Kuf + compute_kn + statistics + "
+                                  "all-reduce of the 2 M' natural-gradient sums), batch split over the ranks",
+                          "global_batch": G, "ms": elbo_ms, "stats_allreduce_ms": ar_ms,
+                          "stats_allreduce_bytes": 2 * Mp * 4, "backend": args.backend if dist else None}}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -259,6 +325,10 @@ def main():
             fn()
             pass_ms.append(time_events(fn, 20, stream))
 
+    legs = None
+    if not args.kop_only and not args.no_legs:
+        legs = multi_gpu_legs(args, m, grids, kf, device, dist, world, rank, args.legs_reps)
+
     # ---- the metric: W warmup + K timed batched K matvec steps --------------------------------
     settle()
     for _ in range(args.warmup):
@@ -328,6 +398,8 @@ def main():
                      "event_op_ms": op_ms, "event_achieved": achieved_ev,
                      "event_frac": achieved_ev / HBM_PEAK_GBS, "passes": kernels},
     }
+    if legs is not None:
+        out.update(legs)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         grids_np = [np.linspace(-1, 1, m, dtype=np.float32) for _ in range(2)]
         out["cpu_baseline"] = cpu_baseline(m, B, grids_np, seed=7, threads=args.cpu_threads)

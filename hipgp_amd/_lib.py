@@ -30,6 +30,7 @@ EXPORTS = (
     "hgp_block_stats", "hgp_sym_toeplitz_dqf", "hgp_plan_column_grad",
     "hgp_plan_dqf", "hgp_pcg_local_flag", "hgp_pcg_set_done", "hgp_pcg_iters",
     "hgp_slab_info", "hgp_slab_pass", "hgp_plan_mem", "hgp_plan_trim",
+    "hgp_slab_pass_ex", "hgp_slab_cg_xr", "hgp_slab_cg_check", "hgp_slab_cg_p",
 )
 KERN_SQEXP, KERN_MATERN12, KERN_MATERN32, KERN_MATERN52, KERN_GNEITING = 0, 1, 2, 3, 4
 
@@ -84,6 +85,10 @@ def lib():
         "hgp_plan_mem": (i32, [vp, pi64, pi64]),
         "hgp_plan_trim": (i32, [vp]),
         "hgp_slab_pass": (i32, [vp, i32, i32, vp, vp, i64, i64, i64, i64]),
+        "hgp_slab_pass_ex": (i32, [vp, i32, i32, vp, vp, i64, i64, i64, i64, vp, vp, vp]),
+        "hgp_slab_cg_xr": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, vp]),
+        "hgp_slab_cg_check": (i32, [vp, vp, i64, dbl, vp, vp]),
+        "hgp_slab_cg_p": (i32, [vp, vp, vp, vp, vp, i64, i64, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

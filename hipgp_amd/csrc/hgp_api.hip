@@ -116,6 +116,8 @@ struct hgp_plan {
   DevBuf ws1, ws2, set1, set2, setM1, setM2, setC;
   // CG state
   DevBuf r, z, p, Ap, part_op, part_u, part_f, scal, flags, bT, xT;
+  // slab-sharded PCG (hgp_slab_cg_*): fused-dot / update partials and per-RHS alpha / beta
+  DevBuf slab_part, slab_coef;
   int64_t cg_nrhs = 0;
   int cg_precond = 0, cg_layout = 0;
   void* cg_x_user = nullptr;
@@ -907,9 +909,19 @@ SlabGeom slab_geom(const hgp_plan* P, int op) {
   return SlabGeom{g.L[1], compact_stride(g.L[2])};
 }
 
+// the INV stage's fused dot: per-row-pair partials [q][Rn] -> dot_out[q] (fixed order)
+template <typename T>
+int slab_dot_parts(hgp_plan* P, PassDesc& D, const void* dotv, int64_t nrhs, int64_t Rn) {
+  if (dotv == nullptr) return 0;
+  HGP_TRY(P->slab_part.ensure((size_t)(nrhs * Rn) * sizeof(T)));
+  D.dot = dotv;
+  D.partial = P->slab_part.ptr;
+  return 0;
+}
+
 template <typename T>
 int slab_pass_t(hgp_plan* P, int op, int stage, const void* in, void* out, int64_t nrhs, int64_t nrows, int64_t g0,
-                int64_t ng) {
+                int64_t ng, const void* dotv, void* dot_out, const int* done) {
   if (P->grid_r && (op == HGP_OP_R || op == HGP_OP_RT))
     return fail(HGP_E_UNSUPPORTED, "grid-block sharding of R / R^T with fp64 lines of more than 16384 points");
   const OpGeom g = op_geom(P, op);
@@ -918,6 +930,11 @@ int slab_pass_t(hgp_plan* P, int op, int stage, const void* in, void* out, int64
   const int conv_mode = g.spec_kind == SPEC_REAL ? PASS_CONV : PASS_CONVC;
   hipStream_t st = P->stream;
   const size_t cs = sizeof(C2<T>);
+  auto sbase = [&]() {      // every slab pass is skipped once the slab PCG's device flag is set
+    PassDesc D = base_desc();
+    D.done = done;
+    return D;
+  };
   auto rowt = [&](int inv, PassDesc& D, int64_t H) -> int {
     hipError_t e = launch_rowt<T>((int)H, inv, EPI_OUT, D, st, 0);
     if (e == hipErrorNotSupported)
@@ -938,7 +955,7 @@ int slab_pass_t(hgp_plan* P, int op, int stage, const void* in, void* out, int64
     const int64_t inner = d == 2 ? 1 : sg.inner;
     const int64_t P0 = std::max(g.in[0], g.out[0]);
     if (ng * nrhs * P0 * inner >= ((int64_t)1 << 31)) return fail(HGP_E_UNSUPPORTED, "slab too large");
-    PassDesc Sd = base_desc();
+    PassDesc Sd = sbase();
     Sd.in = View{const_cast<void*>(in), 0, 0, inner, (int)g.in[0]};
     Sd.out = View{out, 0, 0, inner, (int)g.out[0]};
     Sd.seg_ws = (int)nrows;
@@ -960,7 +977,7 @@ int slab_pass_t(hgp_plan* P, int op, int stage, const void* in, void* out, int64
       // the row kernels address one RHS's columns with 32-bit byte offsets from its base
       if (sg.NG * nrhs * nrows * (int64_t)cs >= ((int64_t)1 << 31))
         return fail(HGP_E_UNSUPPORTED, "slab too large: NG * nrhs * nrows complex values exceed 2 GiB");
-      PassDesc D = base_desc();
+      PassDesc D = sbase();
       D.tw = g.tw[1].ptr; D.Q = (int)nrhs; D.Rn = (int)((nrows + 1) / 2); D.nrows = (int)nrows;
       if (stage == HGP_SLAB_FWD) {
         D.in = View{const_cast<void*>(in), nrows * g.in[1], g.in[1], 1, (int)g.in[1]};
@@ -969,11 +986,14 @@ int slab_pass_t(hgp_plan* P, int op, int stage, const void* in, void* out, int64
       }
       D.in = View{const_cast<void*>(in), nrows, nrhs * nrows, 1, 0};
       D.out = View{out, nrows * g.out[1], g.out[1], 1, (int)g.out[1]};
-      return rowt(1, D, H1);
+      HGP_TRY(slab_dot_parts<T>(P, D, dotv, nrhs, D.Rn));
+      HGP_TRY(rowt(1, D, H1));
+      if (dotv != nullptr) reduce_rows<T>(D.partial, D.Rn, (int)nrhs, dot_out, st);
+      return 0;
     }
     if (stage != HGP_SLAB_CONV) return fail(HGP_E_ARG, "bad slab stage");
     const int64_t P0 = std::max(g.in[0], g.out[0]);
-    PassDesc Bd = base_desc();
+    PassDesc Bd = sbase();
     Bd.in = View{const_cast<void*>(in), P0, nrhs * P0, 1, (int)g.in[0]};
     Bd.out = View{out, P0, nrhs * P0, 1, (int)g.out[0]};
     const size_t se = g.spec_kind == SPEC_REAL ? sizeof(T) : cs;
@@ -992,32 +1012,35 @@ int slab_pass_t(hgp_plan* P, int op, int stage, const void* in, void* out, int64
     HGP_TRY(P->ws1.ensure((size_t)wsz * cs));
     C2<T>* w1 = reinterpret_cast<C2<T>*>(P->ws1.ptr);
     if (stage == HGP_SLAB_FWD) {
-      PassDesc P1 = base_desc();   // axis 2: real row pairs -> w1 [q][i][i1][c2]
+      PassDesc P1 = sbase();   // axis 2: real row pairs -> w1 [q][i][i1][c2]
       P1.in = View{const_cast<void*>(in), nrows * g.in[1] * g.in[2], g.in[2], 1, (int)g.in[2]};
       P1.out = View{w1, nrows * r1 * Sl, Sl, 1, 0};
       P1.tw = g.tw[2].ptr; P1.Q = (int)nrhs; P1.Rn = (int)((nrows * r1 + 1) / 2); P1.nrows = (int)(nrows * r1);
       HGP_TRY(launch<T>((int)H2, PASS_FWD, LAY_RP, P1, nrhs * P1.Rn, st));
-      PassDesc P2 = base_desc();   // axis 1 (strided): w1 -> E [k1][q][i][c2]
+      PassDesc P2 = sbase();   // axis 1 (strided): w1 -> E [k1][q][i][c2]
       P2.in = View{w1, nrows * r1 * Sl, r1 * Sl, Sl, (int)r1};
       P2.out = View{out, nrows * Sl, Sl, nrhs * nrows * Sl, (int)L1};
       P2.tw = g.tw[1].ptr; P2.Q = (int)nrhs; P2.Rn = (int)nrows; P2.In = (int)(H2 + 1);
       return launch<T>((int)(L1 / 2), PASS_FWD, LAY_STRIDED, P2, 0, st);
     }
-    PassDesc P4 = base_desc();     // axis 1 inverse (strided): E [k1][q][o][c2] -> w1 [q][o][o1][c2]
+    PassDesc P4 = sbase();     // axis 1 inverse (strided): E [k1][q][o][c2] -> w1 [q][o][o1][c2]
     P4.in = View{const_cast<void*>(in), nrows * Sl, Sl, nrhs * nrows * Sl, (int)L1};
     P4.out = View{w1, nrows * r1 * Sl, r1 * Sl, Sl, (int)r1};
     P4.tw = g.tw[1].ptr; P4.Q = (int)nrhs; P4.Rn = (int)nrows; P4.In = (int)(H2 + 1);
     HGP_TRY(launch<T>((int)(L1 / 2), PASS_INV, LAY_STRIDED, P4, 0, st));
-    PassDesc P5 = base_desc();     // axis 2 inverse: w1 -> real rows (crop)
+    PassDesc P5 = sbase();     // axis 2 inverse: w1 -> real rows (crop)
     P5.in = View{w1, nrows * r1 * Sl, Sl, 1, (int)g.L[2]};
     P5.out = View{out, nrows * r1 * g.out[2], g.out[2], 1, (int)g.out[2]};
     P5.tw = g.tw[2].ptr; P5.Q = (int)nrhs; P5.Rn = (int)((nrows * r1 + 1) / 2); P5.nrows = (int)(nrows * r1);
-    return launch<T>((int)H2, PASS_INV, LAY_RP, P5, nrhs * P5.Rn, st);
+    HGP_TRY(slab_dot_parts<T>(P, P5, dotv, nrhs, P5.Rn));
+    HGP_TRY(launch<T>((int)H2, PASS_INV, LAY_RP, P5, nrhs * P5.Rn, st));
+    if (dotv != nullptr) reduce_rows<T>(P5.partial, P5.Rn, (int)nrhs, dot_out, st);
+    return 0;
   }
   if (stage != HGP_SLAB_CONV) return fail(HGP_E_ARG, "bad slab stage");
   const int64_t P0 = std::max(g.in[0], g.out[0]);
   if (ng * nrhs * P0 * Sl >= ((int64_t)1 << 31)) return fail(HGP_E_UNSUPPORTED, "slab too large for 32-bit element offsets");
-  PassDesc P3 = base_desc();       // axis 0 conv (strided over i), lines (k1, c2) of each RHS
+  PassDesc P3 = sbase();       // axis 0 conv (strided over i), lines (k1, c2) of each RHS
   P3.in = View{const_cast<void*>(in), P0 * Sl, nrhs * P0 * Sl, Sl, (int)g.in[0]};
   P3.out = View{out, P0 * Sl, nrhs * P0 * Sl, Sl, (int)g.out[0]};
   const size_t se = g.spec_kind == SPEC_REAL ? sizeof(T) : cs;
@@ -1796,8 +1819,8 @@ int hgp_slab_info(const hgp_plan* plan, int op, int64_t* ngroups, int64_t* inner
   return 0;
 }
 
-int hgp_slab_pass(hgp_plan* plan, int op, int stage, const void* in, void* out, int64_t nrhs, int64_t nrows,
-                  int64_t g0, int64_t ng) {
+int hgp_slab_pass_ex(hgp_plan* plan, int op, int stage, const void* in, void* out, int64_t nrhs, int64_t nrows,
+                     int64_t g0, int64_t ng, const void* dotv, void* dot_out, const int* done) {
   HGP_TRY(check_plan(plan));
   if (!plan->have_spec) return fail(HGP_E_STATE, "hgp_plan_set_column has not been called");
   if (op < HGP_OP_K || op > HGP_OP_R) return fail(HGP_E_ARG, "bad op");
@@ -1805,9 +1828,86 @@ int hgp_slab_pass(hgp_plan* plan, int op, int stage, const void* in, void* out, 
   if (stage < HGP_SLAB_FWD || stage > HGP_SLAB_CONV_A2A) return fail(HGP_E_ARG, "bad slab stage");
   if (nrhs < 0 || (nrhs > 0 && (in == nullptr || out == nullptr))) return fail(HGP_E_ARG, "bad in/out/nrhs");
   if (stage != HGP_SLAB_CONV && in == out) return fail(HGP_E_ARG, "in and out must not alias (row stages)");
+  if (dotv != nullptr && (stage != HGP_SLAB_INV || dot_out == nullptr))
+    return fail(HGP_E_ARG, "a fused dot (dotv, dot_out) is an HGP_SLAB_INV option and needs both pointers");
   if (nrhs == 0) return 0;
   HGP_TRY(use_device(plan));
-  return DISPATCH(plan, slab_pass_t, plan, op, stage, in, out, nrhs, nrows, g0, ng);
+  return DISPATCH(plan, slab_pass_t, plan, op, stage, in, out, nrhs, nrows, g0, ng, dotv, dot_out, done);
+}
+
+int hgp_slab_pass(hgp_plan* plan, int op, int stage, const void* in, void* out, int64_t nrhs, int64_t nrows,
+                  int64_t g0, int64_t ng) {
+  return hgp_slab_pass_ex(plan, op, stage, in, out, nrhs, nrows, g0, ng, nullptr, nullptr, nullptr);
+}
+
+}  // extern "C"
+
+// ---- slab-sharded PCG scalars (cg.py:63-78 on all-reduced per-RHS dots) --------------------
+template <typename T>
+int slab_cg_xr_t(hgp_plan* P, void* x, void* r, const void* p, const void* Ap, const void* rs, const void* pAp,
+                 void* rr, int64_t nrhs, int64_t M, const int* done) {
+  hipStream_t st = P->stream;
+  if (M == 0) {             // a rank without rows: its share of r.r is 0
+    HIP_TRY(hipMemsetAsync(rr, 0, (size_t)nrhs * sizeof(T), st));
+    return 0;
+  }
+  const int np = update_np(M);
+  HGP_TRY(P->slab_coef.ensure((size_t)nrhs * sizeof(T)));
+  HGP_TRY(P->slab_part.ensure((size_t)(nrhs * np) * sizeof(T)));
+  cg_alpha<T>(pAp, 1, (int)nrhs, rs, P->slab_coef.ptr, done, st);                 // alpha = rs / p.Ap
+  cg_update_xr<T>(x, r, p, Ap, P->slab_coef.ptr, P->slab_part.ptr, nrhs, M, done, st);
+  reduce_rows<T>(P->slab_part.ptr, np, (int)nrhs, rr, st);                         // local r.r
+  return 0;
+}
+
+template <typename T>
+int slab_cg_check_t(hgp_plan* P, const void* rr, int64_t nrhs, double tol, int* done, int* iters) {
+  // rr are the all-reduced r.r: done = the iteration when every sqrt(r.r) < tol (cg.py:69-71);
+  // k_cg_check writes rnew = the reduced sums again, so it gets a scratch copy
+  HGP_TRY(P->slab_coef.ensure((size_t)nrhs * sizeof(T)));
+  cg_check<T>(rr, 1, (int)nrhs, tol, P->slab_coef.ptr, done, iters, P->stream);
+  return 0;
+}
+
+template <typename T>
+int slab_cg_p_t(hgp_plan* P, void* p, const void* z, void* rs, const void* zr, int64_t nrhs, int64_t M,
+                const int* done) {
+  HGP_TRY(P->slab_coef.ensure((size_t)nrhs * sizeof(T)));
+  cg_beta<T>(zr, 1, (int)nrhs, rs, P->slab_coef.ptr, done, P->stream);           // beta = zr / rs; rs = zr
+  if (M > 0) cg_update_p<T>(p, z, P->slab_coef.ptr, nrhs, M, done, P->stream);    // p = z + beta p
+  return 0;
+}
+
+extern "C" {
+
+static int slab_cg_args(const hgp_plan* plan, int64_t nrhs, int64_t M, const int* done) {
+  HGP_TRY(check_plan(plan));
+  if (nrhs < 1 || M < 0 || done == nullptr) return fail(HGP_E_ARG, "bad nrhs / M / done");
+  return 0;
+}
+
+int hgp_slab_cg_xr(hgp_plan* plan, void* x, void* r, const void* p, const void* Ap, const void* rs, const void* pAp,
+                   void* rr, int64_t nrhs, int64_t M, const int* done) {
+  HGP_TRY(slab_cg_args(plan, nrhs, M, done));
+  if (rs == nullptr || pAp == nullptr || rr == nullptr || (M > 0 && (!x || !r || !p || !Ap)))
+    return fail(HGP_E_ARG, "null vector / scalar");
+  HGP_TRY(use_device(plan));
+  return DISPATCH(plan, slab_cg_xr_t, plan, x, r, p, Ap, rs, pAp, rr, nrhs, M, done);
+}
+
+int hgp_slab_cg_check(hgp_plan* plan, const void* rr, int64_t nrhs, double tol, int* done, int* iters) {
+  HGP_TRY(slab_cg_args(plan, nrhs, 0, done));
+  if (rr == nullptr || iters == nullptr) return fail(HGP_E_ARG, "null rr / iters");
+  HGP_TRY(use_device(plan));
+  return DISPATCH(plan, slab_cg_check_t, plan, rr, nrhs, tol, done, iters);
+}
+
+int hgp_slab_cg_p(hgp_plan* plan, void* p, const void* z, void* rs, const void* zr, int64_t nrhs, int64_t M,
+                  const int* done) {
+  HGP_TRY(slab_cg_args(plan, nrhs, M, done));
+  if (rs == nullptr || zr == nullptr || (M > 0 && (!p || !z))) return fail(HGP_E_ARG, "null vector / scalar");
+  HGP_TRY(use_device(plan));
+  return DISPATCH(plan, slab_cg_p_t, plan, p, z, rs, zr, nrhs, M, done);
 }
 
 int hgp_plan_info(const hgp_plan* plan, int64_t* M, int64_t* Mprime, int64_t* L_K, int64_t* L_R) {
@@ -1823,7 +1923,9 @@ int hgp_plan_info(const hgp_plan* plan, int64_t* M, int64_t* Mprime, int64_t* L_
 
 int64_t plan_scratch_bytes(const hgp_plan* P) {
   const DevBuf* bufs[] = {&P->ws1, &P->ws2, &P->set1, &P->set2, &P->setM1, &P->setM2, &P->setC, &P->r, &P->z,
-                          &P->p, &P->Ap, &P->part_op, &P->part_u, &P->part_f, &P->scal, &P->bT, &P->xT};
+                          &P->p, &P->Ap, &P->part_op, &P->part_u, &P->part_f, &P->scal, &P->bT, &P->xT,
+                          &P->gridA, &P->gridB,    // the full-grid R / R^T buffers (grid_r plans)
+                          &P->slab_part, &P->slab_coef};
   int64_t b = 0;
   for (const DevBuf* d : bufs) b += (int64_t)d->bytes;
   return b;
@@ -1837,7 +1939,7 @@ int hgp_plan_mem(const hgp_plan* plan, int64_t* scratch_bytes, int64_t* table_by
     for (int a = 0; a < 3; ++a)
       b += (int64_t)(plan->twK[a].bytes + plan->twR[a].bytes + plan->tw64K[a].bytes + plan->tw64R[a].bytes +
                      plan->bsPre[a].bytes + plan->bsPost[a].bytes + plan->bsFilt[a].bytes);
-    b += (int64_t)(plan->specK.bytes + plan->specI.bytes + plan->specR.bytes + plan->Dm3.bytes);
+    b += (int64_t)(plan->specK.bytes + plan->specI.bytes + plan->specR.bytes + plan->specRg.bytes + plan->Dm3.bytes);
     *table_bytes = b;
   }
   return 0;
@@ -1852,7 +1954,8 @@ int hgp_plan_trim(hgp_plan* plan) {
     if (plan->side[i]) HIP_TRY(hipStreamSynchronize(plan->side[i]));
   DevBuf* bufs[] = {&plan->ws1, &plan->ws2, &plan->set1, &plan->set2, &plan->setM1, &plan->setM2, &plan->setC,
                     &plan->r, &plan->z, &plan->p, &plan->Ap, &plan->part_op, &plan->part_u, &plan->part_f,
-                    &plan->scal, &plan->bT, &plan->xT, &plan->gridA, &plan->gridB};
+                    &plan->scal, &plan->bT, &plan->xT, &plan->gridA, &plan->gridB, &plan->slab_part,
+                    &plan->slab_coef};
   for (DevBuf* b : bufs) b->release();
   plan->drop_graph();                               // its kernels addressed the freed workspaces
   plan->last_apply = hgp_plan::ApplyKey();

@@ -112,6 +112,7 @@ template <> struct PMax<double> { static constexpr int v = 8; };
 // Transform half-lengths: powers of two, and H = 3 * 2^j (j >= 2, "tri": the R / R^T lengths
 // L_R = 3 * 2^k that replace the next power of two where they are shorter, hgp_plan_create).
 constexpr bool is_pow2(int h) { return h > 0 && (h & (h - 1)) == 0; }
+constexpr int ilog2c(int h) { return h <= 1 ? 0 : 1 + ilog2c(h >> 1); }
 constexpr bool is_tri(int h) { return h >= 12 && h % 3 == 0 && is_pow2(h / 3); }
 // points per thread: P = min(H, PMax) for powers of two, 12 for tri lengths (TT = H / 12 then
 // stays a power of two, and 12 holds the radix-3 stage)

@@ -22,14 +22,28 @@ def expanded_dims(dims):
 # compute_kn call (`hipgp.py:143`); re-using an idle plan of the same grid keeps its twiddle /
 # DCT tables, so only the spectrum is recomputed (hgp_plan_set_column).  Idle plans also keep
 # their scratch (workspaces, CG vectors: the next solve needs the same sizes) while all idle
-# scratch stays under HGP_POOL_MB (default 40 GiB of the 288 GB: one C5 plan's R^T workspace is 26 GB,
-# hgp_api.hip HGP_WS3_MAX, and re-allocating it per compute_kn would cost more than it saves);
-# beyond that a plan is trimmed to its
-# tables when it goes idle (hgp_plan_trim).  release_pool() frees every idle plan, e.g. before
-# a large torch allocation (this memory is outside torch's caching allocator).
+# scratch on a device stays under HGP_POOL_MB (default: an eighth of the device's memory, the
+# same share as the 3-D workspace budget of hgp_api.hip -- 36 GB of the 288 GB: one C5 plan's
+# R^T workspace is 26 GB, and re-allocating it per compute_kn would cost more than it saves);
+# beyond that a plan is trimmed to its tables when it goes idle (hgp_plan_trim).
+# release_pool() frees every idle plan, e.g. before a large torch allocation (this memory is
+# outside torch's caching allocator).
 _POOL = {}
 _POOL_MAX = 2
-_POOL_BYTES = int(os.environ.get("HGP_POOL_MB", "40960")) << 20
+_POOL_ENV = os.environ.get("HGP_POOL_MB")
+_POOL_DEV = {}
+_WS_WARN_BYTES = 4 << 30
+_ws_warned = False
+
+
+def pool_budget(device_index):
+    """Idle-plan scratch cap of one device in bytes (HGP_POOL_MB, else 1/8 of its memory)."""
+    if _POOL_ENV is not None:
+        return int(_POOL_ENV) << 20
+    b = _POOL_DEV.get(device_index)
+    if b is None:
+        b = _POOL_DEV[device_index] = torch.cuda.get_device_properties(device_index).total_memory // 8
+    return b
 
 
 def _scratch_bytes(h):
@@ -38,9 +52,10 @@ def _scratch_bytes(h):
     return b.value
 
 
-def pool_scratch_bytes():
-    """Device bytes of scratch held by idle pooled plans."""
-    return sum(_scratch_bytes(h) for hs in _POOL.values() for h in hs)
+def pool_scratch_bytes(device_index=None):
+    """Device bytes of scratch held by idle pooled plans (of one device, or all)."""
+    return sum(_scratch_bytes(h) for k, hs in _POOL.items() for h in hs
+               if device_index is None or k[2] == device_index)
 
 
 def release_pool():
@@ -98,6 +113,29 @@ class ToeplitzPlan:
             raise ValueError(f"{name} must be (nrhs, {ncols}), got {tuple(t.shape)}")
         return t.contiguous()
 
+    def mem(self):
+        """{"scratch": bytes, "tables": bytes} the plan holds outside torch's allocator
+        (hgp_plan_mem): workspaces + CG vectors, and spectra + twiddle tables."""
+        sb, tb = ctypes.c_int64(0), ctypes.c_int64(0)
+        check(lib().hgp_plan_mem(self._h, ctypes.byref(sb), ctypes.byref(tb)))
+        return {"scratch": sb.value, "tables": tb.value}
+
+    def _report_ws(self):
+        """The first time in a process that a plan's scratch passes 4 GiB, say so once: the 3-D
+        operators size their workspace from the device memory (an eighth, at most 32 GiB, so the
+        axis-0 spectrum is read once per chunk of many RHS), which a process sharing the GPU
+        should know about (HGP_WS_MB caps it; release_pool() frees idle plans)."""
+        global _ws_warned
+        if _ws_warned:
+            return
+        sb = _scratch_bytes(self._h)
+        if sb > _WS_WARN_BYTES:
+            _ws_warned = True
+            import warnings
+            warnings.warn(f"hipgp plan {self.dims} holds {sb / 2**30:.1f} GiB of device scratch outside torch's "
+                          "allocator (workspace budget: HGP_WS_MB; idle plans: hipgp_amd.plan.release_pool())",
+                          ResourceWarning, stacklevel=3)
+
     # -- spectrum ----------------------------------------------------------------------------
     def set_column(self, column, jitter=0.0, clamp_min=1e-6, count_clamped=False):
         """column: kernel-evaluated first row k(x0, x_j), (M,) on the plan device."""
@@ -131,6 +169,8 @@ class ToeplitzPlan:
         self._bind_stream()
         check(lib().hgp_toeplitz_apply(self._h, int(op), ctypes.c_void_p(x.data_ptr()),
                                        ctypes.c_void_p(out.data_ptr()), x.shape[0]))
+        if not _ws_warned:
+            self._report_ws()
         return out
 
     def column_grad(self, op, x, g):
@@ -186,6 +226,8 @@ class ToeplitzPlan:
         check(lib().hgp_pcg_solve(self._h, ctypes.c_void_p(b.data_ptr()), ctypes.c_void_p(x.data_ptr()),
                                   nrhs, int(maxiter), float(tol), int(bool(precond)),
                                   int(layout), ctypes.byref(iters) if return_iters else None))
+        if not _ws_warned:
+            self._report_ws()
         return (x, iters.value) if return_iters else x
 
     def pcg_steps(self, b, maxiter, tol, precond=True, callback=None, layout=_lib.LAYOUT_ROWS):
@@ -254,7 +296,7 @@ class ToeplitzPlan:
             try:
                 idle = _POOL.setdefault(self._key, [])
                 if len(idle) < _POOL_MAX:
-                    if pool_scratch_bytes() + _scratch_bytes(h) > _POOL_BYTES:
+                    if pool_scratch_bytes(self._key[2]) + _scratch_bytes(h) > pool_budget(self._key[2]):
                         lib().hgp_plan_trim(h)
                     idle.append(h)          # stream-ordered re-use (see _POOL)
                 else:

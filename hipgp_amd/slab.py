@@ -61,7 +61,8 @@ def _allreduce(t, group):
 
 
 class HipSlabEngine:
-    """The slab stages on libhipgp (hgp_slab_pass), one replicated plan per rank."""
+    """The slab stages on libhipgp (hgp_slab_pass_ex), one replicated plan per rank, and the
+    slab PCG's vector / scalar updates (hgp_slab_cg_*) on device buffers."""
 
     def __init__(self, plan):
         self.plan = plan
@@ -76,22 +77,49 @@ class HipSlabEngine:
         check(lib().hgp_slab_info(self.plan._h, int(op), ctypes.byref(ng), ctypes.byref(inner)))
         return ng.value, inner.value
 
-    def _run(self, op, stage, x, y, nrhs, nrows, g0=0, ng=0):
-        self.plan._bind_stream()
-        check(lib().hgp_slab_pass(self.plan._h, int(op), int(stage), ctypes.c_void_p(x.data_ptr()),
-                                  ctypes.c_void_p(y.data_ptr()), nrhs, nrows, g0, ng))
+    @staticmethod
+    def _p(t):
+        return ctypes.c_void_p(None if t is None else t.data_ptr())
 
-    def fwd(self, op, x, nrows, E):
-        self._run(op, _lib.SLAB_FWD, x.contiguous(), E, x.shape[0], nrows)
+    def _run(self, op, stage, x, y, nrhs, nrows, g0=0, ng=0, dotv=None, dot_out=None, done=None):
+        self.plan._bind_stream()
+        check(lib().hgp_slab_pass_ex(self.plan._h, int(op), int(stage), self._p(x), self._p(y), nrhs, nrows, g0, ng,
+                                     self._p(dotv), self._p(dot_out), self._p(done)))
+
+    def fwd(self, op, x, nrows, E, done=None):
+        self._run(op, _lib.SLAB_FWD, x.contiguous(), E, x.shape[0], nrows, done=done)
 
     def conv(self, op, lines, g0, ng, nrhs):
         self._run(op, _lib.SLAB_CONV, lines, lines, nrhs, 0, g0, ng)
 
-    def conv_a2a(self, op, recv, send, g0, ng, nrhs, ws):
-        self._run(op, _lib.SLAB_CONV_A2A, recv, send, nrhs, ws, g0, ng)
+    def conv_a2a(self, op, recv, send, g0, ng, nrhs, ws, done=None):
+        self._run(op, _lib.SLAB_CONV_A2A, recv, send, nrhs, ws, g0, ng, done=done)
 
-    def inv(self, op, E, nrows, y):
-        self._run(op, _lib.SLAB_INV, E, y, y.shape[0], nrows)
+    def inv(self, op, E, nrows, y, dotv=None, dot_out=None, done=None):
+        self._run(op, _lib.SLAB_INV, E, y, y.shape[0], nrows, dotv=dotv, dot_out=dot_out, done=done)
+
+    # -- slab PCG updates (cg.py:63-78); dots already all-reduced; no-ops once done ----------
+    def dot(self, a, c, out):
+        if a.shape[1] == 0:
+            out.zero_()
+            return
+        check(lib().hgp_rowdot(_lib.dtype_code(a.dtype), self._p(a), self._p(c), self._p(out), a.shape[0],
+                               a.shape[1], _lib.stream_ptr(a.device)))
+
+    def cg_xr(self, x, r, p, Ap, rs, pAp, rr, done):
+        self.plan._bind_stream()
+        check(lib().hgp_slab_cg_xr(self.plan._h, self._p(x), self._p(r), self._p(p), self._p(Ap), self._p(rs),
+                                   self._p(pAp), self._p(rr), x.shape[0], x.shape[1], self._p(done)))
+
+    def cg_check(self, rr, tol, done, iters):
+        self.plan._bind_stream()
+        check(lib().hgp_slab_cg_check(self.plan._h, self._p(rr), rr.shape[0], float(tol), self._p(done),
+                                      self._p(iters)))
+
+    def cg_p(self, p, z, rs, zr, done):
+        self.plan._bind_stream()
+        check(lib().hgp_slab_cg_p(self.plan._h, self._p(p), self._p(z), self._p(rs), self._p(zr), p.shape[0],
+                                  p.shape[1], self._p(done)))
 
 
 class SlabToeplitz:
@@ -117,6 +145,7 @@ class SlabToeplitz:
             self.rest_n *= self.ndims[a]
         self.rows_m = [split(dims[0], self.ws, k) for k in range(self.ws)]
         self.rows_n = [split(self.ndims[0], self.ws, k) for k in range(self.ws)]
+        self._buf = {}
 
     # -- partition ------------------------------------------------------------------------
     def my_rows(self, grid="m"):
@@ -133,99 +162,126 @@ class SlabToeplitz:
         return v[:, a * rest:b * rest].contiguous()
 
     # -- the operator ---------------------------------------------------------------------
-    def apply(self, op, x):
-        """op (libhipgp OP_*) on this rank's slab x (nrhs, local in-size) -> local out slab."""
+    def _bufs(self, op, nrhs, dtype, dev):
+        """The exchange / all-to-all buffers of (op, nrhs), allocated once and re-used by every
+        apply -- a PCG iteration allocates nothing."""
+        key = (int(op), int(nrhs))
+        b = self._buf.get(key)
+        if b is None:
+            ws, rk = self.ws, self.rank
+            rows_in = self.rows_n if op == _lib.OP_R else self.rows_m
+            rows_out = self.rows_n if op == _lib.OP_RT else self.rows_m
+            NG, inner = self.engine.geometry(op)
+            groups = [split(NG, ws, k) for k in range(ws)]
+            gs0, gs1 = groups[rk]
+            ng = gs1 - gs0
+            ni = rows_in[rk][1] - rows_in[rk][0]
+            no = rows_out[rk][1] - rows_out[rk][0]
+            cd = self.engine.cdtype
+            # E[g][q][i][c] over my input rows; the first all-to-all sends my rows of every group
+            # and receives all rows of my groups as rank blocks [r][g][q][i - a_r][c] (rank r's
+            # rows [a_r, a_r + cnt_r)); the conv writes the return all-to-all's send buffer as
+            # rank blocks [r][g][q][o - b_r][c] (HGP_SLAB_CONV_A2A: no line buffer, no gather /
+            # scatter copies); the return all-to-all delivers my output rows of every group
+            sizes_in = [(groups[s][1] - groups[s][0]) * nrhs * ni * inner for s in range(ws)]
+            sizes_rx = [ng * nrhs * (rows_in[r][1] - rows_in[r][0]) * inner for r in range(ws)]
+            sizes_tx = [ng * nrhs * (rows_out[r][1] - rows_out[r][0]) * inner for r in range(ws)]
+            sizes_back = [(groups[s][1] - groups[s][0]) * nrhs * no * inner for s in range(ws)]
+            b = dict(NG=NG, inner=inner, gs0=gs0, ng=ng, ni=ni, no=no, sizes_in=sizes_in, sizes_rx=sizes_rx,
+                     sizes_tx=sizes_tx, sizes_back=sizes_back,
+                     E=torch.empty((NG, nrhs, ni, inner), dtype=cd, device=dev),
+                     recv=torch.empty(sum(sizes_rx), dtype=cd, device=dev),
+                     send=torch.empty(sum(sizes_tx), dtype=cd, device=dev),
+                     back=torch.empty(NG * nrhs * no * inner, dtype=cd, device=dev))
+            self._buf[key] = b
+        return b
+
+    def apply(self, op, x, out=None, dotv=None, dot_out=None, done=None):
+        """op (libhipgp OP_*) on this rank's slab x (nrhs, local in-size) -> local out slab
+        (written into `out` when given).  dotv / dot_out: also this rank's per-RHS dots
+        sum(out * dotv) (fused into the last stage); done: a device flag after which every
+        stage is a no-op (the slab PCG's masked iterations)."""
         e = self.engine
-        ws, rk = self.ws, self.rank
-        rows_in = self.rows_n if op == _lib.OP_R else self.rows_m
-        rows_out = self.rows_n if op == _lib.OP_RT else self.rows_m
-        rest_out = self.rest_n if op == _lib.OP_RT else self.rest_m
-        in0 = self.ndims[0] if op == _lib.OP_R else self.dims[0]
-        out0 = self.ndims[0] if op == _lib.OP_RT else self.dims[0]
-        P0 = max(in0, out0)
         nrhs = x.shape[0]
-        NG, inner = e.geometry(op)
-        groups = [split(NG, ws, k) for k in range(ws)]
-        gs0, gs1 = groups[rk]
-        ng = gs1 - gs0
-        ni = rows_in[rk][1] - rows_in[rk][0]
-        no = rows_out[rk][1] - rows_out[rk][0]
-        cd, dev = e.cdtype, x.device
-        # 1. local transforms along the other axes: E[g][q][i][c] over my input rows
-        E = torch.empty((NG, nrhs, ni, inner), dtype=cd, device=dev)
+        b = self._bufs(op, nrhs, x.dtype, x.device)
+        rest_out = self.rest_n if op == _lib.OP_RT else self.rest_m
+        E, recv, send, back = b["E"], b["recv"], b["send"], b["back"]
+        ni, no, ng = b["ni"], b["no"], b["ng"]
+        # 1. local transforms along the other axes over my input rows
         if ni > 0:
-            e.fwd(op, x, ni, E)
-        # 2. all-to-all: my rows of every group -> all rows of my groups, received as rank blocks
-        #    [r][g][q][i - a_r][c] (rank r's rows [a_r, a_r + cnt_r))
-        sizes_in = [(groups[s][1] - groups[s][0]) * nrhs * ni * inner for s in range(ws)]
-        sizes_rx = [ng * nrhs * (rows_in[r][1] - rows_in[r][0]) * inner for r in range(ws)]
-        recv = torch.empty(sum(sizes_rx), dtype=cd, device=dev)
-        _a2a(recv, E.reshape(-1), sizes_rx, sizes_in, self.group)
-        # 3. the axis-0 convolution on my groups straight from the receive buffer into the send
-        #    buffer of the return all-to-all, rank blocks [r][g][q][o - b_r][c] of the output rows
-        #    (HGP_SLAB_CONV_A2A: no line buffer, no gather / scatter copies)
-        sizes_tx = [ng * nrhs * (rows_out[r][1] - rows_out[r][0]) * inner for r in range(ws)]
-        send = torch.empty(sum(sizes_tx), dtype=cd, device=dev)
+            e.fwd(op, x, ni, E, done=done)
+        # 2. all-to-all: my rows of every group -> all rows of my groups
+        _a2a(recv, E.reshape(-1), b["sizes_rx"], b["sizes_in"], self.group)
+        # 3. the axis-0 convolution of my groups, receive buffer -> send buffer
         if ng > 0:
-            e.conv_a2a(op, recv, send, gs0, ng, nrhs, ws)
+            e.conv_a2a(op, recv, send, b["gs0"], ng, nrhs, self.ws, done=done)
         # 4. all-to-all back: all rows of my groups -> my output rows of every group
-        back = torch.empty(NG * nrhs * no * inner, dtype=cd, device=dev)
-        sizes_back = [(groups[s][1] - groups[s][0]) * nrhs * no * inner for s in range(ws)]
-        _a2a(back, send, sizes_back, sizes_tx, self.group)
-        E2 = back.view(NG, nrhs, no, inner)      # groups arrive in rank order = group order
-        # 5. local inverse transforms over my output rows
-        y = torch.empty((nrhs, no * rest_out), dtype=x.dtype, device=dev)
+        _a2a(back, send, b["sizes_back"], b["sizes_tx"], self.group)
+        E2 = back.view(b["NG"], nrhs, no, b["inner"])      # groups arrive in rank order = group order
+        # 5. local inverse transforms over my output rows (+ fused dot)
+        y = torch.empty((nrhs, no * rest_out), dtype=x.dtype, device=x.device) if out is None else out
         if no > 0:
-            e.inv(op, E2, no, y)
+            e.inv(op, E2, no, y, dotv=dotv, dot_out=dot_out, done=done)
+        elif dot_out is not None:
+            dot_out.zero_()
         return y
 
     # -- PCG -------------------------------------------------------------------------------
     def dot(self, a, b):
         """Global per-RHS dot products: local row sums, one all-reduce of nrhs values."""
-        s = (a * b).sum(dim=1) if a.shape[1] else a.new_zeros(a.shape[0])
-        return _allreduce(s.contiguous(), self.group)
+        s = torch.empty(a.shape[0], dtype=a.dtype, device=a.device)
+        self.engine.dot(a, b, s)
+        return _allreduce(s, self.group)
 
     def pcg(self, b, maxiter=20, tol=1e-8, precond=True, callback=None):
         """conj_grad2 (`cg.py:44-80`) on the slabs: x0 = 0, per-RHS alpha / beta from all-reduced
         dots, break when EVERY global sqrt(r.r) < tol.  Returns (x, iterations run).
 
-        The break is decided on the device: every rank holds the same reduced r.r, so a device
-        flag `done` (all sqrt(r.r) < tol after some iteration) is identical everywhere; the
-        iterations after it leave x unchanged (alpha masked to 0, the same x as the reference's
-        break) and the host queues all `maxiter` iterations without a synchronisation (RCCL: the
-        dots' all-reduces are stream-ordered).  The iteration count is read once at the end.
-        With a callback (`cg.py:77-78`, called after every iteration that did not break) the
-        host must look at the flag, so that form synchronises per iteration as the reference."""
-        P = (lambda v: self.apply(_lib.OP_CINV, v)) if precond else (lambda v: v)
+        Per iteration: Ap = K p with the local p.Ap fused into its last stage; all-reduce;
+        alpha, x += alpha p, r -= alpha Ap and the local r.r in one update (hgp_slab_cg_xr);
+        all-reduce; the break test on the reduced r.r (identical on every rank: a device flag
+        `done` holding the iteration it fired in, hgp_slab_cg_check); z = C^-1 r with z.r fused;
+        all-reduce; beta, rs and p = z + beta p (hgp_slab_cg_p).  Every kernel of the operators
+        and updates is a no-op once `done` is set, so the host queues all `maxiter` iterations
+        without a synchronisation (RCCL: the all-reduces / all-to-alls are stream-ordered) and
+        the iterations after the break cost their (stale) collectives only; x is the iterate
+        the reference's break returns.  Vectors, scalars and exchange buffers are allocated
+        before the loop.  With a callback (`cg.py:77-78`, after every iteration that did not
+        break) the host must look at the flag, so that form synchronises per iteration."""
+        e = self.engine
+        nrhs = b.shape[0]
+        b = b.contiguous()
         x = torch.zeros_like(b)
         r = b.clone()
-        z = P(r)
-        p = z
-        rs = self.dot(r, z)
-        done = torch.zeros((), dtype=torch.bool, device=b.device)
-        its = torch.zeros((), dtype=torch.int64, device=b.device)
+        z = torch.empty_like(b) if precond else r
+        Ap = torch.empty_like(b)
+        sc = torch.zeros((4, nrhs), dtype=b.dtype, device=b.device)
+        rs, pAp, rr, zr = sc[0], sc[1], sc[2], sc[3]
+        flags = torch.zeros(2, dtype=torch.int32, device=b.device)
+        done, iters = flags[0:1], flags[1:2]
+        if precond:
+            self.apply(_lib.OP_CINV, r, out=z, dotv=r, dot_out=rs)     # z0 = P r, rs = z.r
+        else:
+            e.dot(r, r, rs)
+        _allreduce(rs, self.group)
+        p = z.clone()
         for n in range(int(maxiter)):
-            its += (~done).long()
-            Ap = self.apply(_lib.OP_K, p)
-            # after the break every update is masked out (alpha = 0), so x stays the iterate the
-            # reference returns; torch.where keeps the 0/0 of the masked iterations out
-            alpha = torch.where(done, torch.zeros_like(rs), rs / self.dot(p, Ap))
-            x = x + alpha.unsqueeze(-1) * p
-            r = r - alpha.unsqueeze(-1) * Ap
-            rnew = self.dot(r, r)
-            done = done | torch.all(torch.sqrt(rnew) < tol)
-            if callback is not None:
-                if bool(done):
-                    break
-            z = P(r)
-            zr = self.dot(z, r)
-            beta = zr / rs
-            # p = 0 once done: the masked iterations then see Ap = 0 and finite x, r
-            p = torch.where(done, torch.zeros((), dtype=p.dtype, device=p.device), z + beta.unsqueeze(-1) * p)
-            rs = zr                   # = sum(r * z) at the top of the next iteration (cg.py:64)
+            self.apply(_lib.OP_K, p, out=Ap, dotv=p, dot_out=pAp, done=done)
+            _allreduce(pAp, self.group)
+            e.cg_xr(x, r, p, Ap, rs, pAp, rr, done)
+            _allreduce(rr, self.group)
+            e.cg_check(rr, tol, done, iters)
+            if callback is not None and int(done.item()):
+                break
+            if precond:
+                self.apply(_lib.OP_CINV, r, out=z, dotv=r, dot_out=zr, done=done)
+                _allreduce(zr, self.group)
+                e.cg_p(p, z, rs, zr, done)
+            else:
+                e.cg_p(p, r, rs, rr, done)
             if callback is not None:
                 callback(n, x)
-        return x, int(its)
+        return x, int(iters.item())
 
     def compute_kn(self, Knm_local, maxiter=20, tol=1e-8):
         """kn = R^T K^{-1} Knm^T (`hipgp.py:143-145`) with Knm's axis-0 rows on this rank;

@@ -37,9 +37,14 @@ class SviGP(nn.Module):
         self.pred_scale_factor = 1.
 
     def torch(self, arr):
-        """numpy -> tensor of the model dtype; tensors must already have it (`svi_gp.py:24-32`)."""
+        """numpy -> tensor of the model dtype; tensors must already have it (`svi_gp.py:24-32`).
+
+        Quirk kept: the reference builds `torch.Tensor(arr)` first -- the DEFAULT dtype (fp32)
+        -- and only then casts to the model dtype, so an fp64 model sees its numpy data
+        (observation coordinates, values, noise) rounded to fp32.  With UK-box coordinates
+        (~50-55, G19) the difference is 2e-5 of the first natural-gradient step."""
         if isinstance(arr, np.ndarray):
-            return torch.tensor(arr, dtype=self.dtype)
+            return torch.tensor(arr, dtype=torch.get_default_dtype()).to(self.dtype)
         if isinstance(arr, torch.Tensor):
             assert arr.dtype == self.dtype, f"model dtype = {self.dtype}, data dtype = {arr.dtype}"
             return arr

@@ -137,6 +137,31 @@ enum { HGP_SLAB_FWD = 0, HGP_SLAB_CONV = 1, HGP_SLAB_INV = 2, HGP_SLAB_CONV_A2A 
 int hgp_slab_info(const hgp_plan* plan, int op, int64_t* ngroups, int64_t* inner);
 int hgp_slab_pass(hgp_plan* plan, int op, int stage, const void* in, void* out, int64_t nrhs,
                   int64_t nrows, int64_t g0, int64_t ng);
+/* hgp_slab_pass with two options for the slab PCG (hipgp_amd/slab.py SlabToeplitz.pcg):
+ *   done (device int or NULL): every kernel of the stage is a no-op once *done != 0, so the
+ *        iterations after the all-rank break cost (almost) nothing without a host round trip;
+ *   dotv, dot_out (HGP_SLAB_INV only, device, or NULL): the stage also leaves this rank's
+ *        per-RHS dot dot_out[q] = sum_j y[q, j] dotv[q, j] of its output y (dotv laid out
+ *        like y), from per-row-pair partials summed in a fixed order -- p.Ap / z.r of
+ *        cg.py:66,74 without a second read of the vectors.  dot_out: nrhs values. */
+int hgp_slab_pass_ex(hgp_plan* plan, int op, int stage, const void* in, void* out, int64_t nrhs,
+                     int64_t nrows, int64_t g0, int64_t ng, const void* dotv, void* dot_out,
+                     const int* done);
+
+/* The slab PCG's vector / scalar updates (cg.py:63-78) on this rank's slab (nrhs rows of M
+ * values, plan dtype; M may be 0 on a rank without rows), with every per-RHS dot ALREADY
+ * all-reduced by the caller between the calls.  done / iters: device ints (0 at the start);
+ * every call is a no-op once *done != 0 (done = the iteration the break fired in).
+ *   hgp_slab_cg_xr   : alpha = rs / pAp; x += alpha p; r -= alpha Ap; rr = local sum r.r
+ *   hgp_slab_cg_check: iters += 1; done = iters when every sqrt(rr) < tol (rr reduced; NaN =
+ *                      not converged, cg.py:70)
+ *   hgp_slab_cg_p    : beta = zr / rs; rs = zr; p = z + beta p
+ * All per-RHS scalars are device arrays of nrhs values; ordered on the plan's stream. */
+int hgp_slab_cg_xr(hgp_plan* plan, void* x, void* r, const void* p, const void* Ap, const void* rs,
+                   const void* pAp, void* rr, int64_t nrhs, int64_t M, const int* done);
+int hgp_slab_cg_check(hgp_plan* plan, const void* rr, int64_t nrhs, double tol, int* done, int* iters);
+int hgp_slab_cg_p(hgp_plan* plan, void* p, const void* z, void* rs, const void* zr, int64_t nrhs,
+                  int64_t M, const int* done);
 
 /* The clamped spectrum D (which=HGP_SPEC_D), sqrt(D) or 1/D on the full expanded grid
  * (device, M' reals) — the real parts of ToeplitzTensor.D / D_sqrt / Di

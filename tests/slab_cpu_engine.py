@@ -32,7 +32,13 @@ class CpuSlabEngine:
         outs = self.n if op == _lib.OP_RT else self.dims
         return ins, outs
 
-    def fwd(self, op, x, nrows, E):
+    @staticmethod
+    def _masked(done):
+        return done is not None and int(done.reshape(-1)[0]) != 0
+
+    def fwd(self, op, x, nrows, E, done=None):
+        if self._masked(done):
+            return
         ins, _ = self._io(op)
         xv = x.detach().cpu().numpy().reshape((x.shape[0], nrows) + tuple(ins[1:]))
         if self.d == 2:
@@ -66,9 +72,11 @@ class CpuSlabEngine:
             a += c
         return out
 
-    def conv_a2a(self, op, recv, send, g0, ng, nrhs, ws):
+    def conv_a2a(self, op, recv, send, g0, ng, nrhs, ws, done=None):
         """HGP_SLAB_CONV_A2A: lines read from the receive buffer's rank blocks
         [r][g][q][i - a_r][c], results written to the send buffer's [r][g][q][o - b_r][c]."""
+        if self._masked(done):
+            return
         ins, outs = self._io(op)
         _, inner = self.geometry(op)
         lines = torch.zeros((ng, nrhs, max(ins[0], outs[0]), inner), dtype=self.cdtype)
@@ -85,7 +93,9 @@ class CpuSlabEngine:
             send[off:off + n] = lines[:, :, b:b + c, :].reshape(-1).to(send.device)
             off += n
 
-    def inv(self, op, E, nrows, y):
+    def inv(self, op, E, nrows, y, dotv=None, dot_out=None, done=None):
+        if self._masked(done):
+            return
         _, outs = self._io(op)
         A = E.cpu().numpy()
         if self.d == 2:
@@ -94,3 +104,31 @@ class CpuSlabEngine:
             B = np.fft.ifft(A.transpose(1, 2, 0, 3), n=self.n[1], axis=2)
             Y = np.fft.irfft(B, n=self.n[2], axis=3)[:, :, :outs[1], :outs[2]]
         y.copy_(torch.from_numpy(np.ascontiguousarray(Y.reshape(y.shape))))
+        if dotv is not None:
+            dot_out.copy_((y * dotv).sum(dim=1))
+
+    # -- the slab PCG's updates (the contract of hgp_slab_cg_*: dots already all-reduced) ----
+    def dot(self, a, c, out):
+        out.copy_((a * c).sum(dim=1))
+
+    def cg_xr(self, x, r, p, Ap, rs, pAp, rr, done):
+        if self._masked(done):
+            return
+        al = (rs / pAp).unsqueeze(-1)
+        x += al * p
+        r -= al * Ap
+        rr.copy_((r * r).sum(dim=1))
+
+    def cg_check(self, rr, tol, done, iters):
+        if self._masked(done):
+            return
+        iters += 1
+        if bool(torch.all(torch.sqrt(rr) < tol)):
+            done.copy_(iters)
+
+    def cg_p(self, p, z, rs, zr, done):
+        if self._masked(done):
+            return
+        beta = (zr / rs).unsqueeze(-1)
+        rs.copy_(zr)
+        p.mul_(beta).add_(z)

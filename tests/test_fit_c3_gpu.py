@@ -1,0 +1,121 @@
+"""Config 3's own fit settings on the GPU path against the reference's `svigp_fit` (G19,
+`tests/golden/make_golden_fit_c3.py`): MeanFieldToeplitzGP, Matern-3/2, ell 0.1, jitter 1e-3,
+init_Svar 0.1, sig2 = var(y) - noise^2, N / batch = 500, batch 200, constant lr 1e-2,
+maxiter_cg 20 (`run_ukhousing_experiment.py:22,31,33,49-50,207-208,277`,
+`experiment_util.py:71-180`, `svi_gp.py:172-442`), 20 minibatches on a 64 x 64 grid:
+
+* "box" (the full UK box): the reference converges; the GPU trajectory tracks it;
+* "fine" (config 3's own 2048-point grid spacing): the reference DIVERGES, fp64 included
+  (ELBO x1e4-1e5 per batch); the GPU path diverges the same way -- the same first iterates,
+  the same growth of |theta| batch by batch, fp32 overflowing where the reference's does.
+
+Every natural-gradient step divides by k_n from a 20-iteration PCG that has not converged, so
+the iterates carry the PCG's rounding: two fp64 runs of the reference itself that differ only
+in the FFT implementation (torch.fft vs NumPy's pocketfft in the shim, G19 "{case}_alt_*")
+already differ by ~1e-5 ("box") and ~5e-2 ("fine") after one step.  The fp64 bound is 4x that
+spread of the reference's own (SURVEY §8(c)'s 4x rule with the FFT's rounding as the yardstick);
+fp32 keeps the rule against the reference's own fp32 error.
+"""
+import numpy as np
+import pytest
+import torch
+
+from golden_cases import load
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+NOBS_MODEL = 100_000
+
+
+def _run(fx, case, dtype, tmp_path):
+    import ziggy.hipgp as hg
+    import ziggy.kernels as zk
+    grids = [torch.tensor(fx[f"{case}_grid0"], dtype=dtype), torch.tensor(fx[f"{case}_grid1"], dtype=dtype)]
+    mod = hg.MeanFieldToeplitzGP(zk.Matern(nu=1.5, dtype=dtype), grids, num_obs=NOBS_MODEL,
+                                 sig2_init=float(fx[f"{case}_sig2_init"]), ell_init=.1, init_Svar=.1,
+                                 learn_kernel=False, jitter_val=1e-3, dtype=dtype)
+    with torch.no_grad():
+        mod.global_theta1.copy_(torch.tensor(fx[f"{case}_theta1_init"], dtype=dtype))
+        mod.global_theta2.copy_(torch.tensor(fx[f"{case}_theta2_init"], dtype=dtype))
+    snaps = []
+
+    def batch_cb(m, xb, yb, sb):
+        snaps.append([m.global_theta1.detach().double().cpu().numpy().copy(),
+                      m.global_theta2.detach().double().cpu().numpy().copy()])
+
+    traces = []
+
+    def epoch_cb(odir, m, *args, **kw):
+        traces.append(list(args[15]))
+        return (None,) * 6
+
+    npd = np.float64 if dtype == torch.float64 else np.float32
+    x, y, s = (fx[f"{case}_{k}"].astype(npd) for k in "xys")
+    mod.fit(str(tmp_path), x, y, s, None, None, None, None, None, None, batch_callback=batch_cb,
+            epoch_callback=epoch_cb, do_cuda=True, lr=1e-2, schedule_lr=False, batch_size=200, epochs=1,
+            maxiter_cg=20, batch_log_interval=1, learn_kernel=False)
+    batch_cb(mod, None, None, None)
+    assert len(snaps) == 21
+    return snaps, np.array(traces[0], dtype=np.float64)
+
+
+def _spread_bound(fx, case, name, j, got):
+    """|got - ref| <= 4 |alt - ref| + 1e-9 |ref| (alt: the reference with another FFT)."""
+    ref = fx[f"{case}_{name}_steps"][j]
+    alt = fx[f"{case}_alt_{name}_steps"][j]
+    e_me, e_alt = np.linalg.norm(got - ref), np.linalg.norm(alt - ref)
+    assert e_me <= 4 * e_alt + 1e-9 * np.linalg.norm(ref), (case, name, j, e_me, e_alt, np.linalg.norm(ref))
+
+
+def test_c3_settings_box_fp64(tmp_path):
+    fx = load("G19", "f64")
+    snaps, trace = _run(fx, "box", torch.float64, tmp_path)
+    for j, k in enumerate(fx["box_steps"]):
+        _spread_bound(fx, "box", "theta1", j, snaps[k][0])
+        _spread_bound(fx, "box", "theta2", j, snaps[k][1])
+    e_me = np.abs(trace - fx["box_elbo_trace"])
+    e_alt = np.abs(fx["box_alt_elbo_trace"] - fx["box_elbo_trace"])
+    assert np.all(e_me <= 4 * e_alt + 1e-9 * np.abs(fx["box_elbo_trace"])), (e_me, e_alt)
+    assert trace[-1] > trace[0]                                   # the fit improves the bound
+
+
+def test_c3_settings_box_fp32(tmp_path):
+    fx32, fx64 = load("G19", "f32"), load("G19", "f64")
+    snaps, trace = _run(fx32, "box", torch.float32, tmp_path)
+    for j, k in enumerate(fx64["box_steps"]):
+        for i, name in ((0, "theta1"), (1, "theta2")):
+            ref64 = fx64[f"box_{name}_steps"][j]
+            e_me = np.linalg.norm(snaps[k][i] - ref64)
+            e_ref = np.linalg.norm(fx32[f"box_{name}_steps"][j].astype(np.float64) - ref64)
+            assert e_me <= 4 * e_ref + 1e-6 * np.linalg.norm(ref64), (k, name, e_me, e_ref)
+    t64 = fx64["box_elbo_trace"]
+    e_me = np.abs(trace - t64)
+    e_ref = np.abs(fx32["box_elbo_trace"] - t64)
+    assert np.all(e_me <= 4 * e_ref + 1e-5 * np.abs(t64)), (e_me, e_ref)
+
+
+def test_c3_settings_fine_diverges_like_reference_fp64(tmp_path):
+    fx = load("G19", "f64")
+    snaps, trace = _run(fx, "fine", torch.float64, tmp_path)
+    # the first iterates, within 4x the reference's own FFT-rounding spread
+    for j, k in enumerate(fx["fine_steps"]):
+        _spread_bound(fx, "fine", "theta1", j, snaps[k][0])
+        _spread_bound(fx, "fine", "theta2", j, snaps[k][1])
+    # the divergence itself: |theta1| and the ELBO grow batch by batch as the reference's
+    n1 = np.array([np.linalg.norm(s[0]) for s in snaps])
+    assert np.all(np.abs(np.log(n1 / fx["fine_theta1_norm"])) < np.log(1.5)), (n1, fx["fine_theta1_norm"])
+    assert np.all(np.abs(np.log(trace / fx["fine_elbo_trace"])) < np.log(1.5)), (trace, fx["fine_elbo_trace"])
+    assert trace[-1] < -1e80 and np.all(np.diff(trace) < 0)
+
+
+def test_c3_settings_fine_diverges_like_reference_fp32(tmp_path):
+    fx32, fx64 = load("G19", "f32"), load("G19", "f64")
+    snaps, trace = _run(fx32, "fine", torch.float32, tmp_path)
+    ref = fx32["fine_elbo_trace"]
+    fin = np.isfinite(ref)
+    k_ovf = int(np.argmin(fin))                  # the reference's first non-finite batch (9)
+    assert 5 <= k_ovf <= 12
+    # finite batches: the same growth as the reference's fp32 and fp64 runs
+    assert np.all(np.abs(np.log(trace[:k_ovf - 1] / fx64["fine_elbo_trace"][:k_ovf - 1])) < np.log(2.0)), trace
+    # and the fp32 run overflows within a batch of where the reference's does
+    assert not np.all(np.isfinite(trace[:k_ovf + 2])), trace

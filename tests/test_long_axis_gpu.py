@@ -95,6 +95,12 @@ def test_long_axis_ops_and_pcg_fp64(case):
     rr = P.apply(_lib.OP_R, P.apply(_lib.OP_RT, vt)).cpu().numpy()
     kv = O.matmul_K(v)
     assert float(np.abs(rr - kv).max() / np.abs(kv).max()) < 1e-10
+    if max(dims) > 5462:
+        # the full-grid R / R^T route: its two L_R-grid buffers are scratch and its stored-order
+        # spectrum a table in hgp_plan_mem (so the plan pool sees them)
+        nLR = int(np.prod(P.L_R[:len(dims)]))
+        mem = P.mem()
+        assert mem["scratch"] >= 2 * nLR * 16 and mem["tables"] >= nLR * 16, (mem, nLR)
 
 
 def test_long_axis_refusals():

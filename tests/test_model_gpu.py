@@ -168,8 +168,9 @@ def test_plan_pool_trim_and_release():
     P = hp.ToeplitzPlan(dims, torch.float64, DEV)
     P.set_column(col)
     x1 = P.pcg(v, 10, 1e-30).clone()
-    old = hp._POOL_BYTES
-    hp._POOL_BYTES = 0                      # force trimming on the way into the pool
+    assert P.mem()["scratch"] > 0 and P.mem()["tables"] > 0
+    old = hp._POOL_ENV
+    hp._POOL_ENV = "0"                      # force trimming on the way into the pool
     try:
         del P
         gc.collect()
@@ -180,7 +181,7 @@ def test_plan_pool_trim_and_release():
         del Q
         gc.collect()
     finally:
-        hp._POOL_BYTES = old
+        hp._POOL_ENV = old
     hp.release_pool()
     assert hp.pool_scratch_bytes() == 0 and not hp._POOL
 

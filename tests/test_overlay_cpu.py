@@ -44,8 +44,13 @@ def test_overlay_resolves_reference_modules():
 def test_overlay_without_reference():
     """Alone (the GPU box has no reference), the hot-path modules still import."""
     env = dict(os.environ, PYTHONPATH=ROOT, PYTHONDONTWRITEBYTECODE="1")
-    code = ("import ziggy.hipgp, ziggy.misc.toeplitz_tensor as t, hipgp_amd.ziggy.misc.toeplitz_tensor as u;"
-            "assert t is u; print('alone ok')")
+    code = ("import importlib, ziggy.hipgp, ziggy.misc.toeplitz_tensor as t, hipgp_amd.ziggy.misc.toeplitz_tensor as u;"
+            "import ziggy.misc.cg as c;"
+            "assert t is u;"
+            "assert all(m.__spec__.name == m.__name__ for m in (t, c, ziggy.hipgp)), [t.__spec__.name, c.__spec__.name];"
+            "f = c.conj_grad2; importlib.reload(c); assert c.conj_grad2 is not f;"   # reload re-executes the module
+            "importlib.reload(ziggy.misc.cg); assert ziggy.misc.cg is c;"
+            "print('alone ok')")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240,
                        cwd="/tmp")
     assert r.returncode == 0 and "alone ok" in r.stdout, r.stdout + r.stderr

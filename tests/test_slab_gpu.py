@@ -3,7 +3,10 @@ cuda:0, gloo for the all-to-all transposes and the CG dot all-reduces (RCCL on a
 node) -- of SlabToeplitz on libhipgp's hgp_slab_pass stages.  The gathered K, C^-1, R^T, R and
 the slab PCG / compute_kn agree with the single-rank plan to rounding (fp64 1e-11 on the ops;
 fp32 within FFT rounding); the slab PCG runs the conj_grad2 recurrence with all-reduced
-dots, the single-rank plan the fused device PCG."""
+dots, the single-rank plan the fused device PCG.  World size 3 checks the HIP
+rank-block addressing of HGP_SLAB_CONV_A2A with remainder splits.  The slab PCG allocates
+nothing per iteration (torch.cuda.memory_stats: the same number of device allocations for 3
+and 9 iterations) and its break rule gives the single-rank plan's iteration count."""
 import os
 
 import numpy as np
@@ -48,6 +51,20 @@ def _worker(rank, ws, port, case, out):
             res[name] = S.apply(op, S.scatter_rows(x, grid)).double().cpu().numpy()
         x, it = S.pcg(S.scatter_rows(v), maxiter=10, tol=1e-30)
         res["pcg"] = x.double().cpu().numpy()
+        res["pcg_it"] = it
+        # no device allocation inside the iteration loop
+        counts = []
+        for mi in (3, 9):
+            torch.cuda.synchronize()
+            a0 = torch.cuda.memory_stats()["allocation.all.allocated"]
+            S.pcg(S.scatter_rows(v), maxiter=mi, tol=1e-30)
+            torch.cuda.synchronize()
+            counts.append(torch.cuda.memory_stats()["allocation.all.allocated"] - a0)
+        res["alloc_counts"] = counts
+        # the all-rank break (device flag; the masked iterations leave x alone)
+        tol_brk = float(np.sqrt(np.sum(v.double().cpu().numpy()[0] ** 2))) * (1e-3 if dt == torch.float64 else 1e-2)
+        xb, itb = S.pcg(S.scatter_rows(v), maxiter=200, tol=tol_brk)
+        res["brk"], res["brk_it"], res["brk_tol"] = xb.double().cpu().numpy(), itb, tol_brk
         res["kn"] = S.compute_kn(S.scatter_rows(v), maxiter=10, tol=1e-30).double().cpu().numpy()
         torch.cuda.synchronize()
         out[rank] = res
@@ -55,16 +72,16 @@ def _worker(rank, ws, port, case, out):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("case", sorted(CASES))
-def test_slab_two_ranks_same_device(case):
+@pytest.mark.parametrize("case,ws", [(c, 2) for c in sorted(CASES)] + [("2d_odd_f64", 3), ("3d_f64", 3)])
+def test_slab_ranks_same_device(case, ws):
     from hipgp_amd import _lib
     from hipgp_amd.plan import ToeplitzPlan
     dims, dt = CASES[case]
     mgr = mp.Manager()
     out = mgr.dict()
     port = 29650 + os.getpid() % 100 + len(case)
-    mp.spawn(_worker, args=(2, port, case, out), nprocs=2, join=True)
-    assert len(out) == 2
+    mp.spawn(_worker, args=(ws, port + ws, case, out), nprocs=ws, join=True)
+    assert len(out) == ws
     P = ToeplitzPlan(dims, dt, "cuda")
     P.set_column(torch.tensor(_column(dims), device="cuda", dtype=dt))
     M = int(np.prod(dims))
@@ -72,7 +89,7 @@ def test_slab_two_ranks_same_device(case):
     g = torch.Generator(device="cuda").manual_seed(9)
     v = torch.randn(3, M, device="cuda", generator=g, dtype=torch.float64).to(dt)
     w = torch.randn(3, Mp, device="cuda", generator=g, dtype=torch.float64).to(dt)
-    gat = lambda k: np.concatenate([out[0][k], out[1][k]], axis=1)
+    gat = lambda k: np.concatenate([out[r][k] for r in range(ws)], axis=1)
     tol_op = 1e-11 if dt == torch.float64 else 2e-5
     for name, op, x in (("K", _lib.OP_K, v), ("Cinv", _lib.OP_CINV, v), ("RT", _lib.OP_RT, v), ("R", _lib.OP_R, w)):
         ref = P.apply(op, x).double().cpu().numpy()
@@ -86,4 +103,13 @@ def test_slab_two_ranks_same_device(case):
     assert err < tol_pcg, err
     kn = P.apply(_lib.OP_RT, P.pcg(v, 10, 1e-30, precond=True)).double().cpu().numpy()
     err = float(np.linalg.norm(gat("kn") - kn) / np.linalg.norm(kn))
+    assert err < tol_pcg, err
+    for r in range(ws):
+        assert out[r]["pcg_it"] == 10
+        a3, a9 = out[r]["alloc_counts"]
+        assert a3 == a9, (r, a3, a9)
+    xb, itb = P.pcg(v, 200, out[0]["brk_tol"], precond=True, return_iters=True)
+    assert all(out[r]["brk_it"] == itb for r in range(ws)), ([out[r]["brk_it"] for r in range(ws)], itb)
+    assert itb < 200
+    err = float(np.linalg.norm(gat("brk") - xb.double().cpu().numpy()) / np.linalg.norm(xb.double().cpu().numpy()))
     assert err < tol_pcg, err

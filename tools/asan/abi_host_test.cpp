@@ -63,6 +63,10 @@ int main() {
   EXPECT(hgp_plan_mem(nullptr, i64, i64) == HGP_E_ARG);
   EXPECT(hgp_slab_info(nullptr, HGP_OP_K, i64, i64) == HGP_E_ARG);
   EXPECT(hgp_slab_pass(nullptr, HGP_OP_K, HGP_SLAB_FWD, buf, buf + 8, 1, 1, 0, 0) == HGP_E_ARG);
+  EXPECT(hgp_slab_pass_ex(nullptr, HGP_OP_K, HGP_SLAB_INV, buf, buf + 8, 1, 1, 0, 0, buf, buf, nullptr) == HGP_E_ARG);
+  EXPECT(hgp_slab_cg_xr(nullptr, buf, buf, buf, buf, buf, buf, buf, 1, 4, nullptr) == HGP_E_ARG);
+  EXPECT(hgp_slab_cg_check(nullptr, buf, 1, 1e-8, nullptr, nullptr) == HGP_E_ARG);
+  EXPECT(hgp_slab_cg_p(nullptr, buf, buf, buf, buf, 1, 4, nullptr) == HGP_E_ARG);
 
   // ---- stand-alone kernels: argument checks and empty inputs ---------------------------
   EXPECT(hgp_rowdot(HGP_F32, buf, buf, buf, 0, 16, nullptr) == 0);            // nothing to do

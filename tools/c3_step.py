@@ -1,70 +1,88 @@
-"""C3 minibatch step timing (GPU box): one `svigp_fit` minibatch (`svi_gp.py:172-442` via
-hipgp_amd/ziggy/svi_gp.py) on the C3 shape -- 2048 x 2048 inducing grid on [-1, 1]^2, Matern-3/2
-(ell 0.02, nugget 1e-2), N = 100k synthetic observations, batch 1000 (`experiment_util.py:44-50`),
-PCG maxiter 20: zero grads, elbo_and_grad (fused Kuf + compute_kn + statistics), with learned
-kernel the hyper backward + Adam step, the natural-gradient SGD step (lr 0.01, the svi_gp.py
-default).  One JSON line per (model, learn_kernel, batch).
+"""Config 3 on its own settings at full size (GPU box): the reference's fit driver
+(`svigp_fit`, `svi_gp.py:172-442`, here hipgp_amd/ziggy/svi_gp.py) for 20 minibatches on a
+2048 x 2048 inducing grid over the UK box (-5.7, 1.8) x (50, 55.5), MeanFieldToeplitzGP,
+Matern-3/2, ell 0.1, jitter 1e-3, init_Svar 0.1, sig2 = var(y) - noise^2, batch 200, constant
+lr 1e-2, maxiter_cg 20, N = 100k (num_obs; the fit sees 20 batches) -- the settings of
+`run_ukhousing_experiment.py:22,31,33,49-50,207-208,277` through `experiment_util.py:71-180`.
+Synthetic observations (the UK data are absent): the field of tests/golden/make_golden_fit_c3.py
+on the whole box, noise std .15.
 
-    python tools/c3_step.py > gpurun_out/c3_step.jsonl
+One JSON line per dtype: per-batch wall time (synchronised in the batch callback), the
+500-batch epoch estimate at B = 200, the ELBO trace and |theta1| per batch.  G19 "fine" shows
+the reference's own trajectory at this grid spacing diverging (tests/test_fit_c3_gpu.py).
+
+    python tools/c3_step.py [--dtype f32,f64] [--batches 20] > gpurun_out/c3_fit.jsonl
 """
+import argparse
 import json
 import os
 import sys
+import tempfile
 import time
 
 import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden"))
+
+
+def field(x, box):
+    (x0, x1), (y0, y1) = box
+    t = (x - [x0, y0]) / [x1 - x0, y1 - y0]
+    return .6 * np.sin(2.3 * np.pi * t[:, 0]) * np.cos(1.7 * np.pi * t[:, 1]) + .3 * np.cos(5.1 * t[:, 0] + 3.7 * t[:, 1])
 
 
 def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--dtype", default="f32,f64")
+    ap.add_argument("--batches", type=int, default=20)
+    ap.add_argument("--m", type=int, default=2048)
+    a = ap.parse_args()
     import ziggy.hipgp as hg
     import ziggy.kernels as zk
-    dev = torch.device("cuda", 0)
-    dt = torch.float32
-    m, N, maxiter = 2048, 100_000, 20
-    rng = np.random.default_rng(7)
-    x = rng.uniform(-1, 1, size=(N, 2))
-    y = (np.sin(3 * x[:, 0]) * np.cos(2 * x[:, 1]) + 0.1 * rng.standard_normal(N))[:, None]
-    s = np.full((N, 1), 0.1)
-    grids = [torch.linspace(-1, 1, m, dtype=dt)] * 2
-    # (model, learned kernel, batch): the learned-kernel step keeps autograd graphs of several
-    # (batch, M) tensors (16 GB each at batch 1000), so it runs at the fit default batch 256
-    for cls, learn_kernel, bsz in (("MeanFieldToeplitzGP", False, 1000), ("MeanFieldToeplitzGP", True, 256)):
-        mod = getattr(hg, cls)(zk.Matern(nu=1.5, dtype=dt), grids, num_obs=N, sig2_init=1., ell_init=.02,
-                                jitter_val=1e-2, noise2_init=.01, learn_kernel=learn_kernel, dtype=dt).cuda_params(0)
-        X = torch.tensor(x, dtype=dt, device=dev)
-        Y = torch.tensor(y, dtype=dt, device=dev)
-        S = torch.tensor(s, dtype=dt, device=dev)
-        nat = torch.optim.SGD([mod.global_theta1, mod.global_theta2], lr=0.01)   # svi_gp.py default lr
-        hyp = torch.optim.Adam([mod.log_ell, mod.log_sig2], lr=1e-3) if learn_kernel else None
+    box = ((-5.7, 1.8), (50., 55.5))
+    N, bsz, sd = 100_000, 200, .15
+    nfit = a.batches * bsz
+    rs = np.random.RandomState(3)
+    u = rs.rand(nfit, 2)
+    x = np.column_stack([box[0][0] + 7.5 * u[:, 0], box[1][0] + 5.5 * u[:, 1]])
+    y = field(x, box) + sd * rs.randn(nfit)
+    y = (y - y.mean())[:, None]
+    s = np.full((nfit, 1), sd)
+    sig2 = float(y.var() - sd ** 2)
+    for tag in a.dtype.split(","):
+        dt = torch.float64 if tag == "f64" else torch.float32
+        npd = np.float64 if tag == "f64" else np.float32
+        grids = [torch.linspace(*box[0], a.m, dtype=dt), torch.linspace(*box[1], a.m, dtype=dt)]
+        mod = hg.MeanFieldToeplitzGP(zk.Matern(nu=1.5, dtype=dt), grids, num_obs=N, sig2_init=sig2, ell_init=.1,
+                                     init_Svar=.1, learn_kernel=False, jitter_val=1e-3, dtype=dt)
+        stamps, norms, traces = [], [], []
 
-        def step(b):
-            sl = slice(b * bsz, (b + 1) * bsz)
-            nat.zero_grad()
-            if hyp is not None:
-                hyp.zero_grad()
-            lval = mod.elbo_and_grad(xbatch=X[sl], ybatch=Y[sl], noise_std_batch=S[sl], maxiter_cg=maxiter)
-            if hyp is not None:
-                (-lval).backward()
-                hyp.step()
-            nat.step()
-            return lval
+        def batch_cb(m, xb, yb, sb):
+            torch.cuda.synchronize()
+            stamps.append(time.perf_counter())
+            norms.append(float(torch.linalg.norm(m.global_theta1.detach().double())))
 
-        elbos = [float(step(b)) for b in range(2)]
+        def epoch_cb(odir, m, *args, **kw):
+            traces.append([float(v) for v in args[15]])
+            return (None,) * 6
+
+        with tempfile.TemporaryDirectory() as odir:
+            mod.fit(odir, x.astype(npd), y.astype(npd), s.astype(npd), None, None, None, None, None, None,
+                    batch_callback=batch_cb, epoch_callback=epoch_cb, do_cuda=True, lr=1e-2, schedule_lr=False,
+                    batch_size=bsz, epochs=1, maxiter_cg=20, batch_log_interval=1, learn_kernel=False)
         torch.cuda.synchronize()
-        K = 10
-        t0 = time.perf_counter()
-        for b in range(2, 2 + K):
-            lval = step(b)
-        torch.cuda.synchronize()
-        ms = (time.perf_counter() - t0) / K * 1e3
-        print(json.dumps({"what": "C3 svigp_fit minibatch step", "model": cls, "learn_kernel": learn_kernel,
-                          "grid": [m, m], "M": m * m, "batch": bsz, "maxiter_cg": maxiter, "dtype": "f32",
-                          "ms_per_step": round(ms, 3), "epoch_s_100k": round(ms * (N // bsz) / 1e3, 3),
-                          "elbo_first": elbos, "elbo_last": float(lval), "steps_timed": K}), flush=True)
-        del mod, nat, hyp
+        stamps.append(time.perf_counter())
+        dts = np.diff(stamps) * 1e3
+        steady = float(np.median(dts[2:])) if len(dts) > 3 else float(np.median(dts))
+        print(json.dumps({"what": "C3 svigp_fit on config 3's settings", "grid": [a.m, a.m], "M": a.m * a.m,
+                          "batch": bsz, "num_obs": N, "batches": a.batches, "maxiter_cg": 20, "dtype": tag,
+                          "lr": 1e-2, "ell": .1, "jitter": 1e-3, "init_Svar": .1, "sig2_init": round(sig2, 5),
+                          "ms_per_batch_median": round(steady, 1), "ms_per_batch": [round(v, 1) for v in dts],
+                          "epoch_s_500_batches": round(steady * 500 / 1e3, 1),
+                          "elbo_trace": traces[0] if traces else None, "theta1_norm": norms}), flush=True)
+        del mod
         torch.cuda.empty_cache()
 
 

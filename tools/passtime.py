@@ -19,6 +19,8 @@ def main():
     ap.add_argument("--rhs", type=int, default=25)
     ap.add_argument("--op", default="K", choices=["K", "CINV", "RT", "R"])
     ap.add_argument("--op-only", type=int, default=0, help="only run the op this many times (PMC passes)")
+    ap.add_argument("--pcg-only", type=int, default=0,
+                    help="only run this many batched PCG(20) solves (the fused iteration's kernels, PMC passes)")
     a = ap.parse_args()
     from hipgp_amd import _lib
     import ziggy.kernels as zk
@@ -50,6 +52,12 @@ def main():
         e.synchronize()
         return s.elapsed_time(e) / reps
 
+    if a.pcg_only:
+        for _ in range(a.pcg_only):
+            plan.pcg(x if a.op != "R" else torch.randn(a.rhs, M, device=dev), 20, 1e-8, precond=True)
+        torch.cuda.synchronize()
+        print(json.dumps({"dims": dims, "rhs": a.rhs, "pcg": a.pcg_only}))
+        return
     if a.op_only:
         for _ in range(a.op_only):
             plan.apply(op, x, out=y)
@@ -62,19 +70,19 @@ def main():
     for p in range(npass):
         passes.append(round(tm(lambda: _lib.check(_lib.lib().hgp_toeplitz_apply_pass(
             plan._h, op, x.data_ptr(), y.data_ptr(), a.rhs, p))), 4))
-    d = len(dims)
-    h = dims[-1]
-    if d == 1:
-        bk = 8 * M
-    elif d == 2:
-        bk = 8 * M + 32 * dims[0] * h
-    else:
-        bk = 8 * M + 32 * dims[0] * dims[1] * h + 32 * dims[0] * (2 * dims[1] - 2) * h
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import byte_model
+    bk = byte_model.op_bytes(a.op, dims)
     out = {"dims": dims, "rhs": a.rhs, "op": a.op, "op_ms": round(op_ms, 4), "passes_ms": passes,
-           "L_K": list(plan.L_K)}
-    if a.op in ("K", "CINV"):
-        out["algo_gbs"] = round(a.rhs * bk / (op_ms * 1e-3) / 1e9, 1)
-        out["frac"] = round(out["algo_gbs"] / 8000, 3)
+           "L_K": list(plan.L_K), "L_R": list(plan.L_R)}
+    out["algo_gbs"] = round(a.rhs * bk / (op_ms * 1e-3) / 1e9, 1)
+    out["model"] = "B_RT" if a.op in ("RT", "R") else "B_K"
+    out["frac"] = round(out["algo_gbs"] / 8000, 3)
+    if a.op in ("RT", "R"):
+        n = byte_model.ngrid(dims)
+        real = all(L >= 2 * v - 1 for L, v in zip(plan.L_R, n))
+        per, spec = byte_model.floor_rt(dims, list(plan.L_R), real_spec=real)
+        out["L_R_floor_gbs"] = round((a.rhs * per + spec) / (op_ms * 1e-3) / 1e9, 1)
     print(json.dumps(out), flush=True)
 
 

@@ -12,4 +12,5 @@ for c in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d $OUT/$c -o run -- \
     python3 tools/passtime.py --dims $SHAPE --rhs $RHS --op ${OP:-K} --op-only $NOPS > $OUT/$c.log 2>&1 || { echo "pmc $c failed"; tail -5 $OUT/$c.log; exit 1; }
 done
-python3 tools/pmc_cfg_summary.py $OUT $NOPS "$SHAPE" $RHS | tee $OUT/summary.txt
+LR=$(grep -o '"L_R": \[[0-9, ]*\]' $OUT/stats.log | head -1 | tr -d '"L_R: []')
+python3 tools/pmc_cfg_summary.py $OUT $NOPS "$SHAPE" $RHS ${OP:-K} "$LR" | tee $OUT/summary.txt

@@ -35,7 +35,12 @@ OVERLAY = {
 
 
 class _OverlayFinder(importlib.abc.MetaPathFinder, importlib.abc.Loader):
-    """Resolves the OVERLAY names to the implementation modules themselves."""
+    """Resolves the OVERLAY names to the implementation modules themselves.
+
+    The import system sets `module.__spec__` to the alias's spec after `create_module`
+    (`importlib._bootstrap._init_module_attrs`); `exec_module` puts the implementation's own
+    spec back, so `__spec__.name == __name__` holds and `importlib.reload` re-executes the
+    implementation module."""
 
     def find_spec(self, fullname, path=None, target=None):
         if fullname in OVERLAY:
@@ -43,10 +48,12 @@ class _OverlayFinder(importlib.abc.MetaPathFinder, importlib.abc.Loader):
         return None
 
     def create_module(self, spec):
-        return importlib.import_module(OVERLAY[spec.name])
+        mod = importlib.import_module(OVERLAY[spec.name])
+        mod.__dict__.setdefault("_overlay_spec", mod.__spec__)
+        return mod
 
     def exec_module(self, module):
-        pass
+        module.__spec__ = module.__dict__["_overlay_spec"]
 
 
 if not any(isinstance(f, _OverlayFinder) for f in sys.meta_path):
