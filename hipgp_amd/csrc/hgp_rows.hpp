@@ -311,75 +311,50 @@ __global__ __launch_bounds__((RowTCfg<T, H, G>::THREADS), (RowTCfg<T, H, G>::MIN
 // x is never read by the recurrence, so moving its update from the A p pass to the C^-1 r pass
 // (where p is read anyway) saves one read of p per iteration with the same arithmetic; a
 // break after the r update is finished by the EPI_XP pass alone (PassDesc::cg_fix).
-// The sweep is software-pipelined: UE elements per thread per batch, the vector loads of batch
-// i + 1 issued before batch i is combined and stored, so a thread has 2 UE loads in flight
-// instead of waiting out one memory round trip per 4 elements (the FFT's registers are dead
-// here).  Rows of exactly 2^k outputs (every power-of-two grid) split the sweep index with
-// shifts instead of a division by the runtime row length.  The vectors never alias.
-#ifndef HGP_EPI_UE
-#define HGP_EPI_UE 8
-#endif
-template <typename T, int EPI, int THREADS, int LOG2LEN>
-__device__ __forceinline__ T cg_epilogue_t(const T* __restrict__ ys, int nrow, int out_len, T* __restrict__ xg,
-                                           T* __restrict__ rg, T* __restrict__ pg, int64_t rpitch, T coef, T coef2) {
-  constexpr int UE = HGP_EPI_UE;
-  const int nel = nrow * out_len;
-  // the block's rows are one < 2 GiB window of each vector: raw buffers, 32-bit lane offsets
-  const BufRsrc rp = buf_rsrc(pg, 0x7fffffffu), rx = buf_rsrc(xg, 0x7fffffffu), rr = buf_rsrc(rg, 0x7fffffffu);
-  auto goff = [&](int e) -> uint32_t {
-    int row, c;
-    if constexpr (LOG2LEN >= 0) { row = e >> LOG2LEN; c = e & ((1 << LOG2LEN) - 1); }
-    else { row = e / out_len; c = e - row * out_len; }
-    return ((uint32_t)row * (uint32_t)rpitch + (uint32_t)c) * (uint32_t)sizeof(T);
-  };
-  T pv[2][UE], xv[2][UE], rv[2][UE];
-  auto load = [&](int e0, int b) {
-#pragma unroll
-    for (int u = 0; u < UE; ++u) {
-      const int e = e0 + u * THREADS;
-      const uint32_t g = goff(e < nel ? e : nel - 1);
-      if constexpr (EPI != EPI_R) pv[b][u] = buf_ld<T>(rp, g);
-      if constexpr (EPI == EPI_XR || EPI == EPI_XP) xv[b][u] = buf_ld<T>(rx, g);
-      if constexpr (EPI == EPI_XR || EPI == EPI_R) rv[b][u] = buf_ld<T>(rr, g);
-    }
-  };
-  T s = 0;
-  const int e_first = threadIdx.x;
-  if (e_first < nel) load(e_first, 0);
-  int b = 0;
-  for (int e0 = e_first; e0 < nel; e0 += UE * THREADS) {
-    if (e0 + UE * THREADS < nel) load(e0 + UE * THREADS, b ^ 1);     // next batch in flight
-#pragma unroll
-    for (int u = 0; u < UE; ++u) {
-      const int e = e0 + u * THREADS;
-      if (e < nel) {
-        const uint32_t g = goff(e);
-        const T yv = ys[e];
-        if constexpr (EPI == EPI_XR || EPI == EPI_R) {
-          if constexpr (EPI == EPI_XR) buf_st<T>(xv[b][u] + coef * pv[b][u], rx, g);
-          const T rn = rv[b][u] - coef * yv;
-          buf_st<T>(rn, rr, g);
-          s += rn * rn;
-        } else {
-          buf_st<T>(xv[b][u] + coef2 * pv[b][u], rx, g);
-          buf_st<T>(yv + coef * pv[b][u], rp, g);
-        }
-      }
-    }
-    b ^= 1;
-  }
-  return s;
-}
-
-template <typename T, int EPI, int THREADS, int H>
+// Four elements per thread are loaded before any is stored (the vectors never alias).
+// (Measured and not kept, round 4: a software-pipelined sweep -- 8 elements per batch, the next
+// batch's loads issued before the current one is stored, shift-based indices -- C2 compute_kn
+// 17.3 -> 19.1 ms.  The epilogue's cost is structural: an 8-RHS C2 dispatch is ONE round of
+// blocks per CU, so the r / p / x loads start only after the FFT and nothing overlaps them.)
+template <typename T, int EPI, int THREADS>
 __device__ __forceinline__ T cg_epilogue(const T* __restrict__ ys, int nrow, int out_len, T* __restrict__ xg,
                                          T* __restrict__ rg, T* __restrict__ pg, int64_t rpitch, T coef,
                                          T coef2 = 0) {
-  if constexpr (is_pow2(H)) {
-    if (out_len == H)       // uniform
-      return cg_epilogue_t<T, EPI, THREADS, ilog2c(H)>(ys, nrow, out_len, xg, rg, pg, rpitch, coef, coef2);
+  const int nel = nrow * out_len;
+  // the block's rows are one < 2 GiB window of each vector: raw buffers, 32-bit lane offsets
+  const BufRsrc rp = buf_rsrc(pg, 0x7fffffffu), rx = buf_rsrc(xg, 0x7fffffffu), rr = buf_rsrc(rg, 0x7fffffffu);
+  T s = 0;
+  for (int e0 = threadIdx.x; e0 < nel; e0 += 4 * THREADS) {
+    uint32_t g[4];
+    T yv[4], pv[4], xv[4], rv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = e0 + u * THREADS;
+      const int ee = e < nel ? e : nel - 1;
+      const int row = ee / out_len;
+      const int c = ee - row * out_len;
+      g[u] = ((uint32_t)row * (uint32_t)rpitch + (uint32_t)c) * (uint32_t)sizeof(T);
+      yv[u] = ys[ee];
+      if constexpr (EPI != EPI_R) pv[u] = buf_ld<T>(rp, g[u]);
+      if constexpr (EPI == EPI_XR || EPI == EPI_XP) xv[u] = buf_ld<T>(rx, g[u]);
+      if constexpr (EPI == EPI_XR || EPI == EPI_R) rv[u] = buf_ld<T>(rr, g[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (e0 + u * THREADS < nel) {
+        if constexpr (EPI == EPI_XR || EPI == EPI_R) {
+          if constexpr (EPI == EPI_XR) buf_st<T>(xv[u] + coef * pv[u], rx, g[u]);
+          const T rn = rv[u] - coef * yv[u];
+          buf_st<T>(rn, rr, g[u]);
+          s += rn * rn;
+        } else {
+          buf_st<T>(xv[u] + coef2 * pv[u], rx, g[u]);
+          buf_st<T>(yv[u] + coef * pv[u], rp, g[u]);
+        }
+      }
+    }
   }
-  return cg_epilogue_t<T, EPI, THREADS, -1>(ys, nrow, out_len, xg, rg, pg, rpitch, coef, coef2);
+  return s;
 }
 
 // The x update of an iteration whose break test fired after its r update (EPI_XP pass of that
@@ -615,7 +590,7 @@ __global__ __launch_bounds__((RowTCfg<T, H, G>::THREADS), (RowTCfg<T, H, G>::MIN
     T* xg = EPI != EPI_R ? reinterpret_cast<T*>(d.cg_x) + g0 : pg;
     T* rg = EPI != EPI_XP ? reinterpret_cast<T*>(d.cg_r) + g0 : pg;
     const T coef2 = EPI == EPI_XP ? reinterpret_cast<const T*>(d.cg_coef2)[qc] : (T)0;
-    T s = cg_epilogue<T, EPI, Cfg::THREADS, H>(ys, nrow_blk, out_len, xg, rg, pg, d.out.r_stride, coef, coef2);
+    T s = cg_epilogue<T, EPI, Cfg::THREADS>(ys, nrow_blk, out_len, xg, rg, pg, d.out.r_stride, coef, coef2);
     if constexpr (EPI == EPI_XR || EPI == EPI_R) {   // deterministic block sum of r.r -> partial [q][rb]
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);

@@ -20,8 +20,11 @@ ELBO returned by `elbo_and_grad` carries the autograd graph through Knm, Knn and
 backward PCG + hgp_plan_dqf, the R^T column gradient hgp_plan_column_grad), as the reference's
 fit loop needs it (`svi_gp.py:317-326`).
 
-Not built here (OUT of the hot path): the full-rank variational family and
-`batch_solve`'s dense M'xM' system.
+`batch_solve` (`hipgp.py:278-368`, the full-batch solve of the mean-field family) is built:
+one compute_kn per batch and the device statistics kernel, with the reference's
+UnboundLocalError at `hipgp.py:314` fixed (parity pinned by the oracle restatement only).
+Not built (OUT of the hot path): the full-rank variational family
+(`FullRankToeplitzGP`, `hipgp.py:693-797`: a dense M' x M' covariance, 70 TB at C2).
 """
 import numpy as np
 import torch

@@ -66,6 +66,74 @@ def test_solve_compute_kn_C5_B25():
     assert rel_x < 1e-3 and rel_kn < 1e-3, (rel_x, rel_kn)
 
 
+def _ref_op_torch(column, dims, which, v):
+    """The reference's own arithmetic for one operator (`toeplitz_tensor.py:20-31,70-125`:
+    circulant embedding, D = clamp(Re FFT_n(C), 1e-6), pad -> FFT_n -> x S -> IFFT_n -> crop) in
+    the dtype of `column` / `v`, with torch.fft on the GPU -- the yardstick "the reference's own
+    fp32 error" of SURVEY §8(c) at a size the CPU oracle cannot run in a test (TEST ORACLE ONLY)."""
+    C = column.reshape(dims)
+    for d, m in enumerate(dims):
+        C = torch.cat([C, torch.flip(C, [d]).narrow(d, 1, m - 2)], dim=d)
+    D = torch.fft.fftn(C).real.clamp(min=1e-6)
+    S = {"K": D, "Cinv": 1 / D, "RT": torch.sqrt(D)}[which]
+    n = C.shape
+    B = v.shape[0]
+    out = []
+    for b in range(B):                     # one RHS at a time: the n-grid is 66 M points
+        Vp = torch.zeros(n, dtype=v.dtype, device=v.device)
+        Vp[:dims[0], :dims[1], :dims[2]] = v[b].reshape(dims)
+        Y = torch.fft.ifftn(S * torch.fft.fftn(Vp)).real
+        out.append((Y if which == "RT" else Y[:dims[0], :dims[1], :dims[2]]).reshape(-1))
+        del Vp, Y
+    return torch.stack(out)
+
+
+def test_solve_C5_config5_hyperparameters():
+    """Config 5's OWN kernel settings (Matern-5/2, sig2 .1, ell .1, nugget 1e-3,
+    `run_domain_experiment.py:77-82`):
+    * the operators: fp32 no worse than 4x the reference's own fp32 arithmetic against fp64
+      (at these settings 1/D reaches 1e6 at the clamp and C^-1 amplifies FFT noise:
+      the reference's fp32 C^-1 is itself percent-level off), with the reference's arithmetic run
+      by torch.fft on the GPU (`_ref_op_torch`);
+    * 20 PCG iterations stay far from the solution there, so the fp32 iterate is pinned by its
+      TRUE residual |K x - b| (K of the fp64 plan) against the fp64 plan's own after the same 20
+      iterations -- the rule the clamped goldens G4a-c use."""
+    import ziggy.kernels as zk
+    from ziggy.misc.toeplitz_tensor import ToeplitzTensor
+    B = 4
+    M = int(np.prod(DIMS))
+    g = torch.Generator(device=DEV).manual_seed(37)
+    b64 = torch.randn(B, M, device=DEV, generator=g, dtype=torch.float64)
+    T = {}
+    for dt in (torch.float64, torch.float32):
+        k = zk.Matern(nu=2.5, dtype=dt)
+        T[dt] = ToeplitzTensor(_grids(dt), lambda x, y, k=k: k.forward(x, y, params=(0.1, 0.1)), jitter_val=1e-3)
+        T[dt].set_batch_shape((B,))
+    T64, T32 = T[torch.float64], T[torch.float32]
+    for which, name in (("K", "_matmul_by_K"), ("Cinv", "_matmul_by_Cinv"), ("RT", "_matmul_by_RT")):
+        y64 = _ref_op_torch(T64.column, DIMS, which, b64)
+        r32 = _ref_op_torch(T32.column, DIMS, which, b64.float()).double()
+        me32 = getattr(T32, name)(b64.float()).double()
+        me64 = getattr(T64, name)(b64)
+        scale = float(y64.abs().max())
+        e_me, e_ref = float((me32 - y64).abs().max()), float((r32 - y64).abs().max())
+        e_64 = float((me64 - y64).abs().max())
+        print(f"C5 config-5 {which}: fp32 err {e_me / scale:.3e} (reference's own fp32 {e_ref / scale:.3e}), "
+              f"fp64 {e_64 / scale:.3e}")
+        assert e_64 <= 1e-9 * scale, (which, e_64 / scale)
+        assert e_me <= 4 * e_ref + 1e-5 * scale, (which, e_me / scale, e_ref / scale)
+        del y64, r32, me32, me64
+        torch.cuda.empty_cache()
+    res = {}
+    for dt, Tt in T.items():
+        x = Tt._solve(b64.to(dt), do_precond=True, maxiter=20, tol=1e-8).double()
+        res[dt] = ((T64._matmul_by_K(x) - b64).norm(dim=1) / b64.norm(dim=1)).cpu().numpy()
+    r64, r32 = res[torch.float64], res[torch.float32]
+    print("C5 config-5 settings: true residual after 20 iterations fp64", r64, "fp32", r32)
+    assert np.all(np.isfinite(r32)) and np.all(r64 < 10)
+    assert np.all(r32 <= 3 * r64 + 1e-3), (r32, r64)
+
+
 @pytest.mark.parametrize("estimator", ["analytic", "mc-biased"])
 def test_integrated_elbo_C5(estimator, monkeypatch):
     import ziggy.hipgp as hg

@@ -5,7 +5,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests/test_slab_gpu.py tests/test_fit_c3_gpu.py tests/test_long_axis_gpu.py tests/test_model_gpu.py -v --timeout 300 --timeout-method thread > gpurun_out/pytest_b.log 2>&1
+timeout -k 10 900 python -u -m pytest tests/test_slab_gpu.py tests/test_fit_c3_gpu.py tests/test_long_axis_gpu.py tests/test_model_gpu.py "tests/test_fullsize_c5_gpu.py::test_solve_C5_config5_hyperparameters" -v --timeout 300 --timeout-method thread > gpurun_out/pytest_b.log 2>&1
 rc=$?; grep -E "PASS|FAIL|Error" gpurun_out/pytest_b.log | tail -40; [ $rc -le 1 ] || exit 1
 for ws in 0 2048 4096 8192 16384; do
   for cfg in "4096,4096 25" "2048,2048 200" "1024,1024 32"; do

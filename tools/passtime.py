@@ -80,8 +80,9 @@ def main():
     out["frac"] = round(out["algo_gbs"] / 8000, 3)
     if a.op in ("RT", "R"):
         n = byte_model.ngrid(dims)
-        real = all(L >= 2 * v - 1 for L, v in zip(plan.L_R, n))
-        per, spec = byte_model.floor_rt(dims, list(plan.L_R), real_spec=real)
+        LR = list(plan.L_R)[:len(dims)]
+        real = all(L >= 2 * v - 1 for L, v in zip(LR, n))
+        per, spec = byte_model.floor_rt(dims, LR, real_spec=real)
         out["L_R_floor_gbs"] = round((a.rhs * per + spec) / (op_ms * 1e-3) / 1e9, 1)
     print(json.dumps(out), flush=True)
 
