@@ -34,6 +34,24 @@
 
 namespace hgp {
 
+// Phase stagger of the long-row passes (knob, default off).  A 4096-point row block fills a CU
+// alone (16 waves at ~117 VGPRs), and every CU starts its first block at the launch: all CUs then
+// load, transform and store in step, so HBM idles during the transforms.  With HGP_ROW_STAGGER = n
+// the first-round blocks of every other CU (hardware order: workgroup i -> XCD i % 8, its
+// (i / 8)-th block) sleep n x 127 x 64 clocks first, so half the CUs run half a block out of phase.
+#ifndef HGP_ROW_STAGGER
+#define HGP_ROW_STAGGER 0
+#endif
+template <int THREADS>
+__device__ __forceinline__ void row_stagger() {
+  if constexpr (HGP_ROW_STAGGER > 0 && THREADS >= 1024) {
+    if (blockIdx.x < 256u && ((blockIdx.x >> 3) & 1u)) {
+#pragma unroll 1
+      for (int i = 0; i < HGP_ROW_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
+    }
+  }
+}
+
 // Grouped columns (long fp32 rows).  A block's tile is 2C rows of every compact column; with the
 // plain column-major intermediate W[c][i0] its stores / loads are 2C x sizeof(complex) segments,
 // and at H = 4096 the LDS (four 4096-point exchange images, 139 KB) holds one 4-pair block per
@@ -216,6 +234,7 @@ __global__ __launch_bounds__((RowTCfg<T, H, G>::THREADS), (RowTCfg<T, H, G>::MIN
   using Cfg = RowTCfg<T, H, G>;
   constexpr int P = Cfg::P, TT = Cfg::TT, C = Cfg::C;
   if (d.done != nullptr && *d.done) return;
+  row_stagger<Cfg::THREADS>();
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   C2<T>* lds = reinterpret_cast<C2<T>*>(smem_raw);
   C2<T>* tab = lds + Cfg::AREA;
@@ -397,6 +416,7 @@ __global__ __launch_bounds__((RowTCfg<T, H, G>::THREADS), (RowTCfg<T, H, G>::MIN
       return;
     }
   }
+  row_stagger<Cfg::THREADS>();
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   C2<T>* lds = reinterpret_cast<C2<T>*>(smem_raw);
   C2<T>* tab = lds + Cfg::AREA;
