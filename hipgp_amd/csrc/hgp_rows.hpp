@@ -65,12 +65,13 @@ __device__ __forceinline__ void row_stagger() {
 #ifndef HGP_ROWG_2048
 #define HGP_ROWG_2048 2           // G at H = 2048 (fp32): 4 pairs x 2 columns = 128 B
 #endif
-// H >= 4096: G = 4 (2 pairs x 4 columns = 128 B) speeds both row passes (C4: 1.41 -> 1.16 ms,
-// 1.71 -> 1.63 ms) but the axis-0 pass reading one column of every 32 B loses more (2.52 -> 2.97
-// ms; the interleaved LAY_GRP4 blocks 3.85 ms): C4 K matvec 5.64 (G = 1) vs 5.78 ms (G = 4),
-// profiles/r3_grouped_passtime.txt.  Plain layout there; G = 2 at H = 2048 (C3 1.71 -> 1.63 ms).
+// H >= 4096: G = 4 (2 pairs x 4 columns = 128 B).  Round 3 (before the spill fixes) measured the
+// axis-0 pass reading one column of every 32 B losing more than the rows gained (C4 K matvec 5.64
+// plain vs 5.78 ms).  Round 4, on the spill-free kernels (profiles/r4_e_grouped4096_K_Cinv.txt):
+// rows 1.44 -> 1.12 and 1.52 -> 1.16 ms, the axis-0 pass 2.03 -> 2.41 ms, K matvec 4.98 -> 4.83 ms,
+// C^-1 4.96 -> 4.82 ms (G = 2: 4.91 / 4.99) -- so G = 4.
 #ifndef HGP_ROWG_4096
-#define HGP_ROWG_4096 1
+#define HGP_ROWG_4096 4
 #endif
 // pairs per block of the grouped 4096-point rows (0: 8 / G, i.e. 128-B segments).  2 with G = 2:
 // 64-B segments but a 70 KB block, two per CU.
