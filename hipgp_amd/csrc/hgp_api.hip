@@ -98,7 +98,10 @@ struct hgp_plan {
   size_t esz = 4;
   // tables
   DevBuf twK[3], twR[3], tw64K[3], tw64R[3];
-  DevBuf tw64Rh[3];                       // W_{L_R/2}^q for L_R/2 > 16384-point lines (fft_lines_f64)
+  // fp64 twiddles of the radix-2 levels of fft_lines_f64 for lines longer than one CU's LDS:
+  // level j >= 1 of axis a holds W_{L/2^j} (L = L_K: tw64Kl, L_R: tw64Rl), down to the base pass
+  static constexpr int NLEV = 8;
+  DevBuf tw64Kl[3][NLEV], tw64Rl[3][NLEV];
   DevBuf bsPre[3], bsPost[3], bsFilt[3];   // Bluestein DCT-I tables per axis (fp64)
   // spectra
   DevBuf specK, specI, specR, Dm3;
@@ -109,7 +112,11 @@ struct hgp_plan {
   // fp64 plans whose L_R lines exceed one CU's LDS (L_R / 2 > 8192): R / R^T on the full fp64
   // grid (run_op_grid: fwd_grid_f64's radix-2 step), spectrum in the transforms' stored order
   bool grid_r = false;
-  DevBuf specRg, gridA, gridB;
+  // plans with an axis longer than the passes hold (> 8192 points, both dtypes): K / C^-1 on the
+  // full fp64 L_K grid as well (run_op_grid), spectrum in the transforms' stored order: K in the
+  // real parts, C^-1 in the imaginary parts of specKg
+  bool grid_k = false;
+  DevBuf specRg, specKg, gridA, gridB;
   double clamp_min = 1e-6;                // of the last set_column (the clamp's gradient mask)
   DevBuf nclamp;
   // scratch
@@ -160,10 +167,11 @@ struct hgp_plan {
     drop_graph();
     if (cap_stream) (void)hipStreamDestroy(cap_stream);
     for (int a = 0; a < 3; ++a) {
-      twK[a].release(); twR[a].release(); tw64K[a].release(); tw64R[a].release(); tw64Rh[a].release();
+      twK[a].release(); twR[a].release(); tw64K[a].release(); tw64R[a].release();
+      for (int j = 0; j < NLEV; ++j) { tw64Kl[a][j].release(); tw64Rl[a][j].release(); }
       bsPre[a].release(); bsPost[a].release(); bsFilt[a].release();
     }
-    DevBuf* bufs[] = {&specK, &specI, &specR, &specRg, &gridA, &gridB, &Dm3, &nclamp, &ws1, &ws2, &set1, &set2, &setM1, &setM2, &setC,
+    DevBuf* bufs[] = {&specK, &specI, &specR, &specRg, &specKg, &gridA, &gridB, &Dm3, &nclamp, &ws1, &ws2, &set1, &set2, &setM1, &setM2, &setC,
                       &r, &z, &p, &Ap, &part_op, &part_u, &part_f, &scal, &flags, &bT, &xT};
     for (DevBuf* b : bufs) b->release();
     for (int i = 0; i < 3; ++i) {
@@ -296,14 +304,21 @@ using MidFn = std::function<void(int64_t, int, hipStream_t)>;
 // the fused PCG update, `mid` runs between the column pass and the row-inverse pass.
 int fwd_grid_f64(hgp_plan* P, const int64_t* L, const DevBuf* tw64, double2* a, double2* b, double2** result);
 
-// R / R^T of a grid_r plan, one RHS at a time on the full fp64 L_R grid:
-// y = crop(IFFT(S' FFT(pad x))), S' = S (R^T) or conj(S) (R), the inverse as conj(FFT(conj Y)) / N.
-// Exact like the pass route (same spectrum, fp64 throughout); memory 2 prod(L_R) complex fp64.
+// The full-grid route, one RHS at a time on the full fp64 L-grid of the operator:
+// y = crop(IFFT(S' FFT(pad x))), the inverse as conj(FFT(conj Y)) / N (the 1/N is in the stored
+// spectrum).  R / R^T of grid_r plans on the L_R grid (S' = S for R^T, conj(S) for R, specRg);
+// K / C^-1 of grid_k plans on the L_K grid (S' = Re / Im of specKg, the packed K + i C^-1
+// transform).  Exact like the pass route (same spectra, fp64 throughout); memory 2 prod(L)
+// complex fp64.  A fused dot (dotv) becomes per-RHS row-chunk partials of y . dotv
+// (rowdot_part: update_np(out M) per RHS, the unfused PCG's op_np).
 template <typename T>
-int run_op_grid(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs) {
+int run_op_grid(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void* dotv, void* partial) {
   hipStream_t s = P->stream;
   const int d = P->d;
-  const int64_t N = P->prodLR;
+  const bool rtype = op == HGP_OP_R || op == HGP_OP_RT;
+  const int64_t* Lg = rtype ? P->LR : P->LK;
+  const DevBuf* tw64 = rtype ? P->tw64R : P->tw64K;
+  const int64_t N = rtype ? P->prodLR : P->prodLK;
   HGP_TRY(P->gridA.ensure((size_t)N * sizeof(double2)));
   HGP_TRY(P->gridB.ensure((size_t)N * sizeof(double2)));
   double2* A = reinterpret_cast<double2*>(P->gridA.ptr);
@@ -312,36 +327,45 @@ int run_op_grid(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs) {
   gi.d = go.d = d;
   int64_t inM = 1, outM = 1;
   for (int a = 0; a < 3; ++a) {
-    gi.L[a] = go.L[a] = P->LR[a];
+    gi.L[a] = go.L[a] = Lg[a];
     gi.n[a] = go.n[a] = P->n[a];
     gi.m[a] = (op == HGP_OP_R) ? P->n[a] : P->m[a];
     go.m[a] = (op == HGP_OP_RT) ? P->n[a] : P->m[a];
     if (a < d) { inM *= gi.m[a]; outM *= go.m[a]; }
   }
-  const double2* S = reinterpret_cast<const double2*>(P->specRg.ptr);
+  const double2* S = reinterpret_cast<const double2*>(rtype ? P->specRg.ptr : P->specKg.ptr);
+  const int mode = op == HGP_OP_R ? 1 : op == HGP_OP_RT ? 0 : op == HGP_OP_K ? 2 : 3;
   const size_t es = P->esz;
   for (int64_t q = 0; q < nrhs; ++q) {
     grid_embed(P->dtype, static_cast<const char*>(x) + (size_t)(q * inM) * es, gi, N, A, s);
     double2* F = nullptr;
-    HGP_TRY(fwd_grid_f64(P, P->LR, P->tw64R, A, B, &F));
+    HGP_TRY(fwd_grid_f64(P, Lg, tw64, A, B, &F));
     double2* other = (F == A) ? B : A;
-    grid_mul_unperm(F, S, gi, N, op == HGP_OP_R ? 1 : 0, other, s);
+    grid_mul_unperm(F, S, gi, N, mode, other, s);
     double2* Z = nullptr;
-    HGP_TRY(fwd_grid_f64(P, P->LR, P->tw64R, other, F, &Z));
+    HGP_TRY(fwd_grid_f64(P, Lg, tw64, other, F, &Z));
     grid_crop(P->dtype, Z, go, outM, static_cast<char*>(y) + (size_t)(q * outM) * es, s);
   }
+  if (dotv != nullptr && partial != nullptr)
+    rowdot_part<T>(y, dotv, partial, nrhs, outM, update_np(outM), s);
   HIP_TRY(hipGetLastError());
   return 0;
+}
+
+bool grid_route(const hgp_plan* P, int op) {
+  return (op == HGP_OP_R || op == HGP_OP_RT) ? P->grid_r : P->grid_k;
 }
 
 template <typename T>
 int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void* dotv, void* partial,
            const int* done, int only_pass = -1, void* spart = nullptr, const RowEpi* epi = nullptr,
            const MidFn* mid = nullptr) {
-  if (P->grid_r && (op == HGP_OP_R || op == HGP_OP_RT)) {
-    if (dotv != nullptr || partial != nullptr || spart != nullptr || epi != nullptr || mid != nullptr || only_pass >= 0)
-      return fail(HGP_E_UNSUPPORTED, "internal: the full-grid R / R^T route has no fused dot or pass split");
-    return run_op_grid<T>(P, op, x, y, nrhs);
+  if (grid_route(P, op)) {
+    if (spart != nullptr || epi != nullptr || mid != nullptr || only_pass >= 0)
+      return fail(HGP_E_UNSUPPORTED, "internal: the full-grid route has no fused PCG epilogue or pass split");
+    // (`done` is not checked here: after the break the unfused PCG's update kernels are device
+    // no-ops, and what this route still writes -- Ap / z and the dot partials -- is never read)
+    return run_op_grid<T>(P, op, x, y, nrhs, dotv, partial);
   }
   const OpGeom g = op_geom(P, op);
   const int d = P->d;
@@ -640,51 +664,70 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
 }
 
 // Forward fp64 FFT of length L along lines r < Rn (stride r_stride) x inner lines i < In
-// (adjacent), positions at stride ps: in -> out (in may be clobbered), output in the pass
-// order (index half*L/2 + k = frequency 2k + half).  Lines of L/2 <= 8192 points are one k_pass;
-// longer ones (L_R = 32768 of an axis of 4098..8192 points) are one radix-2 step: the two
-// interleaved half-length subsequences transformed in place by a strided k_pass (twiddles
-// W_{L/2}, tw_half), then k_r2_combine into the order of the full length.
-int fft_lines_f64(hgp_plan* P, double2* in, double2* out, int64_t L, int64_t Rn, int64_t r_stride, int64_t In,
-                  int64_t ps, const void* tw, const void* tw_half) {
+// (adjacent), positions at stride ps, output in the pass order (index half*L/2 + k = frequency
+// 2k + half).  Lines of L/2 <= 8192 points are one k_pass (a -> b).  Longer ones (the L_R = 32768
+// of an axis of 4098..8192 points, and every axis beyond 8192 points) take radix-2 steps, as
+// deep as needed: the two interleaved half-length subsequences (stride 2 ps) are transformed
+// the same way, then k_r2_combine merges them into the pass order of the full length.  Every
+// level moves its lines between the two buffers, so the result may end in either: *result.
+// tw = W_L; lev[j] = W_{L / 2^(j+1)} (the plan's tw64Kl / tw64Rl of the axis).
+int fft_lines_f64(hgp_plan* P, double2* a, double2* b, int64_t L, int64_t Rn, int64_t r_stride, int64_t In,
+                  int64_t ps, const void* tw, const DevBuf* lev, int depth, double2** result) {
   hipStream_t s = P->stream;
   if (L / 2 <= 8192) {
     PassDesc D = base_desc();
-    D.in = View{in, 0, r_stride, ps, (int)L};
-    D.out = View{out, 0, r_stride, ps, (int)L};
+    D.in = View{a, 0, r_stride, ps, (int)L};
+    D.out = View{b, 0, r_stride, ps, (int)L};
     D.tw = tw; D.Q = 1; D.Rn = (int)Rn; D.In = (int)In;
-    if (ps == 1 && In == 1) return launch<double>((int)(L / 2), PASS_FWD, LAY_CONTIG, D, Rn, s);
-    return launch<double>((int)(L / 2), PASS_FWD, LAY_STRIDED, D, 0, s);
+    if (ps == 1 && In == 1) HGP_TRY(launch<double>((int)(L / 2), PASS_FWD, LAY_CONTIG, D, Rn, s));
+    else HGP_TRY(launch<double>((int)(L / 2), PASS_FWD, LAY_STRIDED, D, 0, s));
+    *result = b;
+    return 0;
   }
-  if (L / 2 > 16384 || tw_half == nullptr) return fail(HGP_E_UNSUPPORTED, "fp64 transform longer than 32768 points");
-  PassDesc D = base_desc();       // q = line r, r = subsequence e (offset e * ps), i = inner line
-  D.in = View{in, r_stride, ps, 2 * ps, (int)(L / 2)};
-  D.out = View{in, r_stride, ps, 2 * ps, (int)(L / 2)};
-  D.tw = tw_half; D.Q = (int)Rn; D.Rn = 2; D.In = (int)In;
-  HGP_TRY(launch<double>((int)(L / 4), PASS_FWD, LAY_STRIDED, D, 0, s));
-  r2_combine(in, out, L, Rn, r_stride, In, ps, reinterpret_cast<const double2*>(tw), s);
+  if (lev == nullptr || depth >= hgp_plan::NLEV || lev[depth].ptr == nullptr || L % 4 != 0)
+    return fail(HGP_E_UNSUPPORTED, "fp64 transform of " + std::to_string(L) + " points: no radix-2 twiddle level");
+  double2* half_res = nullptr;
+  for (int e = 0; e < 2; ++e) {
+    double2* r = nullptr;
+    HGP_TRY(fft_lines_f64(P, a + e * ps, b + e * ps, L / 2, Rn, r_stride, In, 2 * ps, lev[depth].ptr, lev, depth + 1, &r));
+    half_res = (r == a + e * ps) ? a : b;
+  }
+  double2* dst = (half_res == a) ? b : a;
+  r2_combine(half_res, dst, L, Rn, r_stride, In, ps, reinterpret_cast<const double2*>(tw), s);
   HIP_TRY(hipGetLastError());
+  *result = dst;
   return 0;
+}
+
+// the radix-2 twiddle levels matching an axis twiddle table of the plan (nullptr: none)
+const DevBuf* tw_levels(const hgp_plan* P, const DevBuf* tw64, int ax) {
+  if (tw64 == P->tw64R) return P->tw64Rl[ax];
+  if (tw64 == P->tw64K) return P->tw64Kl[ax];
+  return nullptr;
 }
 
 // Forward FFT of a full (unpruned) fp64 complex L-grid: a -> result pointer (a or b).
 int fwd_grid_f64(hgp_plan* P, const int64_t* L, const DevBuf* tw64, double2* a, double2* b, double2** result) {
   const int d = P->d;
-  const DevBuf* twh = (tw64 == P->tw64R) ? P->tw64Rh : nullptr;
-  auto half = [&](int ax) -> const void* { return twh ? twh[ax].ptr : nullptr; };
+  double2* cur = a;
+  double2* oth = b;
+  auto step = [&](int ax, int64_t Rn, int64_t rs, int64_t In, int64_t ps) -> int {
+    double2* r = nullptr;
+    HGP_TRY(fft_lines_f64(P, cur, oth, L[ax], Rn, rs, In, ps, tw64[ax].ptr, tw_levels(P, tw64, ax), 0, &r));
+    if (r != cur) std::swap(cur, oth);
+    return 0;
+  };
   if (d == 1) {
-    HGP_TRY(fft_lines_f64(P, a, b, L[0], 1, L[0], 1, 1, tw64[0].ptr, half(0)));
-    *result = b;
+    HGP_TRY(step(0, 1, L[0], 1, 1));
   } else if (d == 2) {
-    HGP_TRY(fft_lines_f64(P, a, b, L[1], L[0], L[1], 1, 1, tw64[1].ptr, half(1)));
-    HGP_TRY(fft_lines_f64(P, b, a, L[0], 1, 0, L[1], L[1], tw64[0].ptr, half(0)));
-    *result = a;
+    HGP_TRY(step(1, L[0], L[1], 1, 1));
+    HGP_TRY(step(0, 1, 0, L[1], L[1]));
   } else {
-    HGP_TRY(fft_lines_f64(P, a, b, L[2], L[0] * L[1], L[2], 1, 1, tw64[2].ptr, half(2)));
-    HGP_TRY(fft_lines_f64(P, b, a, L[1], L[0], L[1] * L[2], L[2], L[2], tw64[1].ptr, half(1)));
-    HGP_TRY(fft_lines_f64(P, a, b, L[0], 1, 0, L[1] * L[2], L[1] * L[2], tw64[0].ptr, half(0)));
-    *result = b;
+    HGP_TRY(step(2, L[0] * L[1], L[2], 1, 1));
+    HGP_TRY(step(1, L[0], L[1] * L[2], L[2], L[2]));
+    HGP_TRY(step(0, 1, 0, L[1] * L[2], L[1] * L[2]));
   }
+  *result = cur;
   return 0;
 }
 
@@ -744,11 +787,21 @@ int make_bluestein(hgp_plan* P, int ax) {
   DevBuf h;
   HGP_TRY(h.ensure((size_t)L * sizeof(double2)));
   chirp_filter(reinterpret_cast<double2*>(h.ptr), m, n, L, 1.0 / (double)L, s);
-  PassDesc D = base_desc();
-  D.in = View{h.ptr, L, L, 1, (int)L};
-  D.out = View{P->bsFilt[ax].ptr, L, L, 1, (int)L};
-  D.tw = P->tw64K[ax].ptr; D.Q = 1; D.Rn = 1; D.In = 1;
-  int rc = launch<double>((int)(L / 2), PASS_FWD, LAY_CONTIG, D, 1, s);
+  int rc = 0;
+  if (L / 2 <= 8192) {
+    PassDesc D = base_desc();
+    D.in = View{h.ptr, L, L, 1, (int)L};
+    D.out = View{P->bsFilt[ax].ptr, L, L, 1, (int)L};
+    D.tw = P->tw64K[ax].ptr; D.Q = 1; D.Rn = 1; D.In = 1;
+    rc = launch<double>((int)(L / 2), PASS_FWD, LAY_CONTIG, D, 1, s);
+  } else {           // an axis of more than 8192 points: the radix-2 levels (pass order as above)
+    double2* hp = reinterpret_cast<double2*>(h.ptr);
+    double2* fp = reinterpret_cast<double2*>(P->bsFilt[ax].ptr);
+    double2* r = nullptr;
+    rc = fft_lines_f64(P, hp, fp, L, 1, L, 1, 1, P->tw64K[ax].ptr, P->tw64Kl[ax], 0, &r);
+    if (rc == 0 && r != fp && hipMemcpyAsync(fp, r, (size_t)L * sizeof(double2), hipMemcpyDeviceToDevice, s) != hipSuccess)
+      rc = fail(HGP_E_HIP, "bluestein filter copy");
+  }
   if (rc == 0 && hipStreamSynchronize(s) != hipSuccess) rc = fail(HGP_E_HIP, "bluestein filter FFT");
   h.release();
   return rc;
@@ -769,6 +822,28 @@ int dct_axis(hgp_plan* P, int ax, const double* in, double* out, int nb, double 
   const double2* pre = reinterpret_cast<const double2*>(P->bsPre[ax].ptr);
   const double2* post = reinterpret_cast<const double2*>(P->bsPost[ax].ptr);
   chirp_pre(in, pre, c, total, m, I, s);
+  if (L / 2 > 8192) {
+    // an axis of more than 8192 points: the Bluestein convolution as forward transform (radix-2
+    // levels, pass order), x filter (pass order), un-permuted to the natural order, and the
+    // inverse as conj(FFT(conj .)) over [O][L][I] line batches
+    DevBuf e1, e2;                   // freed after the stream sync below
+    HGP_TRY(e1.ensure((size_t)(O * L * I) * sizeof(double2)));
+    HGP_TRY(e2.ensure((size_t)(O * L * I) * sizeof(double2)));
+    double2* E1 = reinterpret_cast<double2*>(e1.ptr);
+    double2* E2 = reinterpret_cast<double2*>(e2.ptr);
+    line_embed(c, E1, O, m, I, L, s);
+    double2* X = nullptr;
+    HGP_TRY(fft_lines_f64(P, E1, E2, L, O, L * I, I, I, P->tw64K[ax].ptr, P->tw64Kl[ax], 0, &X));
+    double2* Z = X == E1 ? E2 : E1;
+    line_mul_unperm_conj(X, reinterpret_cast<const double2*>(P->bsFilt[ax].ptr), Z, O, L, I, s);
+    double2* Y = nullptr;
+    HGP_TRY(fft_lines_f64(P, Z, X, L, O, L * I, I, I, P->tw64K[ax].ptr, P->tw64Kl[ax], 0, &Y));
+    line_unperm_conj(Y, c, O, L, I, m, s);
+    chirp_post(c, post, out, total, m, I, scale, s);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(s));
+    return 0;
+  }
   PassDesc D = base_desc();
   D.spec = P->bsFilt[ax].ptr; D.spec_kind = SPEC_CPLX; D.spec_i = 0; D.spec_r = 0; D.spec_p = 1;
   D.tw = P->tw64K[ax].ptr; D.Q = 1;
@@ -835,36 +910,46 @@ int set_column_t(hgp_plan* P, const void* column, double jitter, double clamp_mi
   embed_K(cK, cI, g1, gd, s);
   double2* F = nullptr;
   HGP_TRY(fwd_grid_f64(P, P->LK, P->tw64K, g1, g2, &F));
+  if (P->grid_k) {
+    // K / C^-1 on the full grid: the packed transform itself (K real, C^-1 imaginary), / N
+    HGP_TRY(P->specKg.ensure((size_t)P->prodLK * sizeof(double2)));
+    scale_copy(F, reinterpret_cast<double2*>(P->specKg.ptr), P->prodLK, 1.0 / (double)P->prodLK, s);
+  }
   const int compact = d > 1 ? 1 : 0;
   const int64_t LKl = P->LK[d - 1], LRl = P->LR[d - 1];
   const int64_t SK = compact ? compact_stride(LKl) : LKl, SR = compact ? compact_stride(LRl) : LRl;
   // 3-D: [c2][k1][k0] (c2 <= H2, no pitch padding), the contiguous axis-0 lines (q, c2, k1)
   const int64_t nK = d == 3 ? P->prodLK / LKl * (LKl / 2 + 1) : P->prodLK / LKl * SK;
   const int64_t nR = d == 3 ? P->prodLR / LRl * (LRl / 2 + 1) : P->prodLR / LRl * SR;
-  HGP_TRY(P->specK.ensure((size_t)nK * sizeof(T)));
-  HGP_TRY(P->specI.ensure((size_t)nK * sizeof(T)));
-  // d >= 2: spectra transposed to [compact column][k1][k0] for the contiguous axis-0 pass
-  if (d == 1)
-    extract_pair<T>(F, P->specK.ptr, P->specI.ptr, nK, LKl, SK, compact, 1.0 / (double)P->prodLK, s);
-  else
-    extract_t<T>(F, P->specK.ptr, P->specI.ptr, P->LK[0], d == 3 ? P->LK[1] : 1, LKl / 2, LKl, 0,
-                 1.0 / (double)P->prodLK, s);
+  if (!P->grid_k) {   // the pass spectra (grid_k plans run K / C^-1 on the full grid)
+    HGP_TRY(P->specK.ensure((size_t)nK * sizeof(T)));
+    HGP_TRY(P->specI.ensure((size_t)nK * sizeof(T)));
+    // d >= 2: spectra transposed to [compact column][k1][k0] for the contiguous axis-0 pass
+    if (d == 1)
+      extract_pair<T>(F, P->specK.ptr, P->specI.ptr, nK, LKl, SK, compact, 1.0 / (double)P->prodLK, s);
+    else
+      extract_t<T>(F, P->specK.ptr, P->specI.ptr, P->LK[0], d == 3 ? P->LK[1] : 1, LKl / 2, LKl, 0,
+                   1.0 / (double)P->prodLK, s);
+  }
   for (int ax = 0; ax < 3; ++ax) gd.L[ax] = P->LR[ax];
   bool long_r = false;
   for (int ax = 0; ax < d; ++ax) long_r = long_r || P->LR[ax] / 2 > 8192;
   bool sym = d >= 2 && !long_r;
   for (int ax = 0; ax < d; ++ax) sym = sym && P->LR[ax] >= 2 * P->n[ax] - 1;
-  P->r_real = sym;
-  HGP_TRY(P->specR.ensure((size_t)nR * (sym ? sizeof(T) : sizeof(C2<T>))));
-  if (d == 1) {
+  P->r_real = sym && !P->grid_r;
+  if (P->grid_r) {
+    // R / R^T on the full grid only (run_op_grid): the complex transform in its stored order, / N
+    embed_R(sv, g1, gd, s);
+    HGP_TRY(fwd_grid_f64(P, P->LR, P->tw64R, g1, g2, &F));
+    HGP_TRY(P->specRg.ensure((size_t)P->prodLR * sizeof(double2)));
+    scale_copy(F, reinterpret_cast<double2*>(P->specRg.ptr), P->prodLR, 1.0 / (double)P->prodLR, s);
+  } else if (d == 1) {
+    HGP_TRY(P->specR.ensure((size_t)nR * sizeof(C2<T>)));
     embed_R(sv, g1, gd, s);
     HGP_TRY(fwd_grid_f64(P, P->LR, P->tw64R, g1, g2, &F));
     extract_cplx<T>(F, P->specR.ptr, nR, LRl, SR, compact, 1.0 / (double)P->prodLR, s);
-    if (P->grid_r) {
-      HGP_TRY(P->specRg.ensure((size_t)P->prodLR * sizeof(double2)));
-      scale_copy(F, reinterpret_cast<double2*>(P->specRg.ptr), P->prodLR, 1.0 / (double)P->prodLR, s);
-    }
   } else if (!long_r) {
+    HGP_TRY(P->specR.ensure((size_t)nR * (sym ? sizeof(T) : sizeof(C2<T>))));
     // the R filter is real: real row-pair transform of the last axis, compact columns only after
     embed_R_real(sv, reinterpret_cast<double*>(g1), gd, sym ? 1 : 0, s);
     HGP_TRY(fwd_grid_real_f64(P, P->LR, P->tw64R, reinterpret_cast<const double*>(g1), g2, SR));
@@ -875,15 +960,13 @@ int set_column_t(hgp_plan* P, const void* column, double jitter, double clamp_mi
       extract_t<T>(g2, P->specR.ptr, nullptr, P->LR[0], d == 3 ? P->LR[1] : 1, LRl / 2, SR, 1,
                    1.0 / (double)P->prodLR, s);
   } else {
-    // an axis of L_R > 16384 points: the full complex grid through fft_lines_f64's radix-2 step
+    // an axis of L_R > 16384 points (fp32 passes of 16384-point halves): the full complex grid
+    // through fft_lines_f64's radix-2 step
+    HGP_TRY(P->specR.ensure((size_t)nR * sizeof(C2<T>)));
     embed_R(sv, g1, gd, s);
     HGP_TRY(fwd_grid_f64(P, P->LR, P->tw64R, g1, g2, &F));
     extract_t<T>(F, P->specR.ptr, nullptr, P->LR[0], d == 3 ? P->LR[1] : 1, LRl / 2, LRl, 0,
                  1.0 / (double)P->prodLR, s);
-    if (P->grid_r) {
-      HGP_TRY(P->specRg.ensure((size_t)P->prodLR * sizeof(double2)));
-      scale_copy(F, reinterpret_cast<double2*>(P->specRg.ptr), P->prodLR, 1.0 / (double)P->prodLR, s);
-    }
   }
   HIP_TRY(hipGetLastError());
   P->have_spec = true;
@@ -922,8 +1005,9 @@ int slab_dot_parts(hgp_plan* P, PassDesc& D, const void* dotv, int64_t nrhs, int
 template <typename T>
 int slab_pass_t(hgp_plan* P, int op, int stage, const void* in, void* out, int64_t nrhs, int64_t nrows, int64_t g0,
                 int64_t ng, const void* dotv, void* dot_out, const int* done) {
-  if (P->grid_r && (op == HGP_OP_R || op == HGP_OP_RT))
-    return fail(HGP_E_UNSUPPORTED, "grid-block sharding of R / R^T with fp64 lines of more than 16384 points");
+  if (grid_route(P, op))
+    return fail(HGP_E_UNSUPPORTED, "grid-block sharding of an operator on the full-grid route (fp64 lines of "
+                                   "more than 16384 points, or an axis of more than 8192 points)");
   const OpGeom g = op_geom(P, op);
   const int d = P->d;
   const SlabGeom sg = slab_geom(P, op);
@@ -1060,6 +1144,7 @@ bool planes3d(const hgp_plan* P) {
 }
 template <typename T>
 int rn_last(const hgp_plan* P) {
+  if (P->grid_k) return update_np(P->M);   // run_op_grid's rowdot partials
   if (P->d == 1) return 1;
   if (P->d == 2) return (int)((P->m[0] + 1) / 2);
   if (planes3d<T>(P)) return (int)(P->m[0] * ((P->m[1] + 1) / 2));
@@ -1076,6 +1161,7 @@ int spec_np(const hgp_plan* P) {
 // the fused PCG needs the row-pair kernels of the K / C^-1 rows
 template <typename T>
 bool fused_pcg(const hgp_plan* P) {
+  if (P->grid_k) return false;
   return (P->d == 2 && rowt_fits<T>((int)(P->LK[1] / 2), 1) != 0) || planes3d<T>(P);
 }
 template <typename T>
@@ -1304,24 +1390,32 @@ int hgp_plan_create(int device, int ndim, const int64_t* m, int dtype, int64_t m
     double real_pts = 1, short_pts = 1;
     int64_t Ls[3] = {1, 1, 1};
     bool ok = allow && d >= 2;
+    bool long_axis = false;
     for (int a = 0; a < d; ++a) {
       const int64_t need = 3 * P->m[a] - 3;
       Ls[a] = std::min(next_pow2(need), next_tri(need));
       real_pts *= (double)P->LR[a];
       short_pts *= (double)Ls[a];
       if (Ls[a] / 2 > 8192) ok = false;      // the fp64 set-up transforms hold L_R / 2 <= 8192
+      long_axis = long_axis || P->m[a] > 8192;
     }
     if (ok && short_pts < 0.6 * real_pts)
       for (int a = 0; a < d; ++a) P->LR[a] = Ls[a];
+    // an axis of more than 8192 points: every operator on the full fp64 grid (run_op_grid), whose
+    // radix-2 levels take any L = 2^k or 3 * 2^k -- the shortest admissible L_R on every axis
+    if (long_axis) {
+      for (int a = 0; a < d; ++a) P->LR[a] = Ls[a];
+      P->grid_k = P->grid_r = true;
+    }
   }
   if (d == 0) { delete P; return fail(HGP_E_UNSUPPORTED, "a grid with every axis of size 1 (M = 1) is not supported"); }
   for (int a = 0; a < d; ++a) {
     // L_R / 2 = 16384 (axes of 4098..8192 points): fp32 operator passes hold one such line per
     // block; fp64 lines of 16384 points exceed one CU's LDS (the set-up's fp64 transforms of
     // them take fft_lines_f64's radix-2 step)
-    if (P->LR[a] / 2 > 16384 || P->LK[a] / 2 > 8192) {
+    if (!P->grid_k && (P->LR[a] / 2 > 16384 || P->LK[a] / 2 > 8192)) {
       delete P;
-      return fail(HGP_E_UNSUPPORTED, "grid axis longer than 8192 points is not supported");
+      return fail(HGP_E_UNSUPPORTED, "internal: pass lengths of a grid axis of at most 8192 points");
     }
     // fp64 lines of L_R / 2 > 8192 points exceed one CU's LDS: R / R^T take the full-grid route
     if (dtype == HGP_F64 && P->LR[a] / 2 > 8192) P->grid_r = true;
@@ -1351,7 +1445,16 @@ int hgp_plan_create(int device, int ndim, const int64_t* m, int dtype, int64_t m
       if (!rc) rc = upload_twiddles<float>(P->twR[a], P->LR[a]);
     }
     if (!rc) rc = upload_twiddles<double>(P->tw64K[a], P->LK[a]);
-    if (!rc && P->LR[a] / 2 > 8192) rc = upload_twiddles<double>(P->tw64Rh[a], P->LR[a] / 2);
+    // W_{L/2}, W_{L/4}, ... for the radix-2 levels of lines longer than one fp64 pass
+    for (int w = 0; w < 2 && !rc; ++w) {
+      int64_t Lc = w == 0 ? P->LK[a] : P->LR[a];
+      DevBuf* lev = w == 0 ? P->tw64Kl[a] : P->tw64Rl[a];
+      for (int j = 0; Lc / 2 > 8192 && !rc; ++j) {
+        if (j >= hgp_plan::NLEV) { rc = fail(HGP_E_UNSUPPORTED, "grid axis too long for the fp64 radix-2 levels"); break; }
+        Lc /= 2;
+        rc = upload_twiddles<double>(lev[j], Lc);
+      }
+    }
     if (!rc) rc = upload_twiddles<double>(P->tw64R[a], P->LR[a]);
     if (!rc) rc = make_bluestein(P, a);
   }
@@ -1939,7 +2042,8 @@ int hgp_plan_mem(const hgp_plan* plan, int64_t* scratch_bytes, int64_t* table_by
     for (int a = 0; a < 3; ++a)
       b += (int64_t)(plan->twK[a].bytes + plan->twR[a].bytes + plan->tw64K[a].bytes + plan->tw64R[a].bytes +
                      plan->bsPre[a].bytes + plan->bsPost[a].bytes + plan->bsFilt[a].bytes);
-    b += (int64_t)(plan->specK.bytes + plan->specI.bytes + plan->specR.bytes + plan->specRg.bytes + plan->Dm3.bytes);
+    b += (int64_t)(plan->specK.bytes + plan->specI.bytes + plan->specR.bytes + plan->specRg.bytes + plan->specKg.bytes +
+                   plan->Dm3.bytes);
     *table_bytes = b;
   }
   return 0;

@@ -289,9 +289,10 @@ __global__ void k_grid_embed(const T* __restrict__ x, LGeo G, int64_t prodL, dou
   z[f] = make_double2(in ? (double)x[ix] : 0.0, 0.0);
 }
 
-// out[f] (natural order) = conj(F[pos(f)] S'[pos(f)]), S' = S or conj(S)
+// out[f] (natural order) = conj(F[pos(f)] S'[pos(f)]), S' = S (mode 0), conj(S) (1), Re S (2: the
+// K spectrum of a packed K + i C^-1 transform) or Im S (3: the C^-1 spectrum)
 __global__ void k_grid_mul_unperm(const double2* __restrict__ F, const double2* __restrict__ S, LGeo G,
-                                  int64_t prodL, int conj_spec, double2* __restrict__ out) {
+                                  int64_t prodL, int mode, double2* __restrict__ out) {
   const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (f >= prodL) return;
   int c[3];
@@ -300,7 +301,9 @@ __global__ void k_grid_mul_unperm(const double2* __restrict__ F, const double2* 
   for (int a = 0; a < G.d; ++a) p = p * G.L[a] + pos_of(c[a], G.L[a]);
   const double2 a = F[p];
   double2 w = S[p];
-  if (conj_spec) w.y = -w.y;
+  if (mode == 1) w.y = -w.y;
+  else if (mode == 2) w.y = 0.0;
+  else if (mode == 3) w = make_double2(w.y, 0.0);
   out[f] = make_double2(a.x * w.x - a.y * w.y, -(a.x * w.y + a.y * w.x));
 }
 
@@ -320,6 +323,41 @@ __global__ void k_grid_crop(const double2* __restrict__ Z, LGeo G, int64_t outM,
 __global__ void k_scale_copy(const double2* __restrict__ a, double2* __restrict__ b, int64_t n, double sc) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) b[i] = make_double2(a[i].x * sc, a[i].y * sc);
+}
+
+// Line-batch helpers of the long-axis DCT (hgp_api.hip dct_axis: lines of L/2 > 8192 fp64 points
+// go through fft_lines_f64's radix-2 levels instead of one CONVC pass).  Lines [O][.][I]: the
+// position index at stride I, the I inner lines adjacent.
+// E[o][j][i] = c[o][j][i] for j < m, 0 for m <= j < L
+__global__ void k_line_embed(const double2* __restrict__ c, double2* __restrict__ E, int64_t O, int64_t m, int64_t I,
+                             int64_t L) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= O * L * I) return;
+  const int64_t i = t % I, rest = t / I;
+  const int64_t j = rest % L, o = rest / L;
+  E[t] = j < m ? c[(o * m + j) * I + i] : make_double2(0.0, 0.0);
+}
+// Z[o][f][i] (natural order f) = conj(X[o][pos(f)][i] f[pos(f)]): the filter product of the pass-order
+// transform X, un-permuted and conjugated for the inverse as conj(FFT(conj .))
+__global__ void k_line_mul_unperm_conj(const double2* __restrict__ X, const double2* __restrict__ flt,
+                                       double2* __restrict__ Z, int64_t O, int64_t L, int64_t I) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= O * L * I) return;
+  const int64_t i = t % I, rest = t / I;
+  const int64_t f = rest % L, o = rest / L;
+  const int64_t p = pos_of((int)f, (int)L);
+  const double2 x = X[(o * L + p) * I + i], w = flt[p];
+  Z[t] = make_double2(x.x * w.x - x.y * w.y, -(x.x * w.y + x.y * w.x));
+}
+// c[o][j][i] = conj(Y[o][pos(j)][i]) for j < m: IFFT(Z) = conj(FFT(conj Z)) (the 1/L is in the filter)
+__global__ void k_line_unperm_conj(const double2* __restrict__ Y, double2* __restrict__ c, int64_t O, int64_t L,
+                                   int64_t I, int64_t m) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= O * m * I) return;
+  const int64_t i = t % I, rest = t / I;
+  const int64_t j = rest % m, o = rest / m;
+  const double2 y = Y[(o * L + pos_of((int)j, (int)L)) * I + i];
+  c[t] = make_double2(y.x, -y.y);
 }
 
 LGeo make_lgeo(const GridDims& g) {
@@ -391,15 +429,26 @@ void grid_embed(int dtype, const void* x, const GridDims& gd, int64_t prodL, dou
   else k_grid_embed<float><<<nblk(prodL, 256), 256, 0, s>>>((const float*)x, G, prodL, z);
 }
 
-void grid_mul_unperm(const double2* F, const double2* S, const GridDims& gd, int64_t prodL, int conj_spec,
+void grid_mul_unperm(const double2* F, const double2* S, const GridDims& gd, int64_t prodL, int mode,
                      double2* out, hipStream_t s) {
-  k_grid_mul_unperm<<<nblk(prodL, 256), 256, 0, s>>>(F, S, make_lgeo(gd), prodL, conj_spec, out);
+  k_grid_mul_unperm<<<nblk(prodL, 256), 256, 0, s>>>(F, S, make_lgeo(gd), prodL, mode, out);
 }
 
 void grid_crop(int dtype, const double2* Z, const GridDims& gd, int64_t outM, void* y, hipStream_t s) {
   const LGeo G = make_lgeo(gd);
   if (dtype == 1) k_grid_crop<double><<<nblk(outM, 256), 256, 0, s>>>(Z, G, outM, (double*)y);
   else k_grid_crop<float><<<nblk(outM, 256), 256, 0, s>>>(Z, G, outM, (float*)y);
+}
+
+void line_embed(const double2* c, double2* E, int64_t O, int64_t m, int64_t I, int64_t L, hipStream_t s) {
+  k_line_embed<<<nblk(O * L * I, 256), 256, 0, s>>>(c, E, O, m, I, L);
+}
+void line_mul_unperm_conj(const double2* X, const double2* f, double2* Z, int64_t O, int64_t L, int64_t I,
+                          hipStream_t s) {
+  k_line_mul_unperm_conj<<<nblk(O * L * I, 256), 256, 0, s>>>(X, f, Z, O, L, I);
+}
+void line_unperm_conj(const double2* Y, double2* c, int64_t O, int64_t L, int64_t I, int64_t m, hipStream_t s) {
+  k_line_unperm_conj<<<nblk(O * m * I, 256), 256, 0, s>>>(Y, c, O, L, I, m);
 }
 
 void scale_copy(const double2* a, double2* b, int64_t n, double sc, hipStream_t s) {

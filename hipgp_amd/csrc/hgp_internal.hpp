@@ -104,6 +104,11 @@ void grid_mul_unperm(const double2* F, const double2* S, const GridDims& gd, int
                      double2* out, hipStream_t s);
 void grid_crop(int dtype, const double2* Z, const GridDims& gd, int64_t outM, void* y, hipStream_t s);
 void scale_copy(const double2* a, double2* b, int64_t n, double sc, hipStream_t s);
+// long-axis DCT line batches (hgp_grad.hip)
+void line_embed(const double2* c, double2* E, int64_t O, int64_t m, int64_t I, int64_t L, hipStream_t s);
+void line_mul_unperm_conj(const double2* X, const double2* f, double2* Z, int64_t O, int64_t L, int64_t I,
+                          hipStream_t s);
+void line_unperm_conj(const double2* Y, double2* c, int64_t O, int64_t L, int64_t I, int64_t m, hipStream_t s);
 void gather_n(const double2* F, const GridDims& gd, int h_periodic, int64_t Mp, double invL, double* X, hipStream_t s);
 void gather_flat(int dtype, const double2* F, const GridDims& gd, int64_t M, double invL, void* out, hipStream_t s);
 // CG

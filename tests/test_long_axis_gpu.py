@@ -7,7 +7,15 @@ k_r2_combine).  fp64 plans run K / C^-1 lines of up to 8192 points per half (one
 and R / R^T either as passes (L_R / 2 <= 8192: axes up to 5462 points with the 3 * 2^k or
 power-of-two L_R <= 16384) or, beyond that, on the full fp64 L_R grid (run_op_grid).  Here the
 operators and PCG of 1-D / 2-D / 3-D grids with such an axis (any position) are checked against
-the fp64 oracle of the same column, in both dtypes; axes beyond 8192 points are refused."""
+the fp64 oracle of the same column, in both dtypes.
+
+Round 4: axes of MORE than 8192 points (the passes hold lines of at most 16384 fp32 / 8192 fp64
+points) run every operator on the full fp64 grid (run_op_grid): the set-up's DCT-I (Bluestein),
+the L_K / L_R grid transforms and the operators go through fft_lines_f64's radix-2 levels as
+deep as the length needs (9000 points: L_K = L_R = 32768, one level; 12000: L_R = 49152, two
+levels to a 12288-point base; 20000: L_K = L_R = 65536, two levels), fp32 plans with fp32 in /
+out.  The PCG runs the unfused iteration (dots by row-chunk partials).  `LONG_CASES` pin them
+against the fp64 oracle like the cases above."""
 import numpy as np
 import pytest
 import torch
@@ -19,6 +27,9 @@ DEV = "cuda"
 
 CASES = {"1d_5000": (5000,), "2d_4200x12": (4200, 12), "2d_10x4500": (10, 4500),
          "3d_4100x5x4": (4100, 5, 4), "3d_4x4100x3": (4, 4100, 3), "3d_3x5x4300": (3, 5, 4300)}
+# axes beyond 8192 points: the full-grid route for every operator
+LONG_CASES = {"1d_9000": (9000,), "1d_20000": (20000,), "2d_10000x6": (10000, 6), "2d_5x12000": (5, 12000),
+              "3d_3x9000x4": (3, 9000, 4)}
 
 
 def _column(dims):
@@ -103,12 +114,60 @@ def test_long_axis_ops_and_pcg_fp64(case):
         assert mem["scratch"] >= 2 * nLR * 16 and mem["tables"] >= nLR * 16, (mem, nLR)
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.float64], ids=["f32", "f64"])
+@pytest.mark.parametrize("case", sorted(LONG_CASES))
+def test_beyond_8192_points(case, dt):
+    from hipgp_amd import _lib
+    from hipgp_amd.plan import ToeplitzPlan
+    dims = LONG_CASES[case]
+    col = _column(dims)
+    O = zo.ToeplitzOracle(col, dims)
+    P = ToeplitzPlan(dims, dt, DEV)
+    P.set_column(torch.tensor(col, device=DEV, dtype=dt))
+    rs = np.random.RandomState(6)
+    v = rs.randn(2, O.M)
+    w = rs.randn(2, O.Mp)
+    tol_op = 2e-5 if dt == torch.float32 else 1e-10
+    for name, op, x, ref in (("K", _lib.OP_K, v, O.matmul_K(v)), ("Cinv", _lib.OP_CINV, v, O.matmul_Cinv(v)),
+                             ("RT", _lib.OP_RT, v, O.matmul_RT(v)), ("R", _lib.OP_R, w, O.matmul_R(w))):
+        got = P.apply(op, torch.tensor(x, device=DEV, dtype=dt)).double().cpu().numpy()
+        assert got.shape == ref.shape, name
+        err = float(np.abs(got - ref).max() / np.abs(ref).max())
+        assert err < tol_op, (name, err)
+    # the spectrum served to ToeplitzTensor.D (n-grid) from the long-axis DCT set-up
+    D = P.spectrum(_lib.SPEC_D).double().cpu().numpy().reshape(-1)
+    assert float(np.abs(D - O.D.reshape(-1)).max() / np.abs(O.D).max()) < (1e-6 if dt == torch.float32 else 1e-12)
+    b = rs.randn(2, O.M)
+    x_ref = O.solve(b, do_precond=True, maxiter=10, tol=1e-30)
+    x, it = P.pcg(torch.tensor(b, device=DEV, dtype=dt), 10, 1e-30, precond=True, return_iters=True)
+    err = float(np.linalg.norm(x.double().cpu().numpy() - x_ref) / np.linalg.norm(x_ref))
+    calls = []
+    O.solve(b, do_precond=True, maxiter=10, tol=1e-30, callback=lambda n, xx: calls.append(n))
+    rr = [float(np.linalg.norm(O.matmul_K(x.double().cpu().numpy())[j] - b[j])) for j in range(2)]
+    print(case, dt, "iterations", it, "oracle callbacks", len(calls), "err", err, "true residual", rr)
+    assert err < (1e-4 if dt == torch.float32 else 1e-9), err
+    if dt == torch.float64:
+        # the recursive r.r falls below tol^2 = 1e-60 after 8 iterations here, in the oracle too
+        # (fp32's cannot underflow that far: 10 iterations)
+        assert it == min(10, len(calls) + 1)
+    # the break rule on this route (unfused iteration): the iterate of a maxiter stop
+    xb, itb = P.pcg(torch.tensor(b, device=DEV, dtype=dt), 200, float(np.linalg.norm(b[0])) * 1e-3, precond=True,
+                    return_iters=True)
+    xs = P.pcg(torch.tensor(b, device=DEV, dtype=dt), itb, 1e-30, precond=True)
+    assert itb < 200 and torch.equal(xb, xs)
+
+
 def test_long_axis_refusals():
     from hipgp_amd import _lib
     from hipgp_amd.plan import ToeplitzPlan
-    for dt in (torch.float32, torch.float64):
-        with pytest.raises(_lib.HipgpError, match="longer than 8192"):
-            ToeplitzPlan((8193,), dt, DEV)
-        with pytest.raises(_lib.HipgpError, match="longer than 8192"):
-            ToeplitzPlan((3, 8193), dt, DEV)
-    ToeplitzPlan((8192, 3), torch.float64, DEV)        # the limit itself is accepted in fp64 too
+    # axes of more than 8192 points are accepted (full-grid route); grid-block sharding of them is not
+    P = ToeplitzPlan((8193, 3), torch.float32, DEV)
+    col = _column((8193, 3))
+    P.set_column(torch.tensor(col, device=DEV, dtype=torch.float32))
+    import ctypes
+    with pytest.raises(_lib.HipgpError, match="full-grid route"):
+        E = torch.empty(1024 * 1024, dtype=torch.complex64, device=DEV)
+        x = torch.zeros(1, 8193 * 3, device=DEV)
+        _lib.check(_lib.lib().hgp_slab_pass(P._h, _lib.OP_K, _lib.SLAB_FWD, ctypes.c_void_p(x.data_ptr()),
+                                            ctypes.c_void_p(E.data_ptr()), 1, 1, 0, 0))
+    ToeplitzPlan((8192, 3), torch.float64, DEV)        # the pass limit itself
