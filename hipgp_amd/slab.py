@@ -196,6 +196,10 @@ class SlabToeplitz:
             self._buf[key] = b
         return b
 
+    def release(self):
+        """Drop the cached exchange / all-to-all buffers (they are re-allocated on the next apply)."""
+        self._buf.clear()
+
     def apply(self, op, x, out=None, dotv=None, dot_out=None, done=None):
         """op (libhipgp OP_*) on this rank's slab x (nrhs, local in-size) -> local out slab
         (written into `out` when given).  dotv / dot_out: also this rank's per-RHS dots

@@ -134,10 +134,12 @@ def test_dqf_vs_oracle(n, s, tag):
     assert rel_err(_np(got), want) < (1e-12 if tag == "f64" else 2e-6)
 
 
-@pytest.mark.parametrize("dims", [(33,), (12, 10), (6, 5, 4), (2, 7)], ids=lambda d: "x".join(map(str, d)))
+@pytest.mark.parametrize("dims", [(33,), (12, 10), (6, 5, 4), (2, 7), (9000,), (8300, 2)],
+                         ids=lambda d: "x".join(map(str, d)))
 def test_column_grad_vs_oracle(dims):
     """hgp_plan_column_grad for every operator on grids beyond the golden shapes (incl. an axis
-    of 2 points, whose embedding has no interior copy), fp64, against the oracle."""
+    of 2 points, whose embedding has no interior copy, and axes beyond 8192 points: the full-grid
+    route's radix-2 levels and long-axis DCT), fp64, against the oracle."""
     from hipgp_amd import _lib
     from hipgp_amd.plan import ToeplitzPlan
     rs = np.random.RandomState(sum(dims))
@@ -154,7 +156,8 @@ def test_column_grad_vs_oracle(dims):
         assert rel_err(_np(got), T.column_grad(name, x, g)) < 1e-9, name
 
 
-@pytest.mark.parametrize("dims", [(300,), (12, 10), (2, 9), (6, 5, 4), (3, 2, 7)], ids=lambda d: "x".join(map(str, d)))
+@pytest.mark.parametrize("dims", [(300,), (12, 10), (2, 9), (6, 5, 4), (3, 2, 7), (9000,)],
+                         ids=lambda d: "x".join(map(str, d)))
 @pytest.mark.parametrize("tag", ["f64", "f32"])
 def test_plan_dqf_vs_oracle(dims, tag):
     """hgp_plan_dqf (the flattened-index quadratic form through the grid's factorisation) against
