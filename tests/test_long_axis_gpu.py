@@ -171,3 +171,24 @@ def test_long_axis_refusals():
         _lib.check(_lib.lib().hgp_slab_pass(P._h, _lib.OP_K, _lib.SLAB_FWD, ctypes.c_void_p(x.data_ptr()),
                                             ctypes.c_void_p(E.data_ptr()), 1, 1, 0, 0))
     ToeplitzPlan((8192, 3), torch.float64, DEV)        # the pass limit itself
+
+
+def test_beyond_8192_drop_in_compute_kn():
+    """The drop-in ToeplitzTensor (`toeplitz_tensor.py:9-52`) and `compute_kn` (`hipgp.py:117-146`)
+    on a 9000 x 3 grid (full-grid route), fp64, against the oracle's compute_kn of the same column."""
+    import ziggy.kernels as zk
+    from ziggy.misc.toeplitz_tensor import ToeplitzTensor
+    dims = (9000, 3)
+    ell = 40.0 / max(dims)
+    k = zk.Matern(nu=1.5, dtype=torch.float64)
+    grids = [torch.linspace(-1, 1, m, dtype=torch.float64, device=DEV) for m in dims]
+    T = ToeplitzTensor(grids, lambda x, y: k.forward(x, y, params=(1.0, ell)), jitter_val=0.1)
+    col = T.column.detach().cpu().numpy()
+    O = zo.ToeplitzOracle(col, dims)
+    assert np.abs(col - _column(dims)).max() < 1e-12        # the same first row as the oracle's
+    Knm = np.random.RandomState(8).rand(3, O.M)
+    d0 = T.inv_matmul(torch.tensor(Knm, device=DEV), do_precond=True, maxiter=20, tol=1e-8)
+    kn = T._matmul_by_RT(d0).cpu().numpy()
+    ref = zo.compute_kn(O, Knm, maxiter_cg=20, tol=1e-8)
+    assert kn.shape == ref.shape == (3, O.Mp)
+    assert np.linalg.norm(kn - ref) / np.linalg.norm(ref) < 1e-9
