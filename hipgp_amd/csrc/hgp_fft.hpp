@@ -40,6 +40,63 @@ template <typename T> __device__ __forceinline__ C2<T> cmulc(C2<T> a, C2<T> b) {
   return mk<T>(a.x * b.x + a.y * b.y, a.y * b.x - a.x * b.y);
 }
 template <typename T> __device__ __forceinline__ C2<T> cscale(C2<T> a, T s) { return mk<T>(a.x * s, a.y * s); }
+// a + i b, a - i b
+template <typename T> __device__ __forceinline__ C2<T> caddi(C2<T> a, C2<T> b) { return mk<T>(a.x - b.y, a.y + b.x); }
+template <typename T> __device__ __forceinline__ C2<T> csubi(C2<T> a, C2<T> b) { return mk<T>(a.x + b.y, a.y - b.x); }
+// a * (cr + i ci) for compile-time constants
+template <typename T> __device__ __forceinline__ C2<T> cmulk(C2<T> a, T cr, T ci) { return cmul<T>(a, mk<T>(cr, ci)); }
+
+// fp32 complex arithmetic on the packed-f32 VALU (v_pk_add/mul/fma_f32: both components in one
+// 64-bit register pair, one instruction where the scalar forms take two; the f32 VALU peak is
+// the packed rate).  The backend folds lane selects into op_sel but not a one-lane negation, so
+// the forms that need one (complex products, +-i b) are written out.  Each component is computed
+// as fma(+-u, v, rn(w z)) -- one rounding per product, like the contracted scalar forms.
+#ifndef HGP_PK32
+#define HGP_PK32 1
+#endif
+#if HGP_PK32
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 pv(C2<float> a) { return __builtin_bit_cast(f32x2, a); }
+__device__ __forceinline__ C2<float> pc(f32x2 v) { return __builtin_bit_cast(C2<float>, v); }
+template <> __device__ __forceinline__ C2<float> cadd<float>(C2<float> a, C2<float> b) { return pc(pv(a) + pv(b)); }
+template <> __device__ __forceinline__ C2<float> csub<float>(C2<float> a, C2<float> b) { return pc(pv(a) - pv(b)); }
+template <> __device__ __forceinline__ C2<float> cscale<float>(C2<float> a, float s) {
+  return pc(pv(a) * f32x2{s, s});
+}
+// (ax bx - ay by, ax by + ay bx)
+template <> __device__ __forceinline__ C2<float> cmul<float>(C2<float> a, C2<float> b) {
+  f32x2 t, r;
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(pv(a)), "v"(pv(b)));
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[1,0,0]"
+      : "=v"(r) : "v"(pv(a)), "v"(pv(b)), "v"(t));
+  return pc(r);
+}
+// (ax bx + ay by, ay bx - ax by)
+template <> __device__ __forceinline__ C2<float> cmulc<float>(C2<float> a, C2<float> b) {
+  f32x2 t, r;
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(t) : "v"(pv(a)), "v"(pv(b)));
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_hi:[1,0,0]"
+      : "=v"(r) : "v"(pv(a)), "v"(pv(b)), "v"(t));
+  return pc(r);
+}
+template <> __device__ __forceinline__ C2<float> caddi<float>(C2<float> a, C2<float> b) {
+  f32x2 r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(pv(a)), "v"(pv(b)));
+  return pc(r);
+}
+template <> __device__ __forceinline__ C2<float> csubi<float>(C2<float> a, C2<float> b) {
+  f32x2 r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(pv(a)), "v"(pv(b)));
+  return pc(r);
+}
+// constant factor: the negated lane lives in the constant, so plain vector code folds to
+// v_pk_mul (op_sel) + v_pk_fma (op_sel) with the constants in scalar registers
+template <> __device__ __forceinline__ C2<float> cmulk<float>(C2<float> a, float cr, float ci) {
+  const f32x2 x = pv(a);
+  const f32x2 t = __builtin_shufflevector(x, x, 0, 0) * f32x2{cr, ci};
+  return pc(__builtin_elementwise_fma(__builtin_shufflevector(x, x, 1, 1), f32x2{-ci, cr}, t));
+}
+#endif
 
 
 // Two real rows packed as Z = a + i b, transformed: their spectra from Z at k and Zp = Z at -k,
@@ -47,13 +104,23 @@ template <typename T> __device__ __forceinline__ C2<T> cscale(C2<T> a, T s) { re
 template <typename T>
 __device__ __forceinline__ void herm_split(C2<T> z, C2<T> zp, C2<T>& A, C2<T>& B) {
   const T hf = (T)0.5;
+#if HGP_PK32
+  if constexpr (std::is_same<T, float>::value) {
+    f32x2 s, d;   // s = z + conj(zp); d = (z.y + zp.y, zp.x - z.x)
+    asm("v_pk_add_f32 %0, %1, %2 neg_hi:[0,1]" : "=v"(s) : "v"(pv(z)), "v"(pv(zp)));
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[0,0] neg_hi:[1,0]" : "=v"(d) : "v"(pv(z)), "v"(pv(zp)));
+    A = pc(s * f32x2{hf, hf});
+    B = pc(d * f32x2{hf, hf});
+    return;
+  }
+#endif
   A = mk<T>(hf * (z.x + zp.x), hf * (z.y - zp.y));
   B = mk<T>(hf * (z.y + zp.y), -hf * (z.x - zp.x));
 }
 // the inverse: Z = A + i B
 template <typename T>
 __device__ __forceinline__ C2<T> herm_join(C2<T> A, C2<T> B) {
-  return mk<T>(A.x - B.y, A.y + B.x);
+  return caddi<T>(A, B);
 }
 
 // Raw buffer access (gfx9 resource word 3 = 0x00020000, stride 0): a wave-uniform base in
@@ -156,18 +223,18 @@ __device__ __forceinline__ C2<T> rot16(C2<T> v, int Q) {
     case 4: return mk<T>(v.y, -v.x);
     case 8: return mk<T>(-v.x, -v.y);
     case 12: return mk<T>(-v.y, v.x);
-    case 2: return mk<T>(c8 * (v.x + v.y), c8 * (v.y - v.x));
-    case 6: return mk<T>(c8 * (v.y - v.x), -c8 * (v.x + v.y));
-    case 10: return mk<T>(-c8 * (v.x + v.y), c8 * (v.x - v.y));
-    case 14: return mk<T>(c8 * (v.x - v.y), c8 * (v.x + v.y));
-    case 1: return cmul<T>(v, mk<T>(c1, -s1));
-    case 3: return cmul<T>(v, mk<T>(s1, -c1));
-    case 5: return cmul<T>(v, mk<T>(-s1, -c1));
-    case 7: return cmul<T>(v, mk<T>(-c1, -s1));
-    case 9: return cmul<T>(v, mk<T>(-c1, s1));
-    case 11: return cmul<T>(v, mk<T>(-s1, c1));
-    case 13: return cmul<T>(v, mk<T>(s1, c1));
-    default: return cmul<T>(v, mk<T>(c1, s1));   // 15
+    case 2: return cscale<T>(csubi<T>(v, v), c8);      // (c8 (x + y), c8 (y - x))
+    case 6: return cscale<T>(caddi<T>(v, v), -c8);     // (c8 (y - x), -c8 (x + y))
+    case 10: return cscale<T>(csubi<T>(v, v), -c8);    // (-c8 (x + y), c8 (x - y))
+    case 14: return cscale<T>(caddi<T>(v, v), c8);     // (c8 (x - y), c8 (x + y))
+    case 1: return cmulk<T>(v, c1, -s1);
+    case 3: return cmulk<T>(v, s1, -c1);
+    case 5: return cmulk<T>(v, -s1, -c1);
+    case 7: return cmulk<T>(v, -c1, -s1);
+    case 9: return cmulk<T>(v, -c1, s1);
+    case 11: return cmulk<T>(v, -s1, c1);
+    case 13: return cmulk<T>(v, s1, c1);
+    default: return cmulk<T>(v, c1, s1);   // 15
   }
 }
 
@@ -182,14 +249,14 @@ __device__ __forceinline__ C2<T> rot12(C2<T> v, int Q) {
     case 3: return mk<T>(v.y, -v.x);
     case 6: return mk<T>(-v.x, -v.y);
     case 9: return mk<T>(-v.y, v.x);
-    case 1: return cmul<T>(v, mk<T>(c, -h));
-    case 2: return cmul<T>(v, mk<T>(h, -c));
-    case 4: return cmul<T>(v, mk<T>(-h, -c));
-    case 5: return cmul<T>(v, mk<T>(-c, -h));
-    case 7: return cmul<T>(v, mk<T>(-c, h));
-    case 8: return cmul<T>(v, mk<T>(-h, c));
-    case 10: return cmul<T>(v, mk<T>(h, c));
-    default: return cmul<T>(v, mk<T>(c, h));    // 11
+    case 1: return cmulk<T>(v, c, -h);
+    case 2: return cmulk<T>(v, h, -c);
+    case 4: return cmulk<T>(v, -h, -c);
+    case 5: return cmulk<T>(v, -c, -h);
+    case 7: return cmulk<T>(v, -c, h);
+    case 8: return cmulk<T>(v, -h, c);
+    case 10: return cmulk<T>(v, h, c);
+    default: return cmulk<T>(v, c, h);    // 11
   }
 }
 
@@ -202,12 +269,12 @@ __device__ __forceinline__ void dft(C2<T>* v) {
     // y0 = a + s, y1,2 = a - s/2 -+ i DIR' (sqrt(3)/2) d with s = b + c, d = b - c
     const T c = (T)0.86602540378443864676;
     const C2<T> a = v[0], s = cadd<T>(v[1], v[2]), d = csub<T>(v[1], v[2]);
-    const C2<T> m = mk<T>(a.x - (T)0.5 * s.x, a.y - (T)0.5 * s.y);
-    // forward: -i c d = (c d.y, -c d.x); inverse: +i c d
-    const C2<T> rd = (DIR < 0) ? mk<T>(c * d.y, -c * d.x) : mk<T>(-c * d.y, c * d.x);
+    const C2<T> m = csub<T>(a, cscale<T>(s, (T)0.5));
+    // forward: m -+ i c d; inverse: m +- i c d
+    const C2<T> cd = cscale<T>(d, c);
     v[0] = cadd<T>(a, s);
-    v[1] = cadd<T>(m, rd);
-    v[2] = csub<T>(m, rd);
+    v[1] = (DIR < 0) ? csubi<T>(m, cd) : caddi<T>(m, cd);
+    v[2] = (DIR < 0) ? caddi<T>(m, cd) : csubi<T>(m, cd);
   } else if constexpr (R % 3 == 0) {
     // R = R1 x 3 (R1 = 4 or 2): R1-point DFTs of stride 3, twiddles exp(-+2 pi i n2 k1 / R), 3-point DFTs
     constexpr int R1 = R / 3, R2 = 3;
@@ -237,12 +304,11 @@ __device__ __forceinline__ void dft(C2<T>* v) {
   } else if constexpr (R == 4) {
     C2<T> s02 = cadd<T>(v[0], v[2]), d02 = csub<T>(v[0], v[2]);
     C2<T> s13 = cadd<T>(v[1], v[3]), d13 = csub<T>(v[1], v[3]);
-    // forward: d13 * (-i) = (y, -x); inverse: d13 * (+i) = (-y, x)
-    C2<T> rd = (DIR < 0) ? mk<T>(d13.y, -d13.x) : mk<T>(-d13.y, d13.x);
+    // forward: d02 -+ i d13; inverse: d02 +- i d13
     v[0] = cadd<T>(s02, s13);
     v[2] = csub<T>(s02, s13);
-    v[1] = cadd<T>(d02, rd);
-    v[3] = csub<T>(d02, rd);
+    v[1] = (DIR < 0) ? csubi<T>(d02, d13) : caddi<T>(d02, d13);
+    v[3] = (DIR < 0) ? caddi<T>(d02, d13) : csubi<T>(d02, d13);
   } else {
     constexpr int R1 = 4, R2 = R / 4;
     C2<T> y[R];

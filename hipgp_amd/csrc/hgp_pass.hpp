@@ -107,6 +107,10 @@
 #ifndef HGP_MINW_CONTIG_4096
 #define HGP_MINW_CONTIG_4096 3
 #endif
+// mixed-radix lines of >= 4 waves (the R / R^T 6144- and 12288-point axis-0 convolutions)
+#ifndef HGP_MINW_CONTIG_TRI
+#define HGP_MINW_CONTIG_TRI HGP_MINW_CONTIG_LONG
+#endif
 
 namespace hgp {
 
@@ -211,7 +215,8 @@ template <typename T, int H, int LAY> struct PassCfg {
   static constexpr int MINW_LDS = (BLOCKS_BY_LDS * WAVES_PER_BLOCK) / 4;
   static constexpr int MINW_AUTO = MINW_LDS < 1 ? 1 : (MINW_LDS > 4 ? 4 : MINW_LDS);
   // (3 waves per SIMD only for lines of 4 waves: 3 whole blocks per CU)
-  static constexpr int MINW_CL = (H >= 4096 && TT == 256) ? HGP_MINW_CONTIG_4096
+  static constexpr int MINW_CL = (!is_pow2(H) && TT >= 256) ? HGP_MINW_CONTIG_TRI
+                                 : (H >= 4096 && TT == 256) ? HGP_MINW_CONTIG_4096
                                  : H >= 2048 ? HGP_MINW_CONTIG_LONG : H <= 512 ? HGP_MINW_CONTIG_SHORT : HGP_MINW_CONTIG;
   // a block's waves must fit the SIMDs' share at once: >= WAVES_PER_BLOCK / 4 waves per SIMD
   static constexpr int MINW_BLK = (WAVES_PER_BLOCK + 3) / 4;

@@ -6,7 +6,8 @@ fp32 within FFT rounding); the slab PCG runs the conj_grad2 recurrence with all-
 dots, the single-rank plan the fused device PCG.  World size 3 checks the HIP
 rank-block addressing of HGP_SLAB_CONV_A2A with remainder splits.  The slab PCG allocates
 nothing per iteration (torch.cuda.memory_stats: the same number of device allocations for 3
-and 9 iterations) and its break rule gives the single-rank plan's iteration count."""
+and 9 iterations) and its break rule gives the single-rank plan's iteration count (fp64; fp32 within a
+few iterations of it, the solution held to the single-rank plan's true residual)."""
 import os
 
 import numpy as np
@@ -109,7 +110,22 @@ def test_slab_ranks_same_device(case, ws):
         a3, a9 = out[r]["alloc_counts"]
         assert a3 == a9, (r, a3, a9)
     xb, itb = P.pcg(v, 200, out[0]["brk_tol"], precond=True, return_iters=True)
-    assert all(out[r]["brk_it"] == itb for r in range(ws)), ([out[r]["brk_it"] for r in range(ws)], itb)
     assert itb < 200
-    err = float(np.linalg.norm(gat("brk") - xb.double().cpu().numpy()) / np.linalg.norm(xb.double().cpu().numpy()))
-    assert err < tol_pcg, err
+    # every rank stops at the same iteration (the all-rank break)
+    assert len({out[r]["brk_it"] for r in range(ws)}) == 1, [out[r]["brk_it"] for r in range(ws)]
+    if dt == torch.float64:
+        # the slab recurrence (all-reduced dots) and the fused device PCG agree to 1e-11: same count
+        assert out[0]["brk_it"] == itb, (out[0]["brk_it"], itb)
+        err = float(np.linalg.norm(gat("brk") - xb.double().cpu().numpy()) / np.linalg.norm(xb.double().cpu().numpy()))
+        assert err < tol_pcg, err
+    else:
+        # fp32 at C2 size needs ~85 iterations for tol = 1e-2 |v|: the two recurrences' rounding
+        # (dot order, FFT arithmetic) moves the stopping iteration by a few, so the count is held to
+        # a band and the solution by its true residual against the single-rank plan's
+        assert abs(out[0]["brk_it"] - itb) <= max(3, itb // 20), (out[0]["brk_it"], itb)
+        vt = v.double()
+        Pd = ToeplitzPlan(dims, torch.float64, "cuda")
+        Pd.set_column(torch.tensor(_column(dims), device="cuda", dtype=torch.float64))
+        res = lambda x: float(torch.linalg.norm(vt[0] - Pd.apply(_lib.OP_K, torch.as_tensor(x, device="cuda").double())[0]))
+        r_slab, r_single = res(gat("brk")), res(xb.double())
+        assert r_slab <= 1.5 * max(r_single, out[0]["brk_tol"]), (r_slab, r_single, out[0]["brk_tol"])
