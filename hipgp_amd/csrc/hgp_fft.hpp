@@ -63,7 +63,13 @@ template <> __device__ __forceinline__ C2<float> csub<float>(C2<float> a, C2<flo
 template <> __device__ __forceinline__ C2<float> cscale<float>(C2<float> a, float s) {
   return pc(pv(a) * f32x2{s, s});
 }
-// (ax bx - ay by, ax by + ay bx)
+// One asm block per product: the hazard recognizer pads every VALU read of an inline-asm result
+// that follows it directly with an s_nop (it cannot see the asm writes no dst_sel), so a split
+// mul / fma pair cost one s_nop per product (140 in the C2 column kernel).
+#ifndef HGP_PK_SPLIT
+#define HGP_PK_SPLIT 0    // 1: the product as two asm statements (A/B knob)
+#endif
+#if HGP_PK_SPLIT
 template <> __device__ __forceinline__ C2<float> cmul<float>(C2<float> a, C2<float> b) {
   f32x2 t, r;
   asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(pv(a)), "v"(pv(b)));
@@ -71,7 +77,6 @@ template <> __device__ __forceinline__ C2<float> cmul<float>(C2<float> a, C2<flo
       : "=v"(r) : "v"(pv(a)), "v"(pv(b)), "v"(t));
   return pc(r);
 }
-// (ax bx + ay by, ay bx - ax by)
 template <> __device__ __forceinline__ C2<float> cmulc<float>(C2<float> a, C2<float> b) {
   f32x2 t, r;
   asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(t) : "v"(pv(a)), "v"(pv(b)));
@@ -79,6 +84,24 @@ template <> __device__ __forceinline__ C2<float> cmulc<float>(C2<float> a, C2<fl
       : "=v"(r) : "v"(pv(a)), "v"(pv(b)), "v"(t));
   return pc(r);
 }
+#else
+// (ax bx - ay by, ax by + ay bx)
+template <> __device__ __forceinline__ C2<float> cmul<float>(C2<float> a, C2<float> b) {
+  f32x2 t, r;
+  asm("v_pk_mul_f32 %1, %2, %3 op_sel_hi:[0,1]\n\t"
+      "v_pk_fma_f32 %0, %2, %3, %1 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[1,0,0]"
+      : "=v"(r), "=&v"(t) : "v"(pv(a)), "v"(pv(b)));
+  return pc(r);
+}
+// (ax bx + ay by, ay bx - ax by)
+template <> __device__ __forceinline__ C2<float> cmulc<float>(C2<float> a, C2<float> b) {
+  f32x2 t, r;
+  asm("v_pk_mul_f32 %1, %2, %3 op_sel_hi:[1,0]\n\t"
+      "v_pk_fma_f32 %0, %2, %3, %1 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_hi:[1,0,0]"
+      : "=v"(r), "=&v"(t) : "v"(pv(a)), "v"(pv(b)));
+  return pc(r);
+}
+#endif
 template <> __device__ __forceinline__ C2<float> caddi<float>(C2<float> a, C2<float> b) {
   f32x2 r;
   asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(pv(a)), "v"(pv(b)));
