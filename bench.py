@@ -29,6 +29,11 @@ CAN fail to scale:
                   (hipgp_amd.dist.sharded_elbo_and_grad: fused Kuf + compute_kn + statistics and
                   the all-reduce of the 2 M' natural-gradient sums, hipgp.py:234-266), and that
                   all-reduce (33.5 MB at C2) timed alone
+  strong_c4     = config 4's own multi-GPU workload (BASELINE configs[3]):
+                  compute_kn for its fixed global batch of 200 RHS on the 4096^2 grid
+                  (Matern-3/2, sig2 0.1, ell 0.1, jitter 1e-3), split 200/N per rank -- 25 per GPU
+                  at N = 8 -- with the same all-RHS break; one timed repetition (~2 s at N = 1,
+                  ~130 GB of HBM there); an error is recorded in the line instead of failing it
 """
 import argparse
 import json
@@ -65,6 +70,7 @@ def parse():
                     help="only the timed K matvec steps (for rocprofv3 --pmc passes)")
     ap.add_argument("--no-legs", action="store_true", help="skip the strong-scaling / ELBO-step legs")
     ap.add_argument("--legs-reps", type=int, default=3)
+    ap.add_argument("--no-c4-leg", action="store_true", help="skip the config-4 (200 RHS at 4096^2) strong leg")
     return ap.parse_args()
 
 
@@ -180,6 +186,58 @@ def cpu_baseline(m, B, grids_np, seed, threads=None):
                       f"{reps} repetitions = {el:.2f} s; compute_kn (PCG(20, tol 1e-8, precond) + R^T) on all "
                       f"{B} RHS = {pcg_s:.2f} s",
             "pcg_s": pcg_s, "pcg_rhs": B}
+
+
+def _timed_max(fn, reps, dist, device, backend):
+    """warm-up + median of `reps` barrier-bracketed, synchronised wall-clocks; max over ranks (ms)"""
+    import torch.distributed as tdist
+    out = []
+    fn()
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        if dist:
+            tdist.barrier()
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        if dist:
+            tdist.barrier()
+        out.append(time.perf_counter() - t0)
+    v = float(np.median(out))
+    if dist:
+        tt = torch.tensor([v], device=device if backend == "nccl" else "cpu", dtype=torch.float64)
+        tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
+        v = float(tt.item())
+    return v * 1e3
+
+
+def c4_strong_leg(args, device, dist, world, rank):
+    """Config 4 (4096^2, Matern-3/2, 200 RHS global) compute_kn split over the ranks: the
+    workload the 8-GPU configuration is quoted on (25 RHS per GPU at N = 8)."""
+    import ziggy.hipgp as hg
+    import ziggy.kernels as zk
+    from hipgp_amd import dist as hdist
+    G, m4 = 200, 4096
+    sl = hdist.rhs_shard(G, world, rank)
+    grids4 = [torch.linspace(-1, 1, m4, device=device) for _ in range(2)]
+    g = torch.Generator(device="cpu").manual_seed(2024)       # the same batch on every rank
+    x = (torch.rand(G, 2, generator=g, dtype=torch.float32) * 2 - 1).to(device)
+    out = {"what": "config 4: compute_kn (set-up + PCG(20, tol 1e-8, precond, all-RHS break over ranks) + R^T) "
+                   "for its fixed global batch of 200 RHS on the 4096^2 grid, split over the ranks",
+           "global_rhs": G, "rhs_per_rank": sl.stop - sl.start, "grid": [m4, m4], "scaling": "strong"}
+    try:
+        mod = hg.MeanFieldToeplitzGP(zk.Matern(nu=1.5, dtype=torch.float32), grids4, num_obs=100_000,
+                                     sig2_init=0.1, ell_init=0.1, learn_kernel=False, jitter_val=1e-3,
+                                     dtype=torch.float32).cuda_params(device.index)
+        Knm_local, _ = mod._make_grams(x[sl])
+        ms = _timed_max(lambda: hdist.sharded_compute_kn(mod, Knm_local, maxiter_cg=20, tol=1e-8, exact_break=dist),
+                        1, dist, device, args.backend)
+        out.update({"ms": ms, "rhs_per_s": G / (ms * 1e-3)})
+        del mod, Knm_local
+    except RuntimeError as e:      # e.g. out of device memory on a smaller card: recorded, not fatal
+        out["error"] = str(e).splitlines()[0][:200]
+    torch.cuda.empty_cache()
+    return out
 
 
 def multi_gpu_legs(args, m, grids, kf, device, dist, world, rank, reps):
@@ -329,6 +387,9 @@ def main():
     legs = None
     if not args.kop_only and not args.no_legs:
         legs = multi_gpu_legs(args, m, grids, kf, device, dist, world, rank, args.legs_reps)
+        torch.cuda.empty_cache()
+        if not args.no_c4_leg:
+            legs["strong_c4"] = c4_strong_leg(args, device, dist, world, rank)
 
     # ---- the metric: W warmup + K timed batched K matvec steps --------------------------------
     settle()
