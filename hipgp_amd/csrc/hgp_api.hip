@@ -871,7 +871,7 @@ int set_column_t(hgp_plan* P, const void* column, double jitter, double clamp_mi
   HGP_TRY(P->setM1.ensure(3 * M * sizeof(double)));
   HGP_TRY(P->setM2.ensure(3 * M * sizeof(double)));
   HGP_TRY(P->Dm3.ensure(3 * M * sizeof(double)));
-  HGP_TRY(P->nclamp.ensure(sizeof(unsigned long long)));
+  HGP_TRY(P->nclamp.ensure(3 * sizeof(unsigned long long)));   // count, max D, max 1/D (pack_scale)
   double* a = reinterpret_cast<double*>(P->setM1.ptr);
   double* b = reinterpret_cast<double*>(P->setM2.ptr);
   to_f64<T>(column, a, M, jitter, s);
@@ -881,7 +881,7 @@ int set_column_t(hgp_plan* P, const void* column, double jitter, double clamp_mi
     HGP_TRY(dct_axis(P, ax, a, b, 1, 1.0));
     std::swap(a, b);
   }
-  HIP_TRY(hipMemsetAsync(P->nclamp.ptr, 0, sizeof(unsigned long long), s));
+  HIP_TRY(hipMemsetAsync(P->nclamp.ptr, 0, 3 * sizeof(unsigned long long), s));
   double* D3 = reinterpret_cast<double*>(P->Dm3.ptr);
   clamp_spectrum(a, D3, M, clamp_min, reinterpret_cast<unsigned long long*>(P->nclamp.ptr), s);
   // generators: c_K = IFFT_n(D), c_inv = IFFT_n(1/D), s = IFFT_n(sqrt D) on the m-grid
@@ -907,13 +907,15 @@ int set_column_t(hgp_plan* P, const void* column, double jitter, double clamp_mi
   GridDims gd;
   gd.d = d;
   for (int ax = 0; ax < 3; ++ax) { gd.m[ax] = P->m[ax]; gd.n[ax] = P->n[ax]; gd.L[ax] = P->LK[ax]; }
-  embed_K(cK, cI, g1, gd, s);
+  // K real, C^-1 imaginary, the latter scaled to K's magnitude (pack_scale, hgp_internal.hpp)
+  const unsigned long long* pmx = reinterpret_cast<const unsigned long long*>(P->nclamp.ptr) + 1;
+  embed_K(cK, cI, g1, gd, pmx, s);
   double2* F = nullptr;
   HGP_TRY(fwd_grid_f64(P, P->LK, P->tw64K, g1, g2, &F));
   if (P->grid_k) {
     // K / C^-1 on the full grid: the packed transform itself (K real, C^-1 imaginary), / N
     HGP_TRY(P->specKg.ensure((size_t)P->prodLK * sizeof(double2)));
-    scale_copy(F, reinterpret_cast<double2*>(P->specKg.ptr), P->prodLK, 1.0 / (double)P->prodLK, s);
+    scale_copy(F, reinterpret_cast<double2*>(P->specKg.ptr), P->prodLK, 1.0 / (double)P->prodLK, s, pmx);
   }
   const int compact = d > 1 ? 1 : 0;
   const int64_t LKl = P->LK[d - 1], LRl = P->LR[d - 1];
@@ -926,10 +928,10 @@ int set_column_t(hgp_plan* P, const void* column, double jitter, double clamp_mi
     HGP_TRY(P->specI.ensure((size_t)nK * sizeof(T)));
     // d >= 2: spectra transposed to [compact column][k1][k0] for the contiguous axis-0 pass
     if (d == 1)
-      extract_pair<T>(F, P->specK.ptr, P->specI.ptr, nK, LKl, SK, compact, 1.0 / (double)P->prodLK, s);
+      extract_pair<T>(F, P->specK.ptr, P->specI.ptr, nK, LKl, SK, compact, 1.0 / (double)P->prodLK, s, 0, 0, pmx);
     else
       extract_t<T>(F, P->specK.ptr, P->specI.ptr, P->LK[0], d == 3 ? P->LK[1] : 1, LKl / 2, LKl, 0,
-                   1.0 / (double)P->prodLK, s);
+                   1.0 / (double)P->prodLK, s, pmx);
   }
   for (int ax = 0; ax < 3; ++ax) gd.L[ax] = P->LR[ax];
   bool long_r = false;

@@ -320,9 +320,10 @@ __global__ void k_grid_crop(const double2* __restrict__ Z, LGeo G, int64_t outM,
   y[j] = (T)Z[p].x;
 }
 
-__global__ void k_scale_copy(const double2* __restrict__ a, double2* __restrict__ b, int64_t n, double sc) {
+__global__ void k_scale_copy(const double2* __restrict__ a, double2* __restrict__ b, int64_t n, double sc,
+                             const unsigned long long* mx) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) b[i] = make_double2(a[i].x * sc, a[i].y * sc);
+  if (i < n) b[i] = make_double2(a[i].x * sc, a[i].y * (sc / pack_scale(mx)));
 }
 
 // Line-batch helpers of the long-axis DCT (hgp_api.hip dct_axis: lines of L/2 > 8192 fp64 points
@@ -451,8 +452,8 @@ void line_unperm_conj(const double2* Y, double2* c, int64_t O, int64_t L, int64_
   k_line_unperm_conj<<<nblk(O * m * I, 256), 256, 0, s>>>(Y, c, O, L, I, m);
 }
 
-void scale_copy(const double2* a, double2* b, int64_t n, double sc, hipStream_t s) {
-  k_scale_copy<<<nblk(n, 256), 256, 0, s>>>(a, b, n, sc);
+void scale_copy(const double2* a, double2* b, int64_t n, double sc, hipStream_t s, const unsigned long long* mx) {
+  k_scale_copy<<<nblk(n, 256), 256, 0, s>>>(a, b, n, sc, mx);
 }
 
 }  // namespace hgp

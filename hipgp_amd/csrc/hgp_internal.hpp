@@ -39,9 +39,24 @@ void chirp_pre(const double* x, const double2* pre, double2* c, int64_t total, i
 void chirp_post(const double2* c, const double2* post, double* y, int64_t total, int64_t m, int64_t I, double scale,
                 hipStream_t s);
 template <typename T> void to_f64(const void* src, double* dst, int64_t n, double add0, hipStream_t s);
+// nclamp[0] counts the clamped entries; nclamp[1] / nclamp[2] receive max D / max 1/D (finite
+// values, as the bits of positive doubles) for pack_scale
 void clamp_spectrum(const double* Draw, double* out3, int64_t M, double clamp_min, unsigned long long* nclamp,
                     hipStream_t s);
-void embed_K(const double* cK, const double* cI, double2* out, const GridDims& g, hipStream_t s);
+// The set-up transforms the K and C^-1 generators as ONE complex grid (K real, C^-1 imaginary).
+// A transform's rounding is relative to its largest value, and at the clamp 1/D reaches 1e6 where
+// D stays ~1e3: packed as they are, the K spectrum would carry C^-1-sized rounding (K matvec 400x
+// less accurate in its small modes -- what 20 clamped PCG iterations amplify).  The C^-1
+// generator is therefore packed scaled by pack_scale = 2^(ilogb max D - ilogb max 1/D) (exact)
+// and unscaled on extraction.  `mx` = nclamp + 1 (nullptr: no scaling).
+__device__ __forceinline__ double pack_scale(const unsigned long long* mx) {
+  if (mx == nullptr) return 1.0;
+  const double a = __longlong_as_double((long long)mx[0]), b = __longlong_as_double((long long)mx[1]);
+  if (!(a > 0.0) || !(b > 0.0) || !isfinite(a) || !isfinite(b)) return 1.0;
+  return ldexp(1.0, ilogb(a) - ilogb(b));
+}
+void embed_K(const double* cK, const double* cI, double2* out, const GridDims& g, const unsigned long long* mx,
+             hipStream_t s);
 void embed_R(const double* sv, double2* out, const GridDims& g, hipStream_t s);
 // sym: mirror the filter over (-n, n) on every axis (needs L >= 2n - 1): the embedded filter is
 // then even and its spectrum real (set_column_t, hgp_plan::r_real)
@@ -52,13 +67,14 @@ void r2_combine(const double2* in, double2* out, int64_t L, int64_t Rn, int64_t 
 // complex spectrum into a, else the pair (Re -> a, Im -> b)
 template <typename T>
 void extract_t(const double2* F, void* a, void* b, int64_t L0, int64_t L1, int64_t H, int64_t Ssrc, int compact_src,
-               double scale, hipStream_t s);
+               double scale, hipStream_t s, const unsigned long long* mx = nullptr);
 // the same extraction keeping the real part only (a real spectrum: Re -> a)
 template <typename T>
 void extract_t_re(const double2* F, void* a, int64_t L0, int64_t L1, int64_t H, int64_t Ssrc, int compact_src,
                   double scale, hipStream_t s);
 template <typename T> void extract_pair(const double2* F, void* a, void* b, int64_t n, int64_t L, int64_t S, int compact,
-                                        double scale, hipStream_t s, int64_t L0t = 0, int64_t L1t = 0);
+                                        double scale, hipStream_t s, int64_t L0t = 0, int64_t L1t = 0,
+                                        const unsigned long long* mx = nullptr);
 template <typename T> void extract_cplx(const double2* F, void* o, int64_t n, int64_t L, int64_t S, int compact, double scale,
                                         hipStream_t s, int64_t L0t = 0, int64_t L1t = 0);
 template <typename T> void expand_spec(const double* src, void* out, const GridDims& g, hipStream_t s);
@@ -103,7 +119,8 @@ void grid_embed(int dtype, const void* x, const GridDims& gd, int64_t prodL, dou
 void grid_mul_unperm(const double2* F, const double2* S, const GridDims& gd, int64_t prodL, int conj_spec,
                      double2* out, hipStream_t s);
 void grid_crop(int dtype, const double2* Z, const GridDims& gd, int64_t outM, void* y, hipStream_t s);
-void scale_copy(const double2* a, double2* b, int64_t n, double sc, hipStream_t s);
+void scale_copy(const double2* a, double2* b, int64_t n, double sc, hipStream_t s,
+                const unsigned long long* mx = nullptr);   // mx: the imaginary part also / pack_scale
 // long-axis DCT line batches (hgp_grad.hip)
 void line_embed(const double2* c, double2* E, int64_t O, int64_t m, int64_t I, int64_t L, hipStream_t s);
 void line_mul_unperm_conj(const double2* X, const double2* f, double2* Z, int64_t O, int64_t L, int64_t I,

@@ -92,14 +92,33 @@ template void to_f64<double>(const void*, double*, int64_t, double, hipStream_t)
 __global__ void k_clamp(const double* __restrict__ Draw, double* __restrict__ out3, int64_t M, double clamp_min,
                         unsigned long long* nclamp) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= M) return;
-  double d = Draw[i];
+  const bool in = i < M;
+  double d = in ? Draw[i] : clamp_min;
   if (!(d >= clamp_min)) {      // torch.clamp(min=) semantics: values below min (NaN stays NaN)
     if (d < clamp_min) { d = clamp_min; atomicAdd(nclamp, 1ull); }
   }
-  out3[i] = d;
-  out3[M + i] = 1.0 / d;
-  out3[2 * M + i] = sqrt(d);
+  if (in) {
+    out3[i] = d;
+    out3[M + i] = 1.0 / d;
+    out3[2 * M + i] = sqrt(d);
+  } else {
+    d = 0.0;                    // no contribution to the maxima
+  }
+  // block maxima of D and 1/D (finite values) -> one atomic per block each (pack_scale)
+  __shared__ double smx[2][256 / 64];
+  double a = (d > 0.0 && isfinite(d)) ? d : 0.0, b = (d > 0.0 && isfinite(1.0 / d)) ? 1.0 / d : 0.0;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    a = fmax(a, __shfl_xor(a, off, 64));
+    b = fmax(b, __shfl_xor(b, off, 64));
+  }
+  if ((threadIdx.x & 63) == 0) { smx[0][threadIdx.x >> 6] = a; smx[1][threadIdx.x >> 6] = b; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) { a = fmax(a, smx[0][w]); b = fmax(b, smx[1][w]); }
+    atomicMax(nclamp + 1, (unsigned long long)__double_as_longlong(a));
+    atomicMax(nclamp + 2, (unsigned long long)__double_as_longlong(b));
+  }
 }
 
 void clamp_spectrum(const double* Draw, double* out3, int64_t M, double clamp_min, unsigned long long* nclamp,
@@ -110,9 +129,10 @@ void clamp_spectrum(const double* Draw, double* out3, int64_t M, double clamp_mi
 // K-type embedding (L >= 2m-1): G[u] = c[|t|], t = u (u < m) or u - L (u > L - m); complex
 // pair (re = cK, im = cInv).
 __global__ void k_embed_K(const double* __restrict__ cK, const double* __restrict__ cI, double2* __restrict__ out,
-                          GridDims g, int64_t total) {
+                          GridDims g, int64_t total, const unsigned long long* mx) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= total) return;
+  const double sc = pack_scale(mx);
   int64_t rem = idx, src = 0, mstride = 1;
   bool ok = true;
   for (int a = g.d - 1; a >= 0; --a) {
@@ -127,7 +147,7 @@ __global__ void k_embed_K(const double* __restrict__ cK, const double* __restric
   }
   double2 v;
   v.x = ok ? cK[src] : 0.0;
-  v.y = ok ? cI[src] : 0.0;
+  v.y = ok ? cI[src] * sc : 0.0;
   out[idx] = v;
 }
 
@@ -211,10 +231,11 @@ void embed_R_real(const double* sv, double* out, const GridDims& g, int sym, hip
   hipLaunchKernelGGL(k_embed_R_real, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, sv, out, g, total, sym);
 }
 
-void embed_K(const double* cK, const double* cI, double2* out, const GridDims& g, hipStream_t s) {
+void embed_K(const double* cK, const double* cI, double2* out, const GridDims& g, const unsigned long long* mx,
+             hipStream_t s) {
   int64_t total = 1;
   for (int a = 0; a < g.d; ++a) total *= g.L[a];
-  hipLaunchKernelGGL(k_embed_K, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, cK, cI, out, g, total);
+  hipLaunchKernelGGL(k_embed_K, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, cK, cI, out, g, total, mx);
 }
 void embed_R(const double* sv, double2* out, const GridDims& g, hipStream_t s) {
   int64_t total = 1;
@@ -245,13 +266,14 @@ __device__ __forceinline__ int64_t spec_src(int64_t idx, int64_t L, int64_t S, i
 
 template <typename T>
 __global__ void k_extract_pair(const double2* __restrict__ F, T* __restrict__ a, T* __restrict__ b, int64_t n,
-                               int64_t L, int64_t S, int compact, double scale, int64_t L0t, int64_t L1t) {
+                               int64_t L, int64_t S, int compact, double scale, int64_t L0t, int64_t L1t,
+                               const unsigned long long* mx) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int64_t src = spec_src(i, L, S, compact, L0t, L1t);
   const double2 f = src >= 0 ? F[src] : make_double2(0.0, 0.0);
   a[i] = (T)(f.x * scale);
-  b[i] = (T)(f.y * scale);
+  b[i] = (T)(f.y * (scale / pack_scale(mx)));
 }
 template <typename T>
 __global__ void k_extract_cplx(const double2* __restrict__ F, C2<T>* __restrict__ o, int64_t n, int64_t L, int64_t S,
@@ -268,9 +290,9 @@ __global__ void k_extract_cplx(const double2* __restrict__ F, C2<T>* __restrict_
 // (hgp_lines.hpp); else [outer][c] with pitch S.
 template <typename T>
 void extract_pair(const double2* F, void* a, void* b, int64_t n, int64_t L, int64_t S, int compact, double scale,
-                  hipStream_t s, int64_t L0t, int64_t L1t) {
+                  hipStream_t s, int64_t L0t, int64_t L1t, const unsigned long long* mx) {
   hipLaunchKernelGGL((k_extract_pair<T>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, F, (T*)a, (T*)b, n, L, S,
-                     compact, scale, L0t, L1t);
+                     compact, scale, L0t, L1t, mx);
 }
 template <typename T>
 void extract_cplx(const double2* F, void* o, int64_t n, int64_t L, int64_t S, int compact, double scale, hipStream_t s,
@@ -285,8 +307,10 @@ void extract_cplx(const double2* F, void* o, int64_t n, int64_t L, int64_t S, in
 template <typename T, bool PAIR>
 __global__ __launch_bounds__(256) void k_extract_t(const double2* __restrict__ F, T* __restrict__ a,
                                                    T* __restrict__ b, int64_t L0, int64_t L1, int64_t NC,
-                                                   int64_t Ssrc, int compact_src, int64_t H, double scale) {
+                                                   int64_t Ssrc, int compact_src, int64_t H, double scale,
+                                                   const unsigned long long* mx) {
   __shared__ double2 tile[32][33];
+  const double scale_b = scale / pack_scale(mx);
   const int64_t k1 = blockIdx.z;
   const int64_t c0 = (int64_t)blockIdx.x * 32, k00 = (int64_t)blockIdx.y * 32;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
@@ -307,7 +331,7 @@ __global__ __launch_bounds__(256) void k_extract_t(const double2* __restrict__ F
       const int64_t oi = (c * L1 + k1) * L0 + k0;
       if constexpr (PAIR) {
         a[oi] = (T)(v.x * scale);
-        if (b != nullptr) b[oi] = (T)(v.y * scale);
+        if (b != nullptr) b[oi] = (T)(v.y * scale_b);
       } else {
         reinterpret_cast<C2<T>*>(a)[oi] = mk<T>((T)(v.x * scale), (T)(v.y * scale));
       }
@@ -316,29 +340,33 @@ __global__ __launch_bounds__(256) void k_extract_t(const double2* __restrict__ F
 }
 template <typename T>
 void extract_t(const double2* F, void* a, void* b, int64_t L0, int64_t L1, int64_t H, int64_t Ssrc, int compact_src,
-               double scale, hipStream_t s) {
+               double scale, hipStream_t s, const unsigned long long* mx) {
   const dim3 grid((unsigned)((H + 1 + 31) / 32), (unsigned)((L0 + 31) / 32), (unsigned)L1);
   if (b != nullptr)
     hipLaunchKernelGGL((k_extract_t<T, true>), grid, dim3(256), 0, s, F, (T*)a, (T*)b, L0, L1, H + 1, Ssrc,
-                       compact_src, H, scale);
+                       compact_src, H, scale, mx);
   else
     hipLaunchKernelGGL((k_extract_t<T, false>), grid, dim3(256), 0, s, F, (T*)a, (T*)nullptr, L0, L1, H + 1, Ssrc,
-                       compact_src, H, scale);
+                       compact_src, H, scale, mx);
 }
 template <typename T>
 void extract_t_re(const double2* F, void* a, int64_t L0, int64_t L1, int64_t H, int64_t Ssrc, int compact_src,
                   double scale, hipStream_t s) {
   const dim3 grid((unsigned)((H + 1 + 31) / 32), (unsigned)((L0 + 31) / 32), (unsigned)L1);
   hipLaunchKernelGGL((k_extract_t<T, true>), grid, dim3(256), 0, s, F, (T*)a, (T*)nullptr, L0, L1, H + 1, Ssrc,
-                     compact_src, H, scale);
+                     compact_src, H, scale, (const unsigned long long*)nullptr);
 }
 template void extract_t_re<float>(const double2*, void*, int64_t, int64_t, int64_t, int64_t, int, double, hipStream_t);
 template void extract_t_re<double>(const double2*, void*, int64_t, int64_t, int64_t, int64_t, int, double, hipStream_t);
-template void extract_t<float>(const double2*, void*, void*, int64_t, int64_t, int64_t, int64_t, int, double, hipStream_t);
-template void extract_t<double>(const double2*, void*, void*, int64_t, int64_t, int64_t, int64_t, int, double, hipStream_t);
+template void extract_t<float>(const double2*, void*, void*, int64_t, int64_t, int64_t, int64_t, int, double, hipStream_t,
+                               const unsigned long long*);
+template void extract_t<double>(const double2*, void*, void*, int64_t, int64_t, int64_t, int64_t, int, double, hipStream_t,
+                                const unsigned long long*);
 
-template void extract_pair<float>(const double2*, void*, void*, int64_t, int64_t, int64_t, int, double, hipStream_t, int64_t, int64_t);
-template void extract_pair<double>(const double2*, void*, void*, int64_t, int64_t, int64_t, int, double, hipStream_t, int64_t, int64_t);
+template void extract_pair<float>(const double2*, void*, void*, int64_t, int64_t, int64_t, int, double, hipStream_t, int64_t,
+                                  int64_t, const unsigned long long*);
+template void extract_pair<double>(const double2*, void*, void*, int64_t, int64_t, int64_t, int, double, hipStream_t, int64_t,
+                                   int64_t, const unsigned long long*);
 template void extract_cplx<float>(const double2*, void*, int64_t, int64_t, int64_t, int, double, hipStream_t, int64_t, int64_t);
 template void extract_cplx<double>(const double2*, void*, int64_t, int64_t, int64_t, int, double, hipStream_t, int64_t, int64_t);
 

@@ -4,7 +4,7 @@ These pin the oracle before it is trusted as the checker for the HIP path."""
 import numpy as np
 import pytest
 
-from golden_cases import GRID_CASES, CLAMPED, load, grids_of, rel_err, op_ok
+from golden_cases import GRID_CASES, CLAMPED, load, grids_of, rel_err, op_ok, chaotic_bound
 from oracle import ziggy_oracle as zo
 
 
@@ -56,7 +56,11 @@ def test_grid_case_solves(name):
         key = f"solve_p1_it{mi}"
         x64 = T64.solve(f64["v"], do_precond=True, maxiter=mi, tol=1e-8)
         chaotic = name in CLAMPED and mi == 20
-        assert rel_err(x64, f64[key]) < (0.25 if chaotic else 1e-8), key
+        if chaotic:
+            # the reference's own chaotic spread sets the bound (golden_cases.chaotic_bound)
+            assert rel_err(x64, f64[key]) <= chaotic_bound(name, "f64", key), (key, rel_err(x64, f64[key]))
+        else:
+            assert rel_err(x64, f64[key]) < 1e-8, key
         if name not in CLAMPED:
             x32 = T32.solve(f32["v"], do_precond=True, maxiter=mi, tol=1e-8)
             # oracle fp32 error no worse than 4x the reference's own fp32 error (+ floor)
@@ -66,7 +70,10 @@ def test_grid_case_solves(name):
     x = T64.solve(f64["v"], do_precond=False, maxiter=5, tol=1e-8)
     assert rel_err(x, f64["solve_p0_it5"]) < 1e-8
     kn = zo.compute_kn(T64, f64["v"], maxiter_cg=20, tol=1e-8)
-    assert rel_err(kn, f64["kn_it20"]) < (0.25 if name in CLAMPED else 1e-8)
+    if name in CLAMPED:
+        assert rel_err(kn, f64["kn_it20"]) <= chaotic_bound(name, "f64", "kn_it20"), rel_err(kn, f64["kn_it20"])
+    else:
+        assert rel_err(kn, f64["kn_it20"]) < 1e-8
 
 
 @pytest.mark.parametrize("tag", ["f64", "f32"])

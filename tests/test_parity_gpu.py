@@ -4,13 +4,16 @@ CPU oracle.  Tolerances:
   fp32 ops  : max|y - y_ref| <= 1e-5 max|y_ref| + 1e-7, or no worse than 4x the reference's
               own fp32 error vs fp64 (ops near the clamp, see golden_cases.op_ok)
   fp32 PCG  : ||x - x64|| <= 4 ||x_ref32 - x64|| + 1e-6 ||x64||
-  fp64      : ops 1e-9 relative to max; PCG 1e-8 (clamped long solves: chaotic, see CLAMPED)
+  fp64      : ops 1e-9 relative to max; PCG 1e-8
+  clamped 20-iteration solves (G4a-c, G7: chaotic at the 1e-6 clamp): within 10x the reference's
+              own spread over nine self-perturbed re-runs (tests/golden/make_golden_clamp_alt.py),
+              plus the true-residual check
 """
 import numpy as np
 import pytest
 import torch
 
-from golden_cases import GRID_CASES, CLAMPED, load, grids_of, rel_err, op_ok, pcg_ok
+from golden_cases import GRID_CASES, CLAMPED, load, grids_of, rel_err, op_ok, pcg_ok, alt_spread, chaotic_bound
 from oracle import ziggy_oracle as zo
 
 pytestmark = pytest.mark.gpu
@@ -86,9 +89,14 @@ def test_solves_vs_golden(name, tag):
             assert ok or chaotic, (key, e, eref)
         if chaotic:
             # eigenvalues at the 1e-6 clamp: 20 iterations amplify rounding chaotically, so two
-            # implementations' iterates differ; what they share is how far they got -- the true
-            # residual |K x - b| (fp64 oracle K) of ours is within 3x of the reference's own (the
-            # reference's is 0.3-12 |b| after 20 iterations here: neither has converged)
+            # implementations' iterates differ.  (1) Against the reference's own spread: its nine
+            # self-perturbed re-runs (tests/golden/make_golden_clamp_alt.py) land up to `spread`
+            # from its golden (fp64 1.4e-5 .. 0.14, fp32 4.8e-4 .. 0.26); ours is within 10x that
+            # (capped at 0.25 / 0.5; golden_cases.chaotic_bound).  (2) How far it got: the true
+            # residual |K x - b| (fp64 oracle K) of ours is within 3x of the reference's own
+            # (0.3-12 |b| after 20 iterations: neither has converged).
+            print(name, tag, key, "err vs reference", rel_err(x, fx[key]), "reference spread", alt_spread(name, tag, key))
+            assert rel_err(x, fx[key]) <= chaotic_bound(name, tag, key), (key, rel_err(x, fx[key]))
             O = zo.ToeplitzOracle(_np(T.column).astype(np.float64), T.dims)
             b64 = fx["v"].astype(np.float64)
             res = lambda y: float(np.linalg.norm(O.matmul_K(y.astype(np.float64)) - b64) / np.linalg.norm(b64))
@@ -100,9 +108,13 @@ def test_solves_vs_golden(name, tag):
     else:
         assert pcg_ok(x, f32["solve_p0_it5"], f64["solve_p0_it5"])[0]
     kn = _np(T._matmul_by_RT(T.inv_matmul(v, do_precond=True, maxiter=20, tol=1e-8)))
-    if tag == "f64":
-        assert rel_err(kn, f64["kn_it20"]) < (0.25 if name in CLAMPED else 1e-8)
-    elif name not in CLAMPED:
+    if name in CLAMPED:
+        print(name, tag, "kn_it20 err vs reference", rel_err(kn, fx["kn_it20"]), "reference spread",
+              alt_spread(name, tag, "kn_it20"))
+        assert rel_err(kn, fx["kn_it20"]) <= chaotic_bound(name, tag, "kn_it20"), rel_err(kn, fx["kn_it20"])
+    elif tag == "f64":
+        assert rel_err(kn, f64["kn_it20"]) < 1e-8
+    else:
         assert pcg_ok(kn, f32["kn_it20"], f64["kn_it20"])[0]
 
 
