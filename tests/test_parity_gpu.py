@@ -4,7 +4,7 @@ CPU oracle.  Tolerances:
   fp32 ops  : max|y - y_ref| <= 1e-5 max|y_ref| + 1e-7, or no worse than 4x the reference's
               own fp32 error vs fp64 (ops near the clamp, see golden_cases.op_ok)
   fp32 PCG  : ||x - x64|| <= 4 ||x_ref32 - x64|| + 1e-6 ||x64||
-  fp64      : ops 1e-9 relative to max; PCG 1e-8
+  fp64      : ops within 50x the NumPy oracle's own error vs the reference; PCG 1e-8
   clamped 20-iteration solves (G4a-c, G7: chaotic at the 1e-6 clamp): within 10x the reference's
               own spread over nine self-perturbed re-runs (tests/golden/make_golden_clamp_alt.py),
               plus the true-residual check
@@ -59,12 +59,19 @@ def test_ops_vs_golden(name, tag):
     v = torch.tensor(fx["v"], device=DEV)
     w = torch.tensor(fx["w"], device=DEV)
     T.set_batch_shape(v.shape[:-1])
+    O = zo.ToeplitzOracle(f64["column"].astype(np.float64), T.dims)
+    oracle = {"Kv": O.matmul_K, "Cinv_v": O.matmul_Cinv, "RTv": O.matmul_RT, "Rw": O.matmul_R}
     for key, fn, x in (("Kv", T._matmul_by_K, v), ("Cinv_v", T._matmul_by_Cinv, v),
                        ("RTv", T._matmul_by_RT, v), ("Rw", T._matmul_by_R, w)):
         y = _np(fn(x))
         assert y.shape == fx[key].shape, key
         if tag == "f64":
-            assert rel_err(y, fx[key]) < 1e-9, (key, rel_err(y, fx[key]))
+            # as accurate as an exact fp64 FFT implementation: within 50x the NumPy oracle's own
+            # distance from the reference (1e-9 before round 4 -- loose enough to hide a 400x K
+            # error at the clamp)
+            e_or = rel_err(oracle[key](f64["v" if key != "Rw" else "w"].astype(np.float64)), fx[key])
+            print(name, key, "gpu", rel_err(y, fx[key]), "oracle", e_or)
+            assert rel_err(y, fx[key]) <= 50 * e_or + 1e-14, (key, rel_err(y, fx[key]), e_or)
         else:
             assert op_ok(y, fx[key], f64[key]), (key, rel_err(y, f64[key]), rel_err(fx[key], f64[key]))
 
