@@ -1821,18 +1821,20 @@ int xcorr_grid(hgp_plan* P, int useR, const void* v, const void* h, int h_period
   GridDims gd;
   gd.d = P->d;
   for (int a = 0; a < 3; ++a) { gd.m[a] = P->m[a]; gd.n[a] = P->n[a]; gd.L[a] = L[a]; }
-  for (int i = 0; i < 3; ++i) HGP_TRY(buf[i].ensure((size_t)prodL * sizeof(double2)));
+  // (one spare double2 after S holds the packing maxima of the current RHS)
+  for (int i = 0; i < 3; ++i) HGP_TRY(buf[i].ensure((size_t)(prodL + (i == 2 ? 1 : 0)) * sizeof(double2)));
   double2* z = reinterpret_cast<double2*>(buf[0].ptr);
   double2* w = reinterpret_cast<double2*>(buf[1].ptr);
   double2* S = reinterpret_cast<double2*>(buf[2].ptr);
+  unsigned long long* mx = reinterpret_cast<unsigned long long*>(S + prodL);
   const size_t es = P->esz;
   const int64_t hs = h_periodic ? P->Mp : P->M;
   for (int64_t b = 0; b < nb; ++b) {
     pack_pair(P->dtype, static_cast<const char*>(v) + (size_t)(b * P->M) * es,
-              static_cast<const char*>(h) + (size_t)(b * hs) * es, h_periodic, gd, prodL, z, s);
+              static_cast<const char*>(h) + (size_t)(b * hs) * es, h_periodic, gd, prodL, z, mx, P->M, hs, s);
     double2* Z = nullptr;
     HGP_TRY(fwd_grid_f64(P, L, tw, z, w, &Z));
-    xspec_acc(Z, S, gd, prodL, b == 0 ? 1 : 0, s);
+    xspec_acc(Z, S, gd, prodL, b == 0 ? 1 : 0, mx, s);
   }
   if (nb == 0) HIP_TRY(hipMemsetAsync(S, 0, (size_t)prodL * sizeof(double2), s));
   conj_inplace(S, prodL, s);

@@ -18,6 +18,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "hgp_internal.hpp"
 
 namespace hgp {
@@ -151,11 +153,39 @@ __device__ __forceinline__ void decodeL(int64_t f, const LGeo& G, int* c) {
 // t mod L for t in (-L, 2L)
 __device__ __forceinline__ int wrapL(int t, int L) { return t < 0 ? t + L : (t >= L ? t - L : t); }
 
+// max |v| and max |h| of one RHS (finite values, as the bits of positive doubles) -> mx[0], mx[1]
+// for pack_scale: h is packed with v at v's magnitude, so neither transform carries the other's
+// rounding (the same reason as the set-up's K + i C^-1 grid, hgp_internal.hpp)
+template <typename T>
+__global__ void k_absmax2(const T* __restrict__ v, int64_t nv, const T* __restrict__ h, int64_t nh,
+                          unsigned long long* mx) {
+  double a = 0.0, b = 0.0;
+  const int64_t n = nv > nh ? nv : nh;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (i < nv) { const double x = fabs((double)v[i]); if (isfinite(x)) a = fmax(a, x); }
+    if (i < nh) { const double x = fabs((double)h[i]); if (isfinite(x)) b = fmax(b, x); }
+  }
+  __shared__ double sm[2][256 / 64];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    a = fmax(a, __shfl_xor(a, off, 64));
+    b = fmax(b, __shfl_xor(b, off, 64));
+  }
+  if ((threadIdx.x & 63) == 0) { sm[0][threadIdx.x >> 6] = a; sm[1][threadIdx.x >> 6] = b; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) { a = fmax(a, sm[0][w]); b = fmax(b, sm[1][w]); }
+    atomicMax(mx, (unsigned long long)__double_as_longlong(a));
+    atomicMax(mx + 1, (unsigned long long)__double_as_longlong(b));
+  }
+}
+
 template <typename T>
 __global__ void k_pack_pair(const T* __restrict__ v, const T* __restrict__ h, int h_periodic, LGeo G,
-                            int64_t prodL, double2* __restrict__ z) {
+                            int64_t prodL, double2* __restrict__ z, const unsigned long long* mx) {
   const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (f >= prodL) return;
+  const double sc = pack_scale(mx);
   int c[3];
   decodeL(f, G, c);
   bool inm = true, inh = true;
@@ -170,16 +200,17 @@ __global__ void k_pack_pair(const T* __restrict__ v, const T* __restrict__ h, in
   }
   double2 r;
   r.x = inm ? (double)v[im] : 0.0;
-  r.y = h_periodic ? (inh ? (double)h[ih] : 0.0) : (inm ? (double)h[im] : 0.0);
+  r.y = (h_periodic ? (inh ? (double)h[ih] : 0.0) : (inm ? (double)h[im] : 0.0)) * sc;
   z[f] = r;
 }
 
 // S (+)= conj(V) H with V = (Z + conj Z(-f)) / 2, H = (Z - conj Z(-f)) / 2i; Z in the FWD
 // passes' stored order, S written in natural frequency order (the input of the inverse FFT)
 __global__ void k_xspec_acc(const double2* __restrict__ Z, double2* __restrict__ S, LGeo G, int64_t prodL,
-                            int first) {
+                            int first, const unsigned long long* mx) {
   const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (f >= prodL) return;
+  const double isc = 0.5 / pack_scale(mx);     // H was packed x pack_scale (exact power of two)
   int c[3];
   decodeL(f, G, c);
   int64_t nf = 0, fn = 0;
@@ -190,7 +221,7 @@ __global__ void k_xspec_acc(const double2* __restrict__ Z, double2* __restrict__
   }
   const double2 zf = Z[f], zn = Z[nf];
   const double vr = 0.5 * (zf.x + zn.x), vi = 0.5 * (zf.y - zn.y);      // V
-  const double hr = 0.5 * (zf.y + zn.y), hi = -0.5 * (zf.x - zn.x);     // H
+  const double hr = isc * (zf.y + zn.y), hi = -isc * (zf.x - zn.x);     // H
   double2 p;
   p.x = vr * hr + vi * hi;                                              // conj(V) H
   p.y = vr * hi - vi * hr;
@@ -402,14 +433,23 @@ void mul_mu_out(int dtype, const double* r, int64_t M, const GridDims& gd, void*
 }
 
 void pack_pair(int dtype, const void* v, const void* h, int h_periodic, const GridDims& gd, int64_t prodL, double2* z,
-               hipStream_t s) {
+               unsigned long long* mx, int64_t nv, int64_t nh, hipStream_t s) {
   const LGeo G = make_lgeo(gd);
-  if (dtype == 1) k_pack_pair<double><<<nblk(prodL, 256), 256, 0, s>>>((const double*)v, (const double*)h, h_periodic, G, prodL, z);
-  else k_pack_pair<float><<<nblk(prodL, 256), 256, 0, s>>>((const float*)v, (const float*)h, h_periodic, G, prodL, z);
+  const int64_t n = nv > nh ? nv : nh;
+  const unsigned nb = (unsigned)std::min<int64_t>(1024, (n + 255) / 256);
+  (void)hipMemsetAsync(mx, 0, 2 * sizeof(unsigned long long), s);
+  if (dtype == 1) {
+    k_absmax2<double><<<nb, 256, 0, s>>>((const double*)v, nv, (const double*)h, nh, mx);
+    k_pack_pair<double><<<nblk(prodL, 256), 256, 0, s>>>((const double*)v, (const double*)h, h_periodic, G, prodL, z, mx);
+  } else {
+    k_absmax2<float><<<nb, 256, 0, s>>>((const float*)v, nv, (const float*)h, nh, mx);
+    k_pack_pair<float><<<nblk(prodL, 256), 256, 0, s>>>((const float*)v, (const float*)h, h_periodic, G, prodL, z, mx);
+  }
 }
 
-void xspec_acc(const double2* Z, double2* S, const GridDims& gd, int64_t prodL, int first, hipStream_t s) {
-  k_xspec_acc<<<nblk(prodL, 256), 256, 0, s>>>(Z, S, make_lgeo(gd), prodL, first);
+void xspec_acc(const double2* Z, double2* S, const GridDims& gd, int64_t prodL, int first, const unsigned long long* mx,
+               hipStream_t s) {
+  k_xspec_acc<<<nblk(prodL, 256), 256, 0, s>>>(Z, S, make_lgeo(gd), prodL, first, mx);
 }
 
 void conj_inplace(double2* S, int64_t n, hipStream_t s) { k_conj<<<nblk(n, 256), 256, 0, s>>>(S, n); }

@@ -110,9 +110,12 @@ hipError_t sym_toeplitz_dqf(int dtype, const void* u, const void* v, int64_t nve
 void fold_div_mu(const double* X, int64_t M, const GridDims& gd, double* y, hipStream_t s);
 void spec_bwd(double* y, const double* D3, int64_t M, int kind, double cmin, hipStream_t s);
 void mul_mu_out(int dtype, const double* r, int64_t M, const GridDims& gd, void* out, hipStream_t s);
+// v + i h on the L-grid, h scaled to v's magnitude by pack_scale (mx: 2 device words, reduced
+// here over the nv / nh values of v / h); xspec_acc undoes the scale
 void pack_pair(int dtype, const void* v, const void* h, int h_periodic, const GridDims& gd, int64_t prodL, double2* z,
+               unsigned long long* mx, int64_t nv, int64_t nh, hipStream_t s);
+void xspec_acc(const double2* Z, double2* S, const GridDims& gd, int64_t prodL, int first, const unsigned long long* mx,
                hipStream_t s);
-void xspec_acc(const double2* Z, double2* S, const GridDims& gd, int64_t prodL, int first, hipStream_t s);
 void conj_inplace(double2* S, int64_t n, hipStream_t s);
 // fp64 full-grid route of R / R^T (hgp_grad.hip): gd.m = the input / output extents, gd.L = L_R
 void grid_embed(int dtype, const void* x, const GridDims& gd, int64_t prodL, double2* z, hipStream_t s);

@@ -156,6 +156,30 @@ def test_column_grad_vs_oracle(dims):
         assert rel_err(_np(got), T.column_grad(name, x, g)) < 1e-9, name
 
 
+@pytest.mark.parametrize("scale", [1e6, 1e-6], ids=["x_big", "x_small"])
+def test_column_grad_mismatched_scales(scale):
+    """The column gradient correlates x with the upstream gradient g through one packed complex
+    transform (x + i g): with |x| / |g| = 1e6 (a solve at the 1e-6 clamp against an O(1) loss
+    gradient) or 1e-6, the smaller one must not carry the larger one's rounding -- g is packed at
+    x's magnitude by a power of two (hgp_grad.hip k_absmax2 / pack_scale).  fp64 vs the oracle."""
+    from hipgp_amd import _lib
+    from hipgp_amd.plan import ToeplitzPlan
+    dims = (24, 20)
+    rs = np.random.RandomState(7)
+    grids = [np.linspace(-1, 1, m) for m in dims]
+    col = zo.toeplitz_column(grids, lambda a, b: zo.kernel_eval("matern", a, b, (1., .3), nu=1.5), 1e-3)
+    T = zo.ToeplitzOracle(col, dims)
+    P = ToeplitzPlan(dims, dtype=torch.float64, device=DEV)
+    P.set_column(torch.tensor(col, device=DEV))
+    for op, name, nin, nout in ((_lib.OP_K, "K", T.M, T.M), (_lib.OP_CINV, "Cinv", T.M, T.M),
+                                (_lib.OP_RT, "RT", T.M, T.Mp), (_lib.OP_R, "R", T.Mp, T.M)):
+        x, g = rs.randn(2, nin) * scale, rs.randn(2, nout)
+        got = P.column_grad(op, torch.tensor(x, device=DEV), torch.tensor(g, device=DEV))
+        err = rel_err(_np(got), T.column_grad(name, x, g))
+        print(name, scale, err)
+        assert err < 1e-12, (name, err)
+
+
 @pytest.mark.parametrize("dims", [(300,), (12, 10), (2, 9), (6, 5, 4), (3, 2, 7), (9000,)],
                          ids=lambda d: "x".join(map(str, d)))
 @pytest.mark.parametrize("tag", ["f64", "f32"])
