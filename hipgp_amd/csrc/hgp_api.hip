@@ -883,7 +883,10 @@ int set_column_t(hgp_plan* P, const void* column, double jitter, double clamp_mi
   }
   HIP_TRY(hipMemsetAsync(P->nclamp.ptr, 0, 3 * sizeof(unsigned long long), s));
   double* D3 = reinterpret_cast<double*>(P->Dm3.ptr);
-  clamp_spectrum(a, D3, M, clamp_min, reinterpret_cast<unsigned long long*>(P->nclamp.ptr), s);
+  GridDims gm;
+  gm.d = d;
+  for (int ax = 0; ax < 3; ++ax) { gm.m[ax] = P->m[ax]; gm.n[ax] = P->n[ax]; gm.L[ax] = P->LK[ax]; }
+  clamp_spectrum(a, D3, M, clamp_min, reinterpret_cast<unsigned long long*>(P->nclamp.ptr), gm, s);
   // generators: c_K = IFFT_n(D), c_inv = IFFT_n(1/D), s = IFFT_n(sqrt D) on the m-grid
   double* src = D3;
   double* dst = a;

@@ -42,7 +42,7 @@ template <typename T> void to_f64(const void* src, double* dst, int64_t n, doubl
 // nclamp[0] counts the clamped entries; nclamp[1] / nclamp[2] receive max D / max 1/D (finite
 // values, as the bits of positive doubles) for pack_scale
 void clamp_spectrum(const double* Draw, double* out3, int64_t M, double clamp_min, unsigned long long* nclamp,
-                    hipStream_t s);
+                    const GridDims& g, hipStream_t s);
 // The set-up transforms the K and C^-1 generators as ONE complex grid (K real, C^-1 imaginary).
 // A transform's rounding is relative to its largest value, and at the clamp 1/D reaches 1e6 where
 // D stays ~1e3: packed as they are, the K spectrum would carry C^-1-sized rounding (K matvec 400x

@@ -1,4 +1,6 @@
 // hgp_kernels.hip — pass dispatch, spectrum-setup kernels and batched-CG kernels.
+#include <algorithm>
+
 #include "hgp_internal.hpp"
 
 namespace hgp {
@@ -88,42 +90,59 @@ void to_f64(const void* src, double* dst, int64_t n, double add0, hipStream_t s)
 template void to_f64<float>(const void*, double*, int64_t, double, hipStream_t);
 template void to_f64<double>(const void*, double*, int64_t, double, hipStream_t);
 
-// D = max(Draw, clamp); write [D | 1/D | sqrt(D)] (3 x M) and count clamped entries.
+// D = max(Draw, clamp); write [D | 1/D | sqrt(D)] (3 x M) and count clamped entries; the
+// maxima of D and 1/D (pack_scale) by a grid-stride sweep of <= 1024 blocks, one atomic each per
+// block (one per 256 elements serialised on two words: 97 us at 1M elements)
+// The m-grid holds the DCT-I half spectrum: entry (k_0, .., k_{d-1}) stands for prod_a w(k_a)
+// eigenvalues of the circulant (w = 1 at k = 0 and k = m - 1, else 2: the mirror n - k), so the
+// count is the number of clamped eigenvalues of the full expanded spectrum the reference clamps.
 __global__ void k_clamp(const double* __restrict__ Draw, double* __restrict__ out3, int64_t M, double clamp_min,
-                        unsigned long long* nclamp) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool in = i < M;
-  double d = in ? Draw[i] : clamp_min;
-  if (!(d >= clamp_min)) {      // torch.clamp(min=) semantics: values below min (NaN stays NaN)
-    if (d < clamp_min) { d = clamp_min; atomicAdd(nclamp, 1ull); }
-  }
-  if (in) {
+                        unsigned long long* nclamp, GridDims g) {
+  double a = 0.0, b = 0.0;
+  unsigned long long nc = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < M; i += (int64_t)gridDim.x * blockDim.x) {
+    double d = Draw[i];
+    if (!(d >= clamp_min)) {    // torch.clamp(min=) semantics: values below min (NaN stays NaN)
+      if (d < clamp_min) {
+        d = clamp_min;
+        unsigned long long w = 1;
+        int64_t r = i;
+        for (int ax = g.d - 1; ax >= 0; --ax) {
+          const int64_t k = r % g.m[ax];
+          r /= g.m[ax];
+          if (k != 0 && k != g.m[ax] - 1) w *= 2;
+        }
+        nc += w;
+      }
+    }
     out3[i] = d;
     out3[M + i] = 1.0 / d;
     out3[2 * M + i] = sqrt(d);
-  } else {
-    d = 0.0;                    // no contribution to the maxima
+    if (d > 0.0 && isfinite(d)) a = fmax(a, d);
+    if (d > 0.0 && isfinite(1.0 / d)) b = fmax(b, 1.0 / d);
   }
-  // block maxima of D and 1/D (finite values) -> one atomic per block each (pack_scale)
   __shared__ double smx[2][256 / 64];
-  double a = (d > 0.0 && isfinite(d)) ? d : 0.0, b = (d > 0.0 && isfinite(1.0 / d)) ? 1.0 / d : 0.0;
+  __shared__ unsigned long long snc[256 / 64];
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     a = fmax(a, __shfl_xor(a, off, 64));
     b = fmax(b, __shfl_xor(b, off, 64));
+    nc += __shfl_xor(nc, off, 64);
   }
-  if ((threadIdx.x & 63) == 0) { smx[0][threadIdx.x >> 6] = a; smx[1][threadIdx.x >> 6] = b; }
+  if ((threadIdx.x & 63) == 0) { smx[0][threadIdx.x >> 6] = a; smx[1][threadIdx.x >> 6] = b; snc[threadIdx.x >> 6] = nc; }
   __syncthreads();
   if (threadIdx.x == 0) {
-    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) { a = fmax(a, smx[0][w]); b = fmax(b, smx[1][w]); }
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) { a = fmax(a, smx[0][w]); b = fmax(b, smx[1][w]); nc += snc[w]; }
+    if (nc) atomicAdd(nclamp, nc);
     atomicMax(nclamp + 1, (unsigned long long)__double_as_longlong(a));
     atomicMax(nclamp + 2, (unsigned long long)__double_as_longlong(b));
   }
 }
 
 void clamp_spectrum(const double* Draw, double* out3, int64_t M, double clamp_min, unsigned long long* nclamp,
-                    hipStream_t s) {
-  hipLaunchKernelGGL(k_clamp, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, s, Draw, out3, M, clamp_min, nclamp);
+                    const GridDims& g, hipStream_t s) {
+  const int64_t nb = std::max<int64_t>(1, std::min<int64_t>(1024, (M + 255) / 256));
+  hipLaunchKernelGGL(k_clamp, dim3((unsigned)nb), dim3(256), 0, s, Draw, out3, M, clamp_min, nclamp, g);
 }
 
 // K-type embedding (L >= 2m-1): G[u] = c[|t|], t = u (u < m) or u - L (u > L - m); complex

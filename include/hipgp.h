@@ -56,7 +56,9 @@ int hgp_plan_set_stream(hgp_plan* plan, void* hip_stream);
  * column[0] += jitter (toeplitz_tensor.py:132; pass 0 when already included), circulant
  * embedding (toeplitz_tensor.py:135-143), D = clamp(Re FFT(C), clamp_min) (:25-31), and the
  * operator spectra for K, C^-1 and R/R^T.  Replaces toeplitz_tensor.py:12-33.
- * If n_clamped != NULL it receives the number of clamped eigenvalues (synchronises). */
+ * If n_clamped != NULL it receives the number of clamped eigenvalues of the full expanded
+ * (n-grid) spectrum, each mirror image counted, as (D_raw < clamp_min).sum() over the
+ * reference's D (synchronises). */
 int hgp_plan_set_column(hgp_plan* plan, const void* column, double jitter, double clamp_min,
                         int64_t* n_clamped);
 

@@ -56,6 +56,13 @@ def test_ops_vs_golden(name, tag):
     assert rel_err(1 / _np(T.Di[..., 0]).astype(np.float64), 1 / f64["Di"]) < dtol
     if tag == "f64":
         assert np.array_equal(_np(T.D[..., 0]) <= 1e-6, fx["D"] <= 1e-6)
+        # the set-up's clamp counter (hgp_plan_set_column n_clamped) against the raw spectrum
+        from hipgp_amd.plan import ToeplitzPlan
+        P = ToeplitzPlan(T.dims, dtype=torch.float64, device=DEV)
+        # (the golden column already holds the jitter on c0, as the reference's T.column)
+        n = P.set_column(torch.tensor(fx["column"], device=DEV), count_clamped=True)
+        raw = np.fft.fftn(zo.circulant_embed(fx["column"].reshape(T.dims))).real
+        assert n == int(np.sum(raw < 1e-6)), (n, int(np.sum(raw < 1e-6)))
     v = torch.tensor(fx["v"], device=DEV)
     w = torch.tensor(fx["w"], device=DEV)
     T.set_batch_shape(v.shape[:-1])
