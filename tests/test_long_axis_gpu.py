@@ -133,6 +133,7 @@ def test_beyond_8192_points(case, dt):
         got = P.apply(op, torch.tensor(x, device=DEV, dtype=dt)).double().cpu().numpy()
         assert got.shape == ref.shape, name
         err = float(np.abs(got - ref).max() / np.abs(ref).max())
+        print(case, dt, name, "op err vs oracle", err)
         assert err < tol_op, (name, err)
     # the spectrum served to ToeplitzTensor.D (n-grid) from the long-axis DCT set-up
     D = P.spectrum(_lib.SPEC_D).double().cpu().numpy().reshape(-1)
