@@ -127,7 +127,9 @@ def test_beyond_8192_points(case, dt):
     rs = np.random.RandomState(6)
     v = rs.randn(2, O.M)
     w = rs.randn(2, O.Mp)
-    tol_op = 2e-5 if dt == torch.float32 else 1e-10
+    # measured (profiles/r4_w_long_axis_op_errors.txt): fp64 2e-15 .. 2.4e-14 (C^-1), fp32 6e-8 ..
+    # 1.3e-6 (C^-1) -- an exact implementation's rounding; the bounds keep >= 8x margin
+    tol_op = 1e-5 if dt == torch.float32 else 1e-12
     for name, op, x, ref in (("K", _lib.OP_K, v, O.matmul_K(v)), ("Cinv", _lib.OP_CINV, v, O.matmul_Cinv(v)),
                              ("RT", _lib.OP_RT, v, O.matmul_RT(v)), ("R", _lib.OP_R, w, O.matmul_R(w))):
         got = P.apply(op, torch.tensor(x, device=DEV, dtype=dt)).double().cpu().numpy()

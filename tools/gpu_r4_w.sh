@@ -4,5 +4,5 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests/test_long_axis_gpu.py -k "beyond_8192_points and float64" -v -s --timeout 300 --timeout-method thread > gpurun_out/pytest_w.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_long_axis_gpu.py -k "test_beyond_8192_points" -v -s --timeout 300 --timeout-method thread > gpurun_out/pytest_w.log 2>&1
 rc=$?; grep -E "op err|passed|failed" gpurun_out/pytest_w.log | tail -40; exit $rc
