@@ -211,9 +211,25 @@ def _timed_max(fn, reps, dist, device, backend):
     return v * 1e3
 
 
+def _all_ok(ok, dist, device, backend):
+    """True on every rank iff `ok` on every rank (one MIN all-reduce; no-op at N = 1)."""
+    if not dist:
+        return ok
+    import torch.distributed as tdist
+    t = torch.tensor([1 if ok else 0], device=device if backend == "nccl" else "cpu", dtype=torch.int32)
+    tdist.all_reduce(t, op=tdist.ReduceOp.MIN)
+    return bool(int(t.item()))
+
+
 def c4_strong_leg(args, device, dist, world, rank):
     """Config 4 (4096^2, Matern-3/2, 200 RHS global) compute_kn split over the ranks: the
-    workload the 8-GPU configuration is quoted on (25 RHS per GPU at N = 8)."""
+    workload the 8-GPU configuration is quoted on (25 RHS per GPU at N = 8).
+
+    The set-up (model, Knm) holds no collective: a failure there (e.g. out of device memory on
+    a smaller card) is agreed on by every rank (one all-reduce of an ok flag) and the leg is
+    skipped on all of them together, so no rank waits in a collective another one left.  The
+    timed solve all-reduces every PCG iteration; an error there is recorded only at N = 1 and
+    re-raised otherwise (torchrun then stops every rank instead of leaving them blocked)."""
     import ziggy.hipgp as hg
     import ziggy.kernels as zk
     from hipgp_amd import dist as hdist
@@ -225,17 +241,30 @@ def c4_strong_leg(args, device, dist, world, rank):
     out = {"what": "config 4: compute_kn (set-up + PCG(20, tol 1e-8, precond, all-RHS break over ranks) + R^T) "
                    "for its fixed global batch of 200 RHS on the 4096^2 grid, split over the ranks",
            "global_rhs": G, "rhs_per_rank": sl.stop - sl.start, "grid": [m4, m4], "scaling": "strong"}
+    mod = Knm_local = None
+    err = None
     try:
         mod = hg.MeanFieldToeplitzGP(zk.Matern(nu=1.5, dtype=torch.float32), grids4, num_obs=100_000,
                                      sig2_init=0.1, ell_init=0.1, learn_kernel=False, jitter_val=1e-3,
                                      dtype=torch.float32).cuda_params(device.index)
         Knm_local, _ = mod._make_grams(x[sl])
+        torch.cuda.synchronize()
+    except RuntimeError as e:      # e.g. out of device memory on a smaller card
+        err = str(e).splitlines()[0][:200]
+    if not _all_ok(err is None, dist, device, args.backend):
+        out["error"] = err if err is not None else "set-up failed on another rank"
+        del mod, Knm_local
+        torch.cuda.empty_cache()
+        return out
+    try:
         ms = _timed_max(lambda: hdist.sharded_compute_kn(mod, Knm_local, maxiter_cg=20, tol=1e-8, exact_break=dist),
                         1, dist, device, args.backend)
         out.update({"ms": ms, "rhs_per_s": G / (ms * 1e-3)})
-        del mod, Knm_local
-    except RuntimeError as e:      # e.g. out of device memory on a smaller card: recorded, not fatal
+    except RuntimeError as e:
+        if dist:
+            raise
         out["error"] = str(e).splitlines()[0][:200]
+    del mod, Knm_local
     torch.cuda.empty_cache()
     return out
 
@@ -425,8 +454,10 @@ def main():
     pair_int = m * L[1] * 8                                  # complex intermediate per RHS pair
     Q = (B + 1) // 2
     pass_bytes = [Q * (2 * M * 4 + pair_int), Q * 2 * pair_int + L[0] * L[1] * 4, Q * (pair_int + 2 * M * 4)]
-    kernels = [{"pass": i, "ms": round(pass_ms[i], 4),
-                "gbs": round(pass_bytes[i] / (pass_ms[i] * 1e-3) / 1e9, 1)} for i in range(npass)]
+    kernels = [{"pass": i, "kernel": ("rows fwd", "column conv", "rows inv")[i] if npass == 3 else str(i),
+                "ms": round(pass_ms[i], 4), "bytes": pass_bytes[i],
+                "gbs": round(pass_bytes[i] / (pass_ms[i] * 1e-3) / 1e9, 1),
+                "frac": round(pass_bytes[i] / (pass_ms[i] * 1e-3) / 1e9 / HBM_PEAK_GBS, 3)} for i in range(npass)]
     pcg_ms = reduce_max(float(np.median(pcg_times) * 1e3))
     traffic, traffic_src = pmc_traffic(M, B)
 
@@ -458,7 +489,10 @@ def main():
                      "kernel": "batched K matvec = 3 pass kernels (FWD rows, CONV cols, INV rows)",
                      "bytes_per_launch": bytes_launch,
                      "event_op_ms": op_ms, "event_achieved": achieved_ev,
-                     "event_frac": achieved_ev / HBM_PEAK_GBS, "passes": kernels},
+                     "event_frac": achieved_ev / HBM_PEAK_GBS, "passes": kernels,
+                     # the op's slowest pass-isolated kernel (the column conv at C2) with its own
+                     # algorithmic bytes and roofline fraction
+                     "dominant_pass": max(kernels, key=lambda k: k["ms"])},
     }
     if legs is not None:
         out.update(legs)

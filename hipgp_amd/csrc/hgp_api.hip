@@ -148,11 +148,22 @@ struct hgp_plan {
     void* y = nullptr;
     int64_t nrhs = 0;
     hipStream_t stream = nullptr;
-    void *ws1 = nullptr, *ws2 = nullptr;
+    // every plan-owned buffer an op's launches address (workspaces, the full-grid route's
+    // buffers, the spectra): a reallocation of any of them -- e.g. R^T on a grid_k plan growing
+    // gridA / gridB past K's size -- must invalidate a captured graph
+    static constexpr int NB = 9;
+    const void* buf[NB] = {};
     bool operator==(const ApplyKey& o) const {
-      return op == o.op && x == o.x && y == o.y && nrhs == o.nrhs && stream == o.stream && ws1 == o.ws1 && ws2 == o.ws2;
+      if (!(op == o.op && x == o.x && y == o.y && nrhs == o.nrhs && stream == o.stream)) return false;
+      for (int i = 0; i < NB; ++i)
+        if (buf[i] != o.buf[i]) return false;
+      return true;
     }
   };
+  void key_buffers(ApplyKey& k) const {
+    const DevBuf* b[ApplyKey::NB] = {&ws1, &ws2, &gridA, &gridB, &specK, &specI, &specR, &specRg, &specKg};
+    for (int i = 0; i < ApplyKey::NB; ++i) k.buf[i] = b[i]->ptr;
+  }
   ApplyKey last_apply, graph_key;
   hipGraphExec_t graph_exec = nullptr;
   hipStream_t cap_stream = nullptr;       // captures run here (torch's default stream cannot capture)
@@ -302,7 +313,8 @@ using MidFn = std::function<void(int64_t, int, hipStream_t)>;
 // pass of the sequence (profiling).  2-D only: `spart` receives the column pass's spectral
 // dots <x, op x> per (RHS, compact column) [q][L_1/2 + 1]; `epi` replaces the output store by
 // the fused PCG update, `mid` runs between the column pass and the row-inverse pass.
-int fwd_grid_f64(hgp_plan* P, const int64_t* L, const DevBuf* tw64, double2* a, double2* b, double2** result);
+int fwd_grid_f64(hgp_plan* P, const int64_t* L, const DevBuf* tw64, double2* a, double2* b, double2** result,
+                 const int* done = nullptr);
 
 // The full-grid route, one RHS at a time on the full fp64 L-grid of the operator:
 // y = crop(IFFT(S' FFT(pad x))), the inverse as conj(FFT(conj Y)) / N (the 1/N is in the stored
@@ -312,7 +324,8 @@ int fwd_grid_f64(hgp_plan* P, const int64_t* L, const DevBuf* tw64, double2* a, 
 // complex fp64.  A fused dot (dotv) becomes per-RHS row-chunk partials of y . dotv
 // (rowdot_part: update_np(out M) per RHS, the unfused PCG's op_np).
 template <typename T>
-int run_op_grid(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void* dotv, void* partial) {
+int run_op_grid(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void* dotv, void* partial,
+                const int* done) {
   hipStream_t s = P->stream;
   const int d = P->d;
   const bool rtype = op == HGP_OP_R || op == HGP_OP_RT;
@@ -337,14 +350,14 @@ int run_op_grid(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const
   const int mode = op == HGP_OP_R ? 1 : op == HGP_OP_RT ? 0 : op == HGP_OP_K ? 2 : 3;
   const size_t es = P->esz;
   for (int64_t q = 0; q < nrhs; ++q) {
-    grid_embed(P->dtype, static_cast<const char*>(x) + (size_t)(q * inM) * es, gi, N, A, s);
+    grid_embed(P->dtype, static_cast<const char*>(x) + (size_t)(q * inM) * es, gi, N, A, s, done);
     double2* F = nullptr;
-    HGP_TRY(fwd_grid_f64(P, Lg, tw64, A, B, &F));
+    HGP_TRY(fwd_grid_f64(P, Lg, tw64, A, B, &F, done));
     double2* other = (F == A) ? B : A;
-    grid_mul_unperm(F, S, gi, N, mode, other, s);
+    grid_mul_unperm(F, S, gi, N, mode, other, s, done);
     double2* Z = nullptr;
-    HGP_TRY(fwd_grid_f64(P, Lg, tw64, other, F, &Z));
-    grid_crop(P->dtype, Z, go, outM, static_cast<char*>(y) + (size_t)(q * outM) * es, s);
+    HGP_TRY(fwd_grid_f64(P, Lg, tw64, other, F, &Z, done));
+    grid_crop(P->dtype, Z, go, outM, static_cast<char*>(y) + (size_t)(q * outM) * es, s, done);
   }
   if (dotv != nullptr && partial != nullptr)
     rowdot_part<T>(y, dotv, partial, nrhs, outM, update_np(outM), s);
@@ -363,9 +376,10 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
   if (grid_route(P, op)) {
     if (spart != nullptr || epi != nullptr || mid != nullptr || only_pass >= 0)
       return fail(HGP_E_UNSUPPORTED, "internal: the full-grid route has no fused PCG epilogue or pass split");
-    // (`done` is not checked here: after the break the unfused PCG's update kernels are device
-    // no-ops, and what this route still writes -- Ap / z and the dot partials -- is never read)
-    return run_op_grid<T>(P, op, x, y, nrhs, dotv, partial);
+    // after the break (`done` set) every transform / embed / crop kernel of the route is a device
+    // no-op, so the iterations up to maxiter cost launches only; the dot partials it may still
+    // write are never read
+    return run_op_grid<T>(P, op, x, y, nrhs, dotv, partial, done);
   }
   const OpGeom g = op_geom(P, op);
   const int d = P->d;
@@ -520,10 +534,14 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
         // (group, RHS) with the columns interleaved over its threads (LAY_GRP*) -- coalesced
         // 512-B accesses, but measured slower (C4 CONV 2.97 -> 3.85 ms, C3 0.765 -> 0.82 ms:
         // 16-wave blocks / interleaved exchange images, profiles/r3_grouped_passtime.txt)
-        const int glay = G2 == 2 ? LAY_GRP2 : G2 == 4 ? LAY_GRP4 : -1;
+        // G2 = 4 is stored in the quad order (HGP_QUAD, hgp_rows.hpp wg_off<4>): LAY_CONTIG_Q, two
+        // lines (one 64-B half of a group's units) per block
+        const bool quad = HGP_QUAD && G2 == 4;
+        const int glay = G2 == 2 ? LAY_GRP2 : (G2 == 4 && !quad) ? LAY_GRP4 : -1;
         static const bool grp_on = [] { const char* e = std::getenv("HGP_GRP_BLOCKS"); return e && std::atoi(e) == 1; }();
         const bool use_grp = glay >= 0 && grp_on && pass_geom<T>((int)(g.L[0] / 2), glay).C == G2;
-        HGP_TRY(run((int)(g.L[0] / 2), conv_mode, use_grp ? glay : LAY_CONTIG_G, Bd, (int64_t)qn * ((H1 + G2) / G2) * G2));
+        const int clay = use_grp ? glay : quad ? LAY_CONTIG_Q : LAY_CONTIG_G;
+        HGP_TRY(run((int)(g.L[0] / 2), conv_mode, clay, Bd, (int64_t)qn * ((H1 + G2) / G2) * G2));
       } else {
         HGP_TRY(run((int)(g.L[0] / 2), conv_mode, LAY_CONTIG, Bd, (int64_t)qn * Bd.Rn));
       }
@@ -672,10 +690,12 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
 // level moves its lines between the two buffers, so the result may end in either: *result.
 // tw = W_L; lev[j] = W_{L / 2^(j+1)} (the plan's tw64Kl / tw64Rl of the axis).
 int fft_lines_f64(hgp_plan* P, double2* a, double2* b, int64_t L, int64_t Rn, int64_t r_stride, int64_t In,
-                  int64_t ps, const void* tw, const DevBuf* lev, int depth, double2** result) {
+                  int64_t ps, const void* tw, const DevBuf* lev, int depth, double2** result,
+                  const int* done = nullptr) {
   hipStream_t s = P->stream;
   if (L / 2 <= 8192) {
     PassDesc D = base_desc();
+    D.done = done;
     D.in = View{a, 0, r_stride, ps, (int)L};
     D.out = View{b, 0, r_stride, ps, (int)L};
     D.tw = tw; D.Q = 1; D.Rn = (int)Rn; D.In = (int)In;
@@ -689,11 +709,12 @@ int fft_lines_f64(hgp_plan* P, double2* a, double2* b, int64_t L, int64_t Rn, in
   double2* half_res = nullptr;
   for (int e = 0; e < 2; ++e) {
     double2* r = nullptr;
-    HGP_TRY(fft_lines_f64(P, a + e * ps, b + e * ps, L / 2, Rn, r_stride, In, 2 * ps, lev[depth].ptr, lev, depth + 1, &r));
+    HGP_TRY(fft_lines_f64(P, a + e * ps, b + e * ps, L / 2, Rn, r_stride, In, 2 * ps, lev[depth].ptr, lev, depth + 1, &r,
+                          done));
     half_res = (r == a + e * ps) ? a : b;
   }
   double2* dst = (half_res == a) ? b : a;
-  r2_combine(half_res, dst, L, Rn, r_stride, In, ps, reinterpret_cast<const double2*>(tw), s);
+  r2_combine(half_res, dst, L, Rn, r_stride, In, ps, reinterpret_cast<const double2*>(tw), s, done);
   HIP_TRY(hipGetLastError());
   *result = dst;
   return 0;
@@ -707,13 +728,14 @@ const DevBuf* tw_levels(const hgp_plan* P, const DevBuf* tw64, int ax) {
 }
 
 // Forward FFT of a full (unpruned) fp64 complex L-grid: a -> result pointer (a or b).
-int fwd_grid_f64(hgp_plan* P, const int64_t* L, const DevBuf* tw64, double2* a, double2* b, double2** result) {
+int fwd_grid_f64(hgp_plan* P, const int64_t* L, const DevBuf* tw64, double2* a, double2* b, double2** result,
+                 const int* done) {
   const int d = P->d;
   double2* cur = a;
   double2* oth = b;
   auto step = [&](int ax, int64_t Rn, int64_t rs, int64_t In, int64_t ps) -> int {
     double2* r = nullptr;
-    HGP_TRY(fft_lines_f64(P, cur, oth, L[ax], Rn, rs, In, ps, tw64[ax].ptr, tw_levels(P, tw64, ax), 0, &r));
+    HGP_TRY(fft_lines_f64(P, cur, oth, L[ax], Rn, rs, In, ps, tw64[ax].ptr, tw_levels(P, tw64, ax), 0, &r, done));
     if (r != cur) std::swap(cur, oth);
     return 0;
   };
@@ -1496,7 +1518,8 @@ int hgp_toeplitz_apply(hgp_plan* plan, int op, const void* x, void* y, int64_t n
   HGP_TRY(use_device(plan));
   hgp_plan* P = plan;
   hgp_plan::ApplyKey key;
-  key.op = op; key.x = x; key.y = y; key.nrhs = nrhs; key.stream = P->stream; key.ws1 = P->ws1.ptr; key.ws2 = P->ws2.ptr;
+  key.op = op; key.x = x; key.y = y; key.nrhs = nrhs; key.stream = P->stream;
+  P->key_buffers(key);
   // a caller that is itself capturing (e.g. torch.cuda.graphs) records our launches directly
   hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(P->stream, &cst) != hipSuccess) { (void)hipGetLastError(); cst = hipStreamCaptureStatusActive; }
@@ -1510,7 +1533,7 @@ int hgp_toeplitz_apply(hgp_plan* plan, int op, const void* x, void* y, int64_t n
     // first call with these arguments: run it directly (workspaces are allocated here, so a
     // later capture never allocates); remember the workspaces it ended with
     HGP_TRY(DISPATCH(plan, run_op, plan, op, x, y, nrhs, nullptr, nullptr, nullptr));
-    key.ws1 = P->ws1.ptr; key.ws2 = P->ws2.ptr;
+    P->key_buffers(key);
     P->last_apply = key;
     return 0;
   }

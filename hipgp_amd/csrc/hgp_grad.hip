@@ -306,7 +306,9 @@ __global__ void k_gather_flat(const double2* __restrict__ F, LGeo G, int64_t M, 
 // pos_of per axis) and the inverse as conj(FFT(conj Y)) / N (the 1/N is in the stored S).
 // z[f] = x at natural grid point f when inside the input extents (G.m), else 0
 template <typename T>
-__global__ void k_grid_embed(const T* __restrict__ x, LGeo G, int64_t prodL, double2* __restrict__ z) {
+__global__ void k_grid_embed(const T* __restrict__ x, LGeo G, int64_t prodL, double2* __restrict__ z,
+                             const int* done) {
+  if (done != nullptr && *done) return;
   const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (f >= prodL) return;
   int c[3];
@@ -323,7 +325,8 @@ __global__ void k_grid_embed(const T* __restrict__ x, LGeo G, int64_t prodL, dou
 // out[f] (natural order) = conj(F[pos(f)] S'[pos(f)]), S' = S (mode 0), conj(S) (1), Re S (2: the
 // K spectrum of a packed K + i C^-1 transform) or Im S (3: the C^-1 spectrum)
 __global__ void k_grid_mul_unperm(const double2* __restrict__ F, const double2* __restrict__ S, LGeo G,
-                                  int64_t prodL, int mode, double2* __restrict__ out) {
+                                  int64_t prodL, int mode, double2* __restrict__ out, const int* done) {
+  if (done != nullptr && *done) return;
   const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (f >= prodL) return;
   int c[3];
@@ -340,7 +343,9 @@ __global__ void k_grid_mul_unperm(const double2* __restrict__ F, const double2* 
 
 // y[j] (j over the output extents G.m) = Re Z[pos(j)]
 template <typename T>
-__global__ void k_grid_crop(const double2* __restrict__ Z, LGeo G, int64_t outM, T* __restrict__ y) {
+__global__ void k_grid_crop(const double2* __restrict__ Z, LGeo G, int64_t outM, T* __restrict__ y,
+                            const int* done) {
+  if (done != nullptr && *done) return;
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= outM) return;
   int c[3] = {0, 0, 0};
@@ -464,21 +469,23 @@ void gather_flat(int dtype, const double2* F, const GridDims& gd, int64_t M, dou
   else k_gather_flat<float><<<nblk(M, 256), 256, 0, s>>>(F, G, M, invL, (float*)out);
 }
 
-void grid_embed(int dtype, const void* x, const GridDims& gd, int64_t prodL, double2* z, hipStream_t s) {
+void grid_embed(int dtype, const void* x, const GridDims& gd, int64_t prodL, double2* z, hipStream_t s,
+                const int* done) {
   const LGeo G = make_lgeo(gd);
-  if (dtype == 1) k_grid_embed<double><<<nblk(prodL, 256), 256, 0, s>>>((const double*)x, G, prodL, z);
-  else k_grid_embed<float><<<nblk(prodL, 256), 256, 0, s>>>((const float*)x, G, prodL, z);
+  if (dtype == 1) k_grid_embed<double><<<nblk(prodL, 256), 256, 0, s>>>((const double*)x, G, prodL, z, done);
+  else k_grid_embed<float><<<nblk(prodL, 256), 256, 0, s>>>((const float*)x, G, prodL, z, done);
 }
 
 void grid_mul_unperm(const double2* F, const double2* S, const GridDims& gd, int64_t prodL, int mode,
-                     double2* out, hipStream_t s) {
-  k_grid_mul_unperm<<<nblk(prodL, 256), 256, 0, s>>>(F, S, make_lgeo(gd), prodL, mode, out);
+                     double2* out, hipStream_t s, const int* done) {
+  k_grid_mul_unperm<<<nblk(prodL, 256), 256, 0, s>>>(F, S, make_lgeo(gd), prodL, mode, out, done);
 }
 
-void grid_crop(int dtype, const double2* Z, const GridDims& gd, int64_t outM, void* y, hipStream_t s) {
+void grid_crop(int dtype, const double2* Z, const GridDims& gd, int64_t outM, void* y, hipStream_t s,
+               const int* done) {
   const LGeo G = make_lgeo(gd);
-  if (dtype == 1) k_grid_crop<double><<<nblk(outM, 256), 256, 0, s>>>(Z, G, outM, (double*)y);
-  else k_grid_crop<float><<<nblk(outM, 256), 256, 0, s>>>(Z, G, outM, (float*)y);
+  if (dtype == 1) k_grid_crop<double><<<nblk(outM, 256), 256, 0, s>>>(Z, G, outM, (double*)y, done);
+  else k_grid_crop<float><<<nblk(outM, 256), 256, 0, s>>>(Z, G, outM, (float*)y, done);
 }
 
 void line_embed(const double2* c, double2* E, int64_t O, int64_t m, int64_t I, int64_t L, hipStream_t s) {

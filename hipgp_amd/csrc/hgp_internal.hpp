@@ -62,7 +62,7 @@ void embed_R(const double* sv, double2* out, const GridDims& g, hipStream_t s);
 // then even and its spectrum real (set_column_t, hgp_plan::r_real)
 void embed_R_real(const double* sv, double* out, const GridDims& g, int sym, hipStream_t s);
 void r2_combine(const double2* in, double2* out, int64_t L, int64_t Rn, int64_t r_stride, int64_t In, int64_t ps,
-                const double2* tw, hipStream_t s);
+                const double2* tw, hipStream_t s, const int* done = nullptr);
 // d >= 2: tiled transposing extraction into [c][k1][k0] (hgp_kernels.hip k_extract_t); b == nullptr:
 // complex spectrum into a, else the pair (Re -> a, Im -> b)
 template <typename T>
@@ -117,11 +117,14 @@ void pack_pair(int dtype, const void* v, const void* h, int h_periodic, const Gr
 void xspec_acc(const double2* Z, double2* S, const GridDims& gd, int64_t prodL, int first, const unsigned long long* mx,
                hipStream_t s);
 void conj_inplace(double2* S, int64_t n, hipStream_t s);
-// fp64 full-grid route of R / R^T (hgp_grad.hip): gd.m = the input / output extents, gd.L = L_R
-void grid_embed(int dtype, const void* x, const GridDims& gd, int64_t prodL, double2* z, hipStream_t s);
+// fp64 full-grid route of R / R^T (hgp_grad.hip): gd.m = the input / output extents, gd.L = L_R;
+// done (optional device flag): every kernel is a no-op once *done != 0 (the PCG's break)
+void grid_embed(int dtype, const void* x, const GridDims& gd, int64_t prodL, double2* z, hipStream_t s,
+                const int* done = nullptr);
 void grid_mul_unperm(const double2* F, const double2* S, const GridDims& gd, int64_t prodL, int conj_spec,
-                     double2* out, hipStream_t s);
-void grid_crop(int dtype, const double2* Z, const GridDims& gd, int64_t outM, void* y, hipStream_t s);
+                     double2* out, hipStream_t s, const int* done = nullptr);
+void grid_crop(int dtype, const double2* Z, const GridDims& gd, int64_t outM, void* y, hipStream_t s,
+               const int* done = nullptr);
 void scale_copy(const double2* a, double2* b, int64_t n, double sc, hipStream_t s,
                 const unsigned long long* mx = nullptr);   // mx: the imaginary part also / pack_scale
 // long-axis DCT line batches (hgp_grad.hip)

@@ -198,7 +198,9 @@ __global__ void k_embed_R(const double* __restrict__ s, double2* __restrict__ ou
 // (e = 0, 1 at offsets e * ps, positions at 2 ps) hold their length-L/2 spectra in pass order;
 // X[f] = E[f'] +- W_L^f' O[f'] (f' = f mod L/2), written in the pass order of length L.
 __global__ void k_r2_combine(const double2* __restrict__ in, double2* __restrict__ out, int64_t L, int64_t Rn,
-                             int64_t r_stride, int64_t In, int64_t ps, const double2* __restrict__ tw) {
+                             int64_t r_stride, int64_t In, int64_t ps, const double2* __restrict__ tw,
+                             const int* done) {
+  if (done != nullptr && *done) return;
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t half_len = L / 2, Hp = L / 4;
   if (t >= Rn * In * half_len) return;
@@ -216,10 +218,10 @@ __global__ void k_r2_combine(const double2* __restrict__ in, double2* __restrict
   out[base + (oa + half_len / 2) * ps] = make_double2(E.x - wo.x, E.y - wo.y);
 }
 void r2_combine(const double2* in, double2* out, int64_t L, int64_t Rn, int64_t r_stride, int64_t In, int64_t ps,
-                const double2* tw, hipStream_t s) {
+                const double2* tw, hipStream_t s, const int* done) {
   const int64_t total = Rn * In * (L / 2);
   hipLaunchKernelGGL(k_r2_combine, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, in, out, L, Rn, r_stride, In,
-                     ps, tw);
+                     ps, tw, done);
 }
 
 // the same R filter as a REAL grid (the set-up transforms it with the real row-pair pass)

@@ -42,6 +42,15 @@
 //                 NL = Rn Q.  _C: position-fast lines (d = 2, inner = 1); _S: C adjacent c lines
 //                 per block as LAY_STRIDED (d = 3, In lines, inner = in.p_stride).  Input split
 //                 over in.len rows, output split over out.len rows.
+//   LAY_CONTIG_Q: the grouped intermediate of G = 4 columns in the "quad" order (hgp_rows.hpp
+//                 wg_off<4>): within a group's 128-B unit of 4 positions x 4 columns the columns
+//                 go in two 64-B halves of 2 columns, each half 4 positions x 2 columns, element
+//                 (c, p) at (c / 4) 4 S0 + (p / 4) 16 + ((c / 2) % 2) 8 + (p % 4) 2 + c % 2.  A block
+//                 holds the 2 columns of one half (C = 2 lines, position-fast), so its two lines'
+//                 stores of the same position fill whole 16-B pairs and every 64-B half of a line
+//                 comes from one block at one time (no partially written 32-B sectors, which the
+//                 plain G = 4 order with one column per block left to four blocks, C4 K op conv
+//                 writes 1.54x their bytes, profiles/r4_C4K_kernel_bytes_final.txt).
 //   LAY_GRP2 / LAY_GRP4: the grouped-column intermediate as LAY_CONTIG_G, but a block holds the
 //                 G = 2 / 4 columns of one group of one RHS with threads column-fast (the strided
 //                 mapping, C = G): every load / store instruction of a wave covers one contiguous
@@ -111,12 +120,23 @@
 #ifndef HGP_MINW_CONTIG_TRI
 #define HGP_MINW_CONTIG_TRI HGP_MINW_CONTIG_LONG
 #endif
+// the G = 4 grouped intermediate in the quad order (LAY_CONTIG_Q; 0: the plain G = 4 order,
+// one column per axis-0 block, LAY_CONTIG_G)
+#ifndef HGP_QUAD
+#define HGP_QUAD 1
+#endif
+// the quad-order (LAY_CONTIG_Q) column pass of 4096-point lines: two 8-wave blocks per CU
+#ifndef HGP_MINW_CONTIG_Q4096
+#define HGP_MINW_CONTIG_Q4096 4
+#endif
 
 namespace hgp {
 
 enum { PASS_FWD = 0, PASS_INV = 1, PASS_CONV = 2, PASS_CONVC = 3 };   // CONV: real spectrum, CONVC: complex
 enum { LAY_STRIDED = 0, LAY_CONTIG = 1, LAY_RP = 2, LAY_R1 = 3, LAY_CONTIG_G = 4, LAY_SEG_C = 5, LAY_SEG_S = 6,
-       LAY_GRP2 = 7, LAY_GRP4 = 8 };
+       LAY_GRP2 = 7, LAY_GRP4 = 8, LAY_CONTIG_Q = 9 };
+// element offset of position p within its line in the quad order (LAY_CONTIG_Q, wg_off<4>)
+__host__ __device__ constexpr int quad_pos(int p) { return ((p >> 2) << 4) + ((p & 3) << 1); }
 // columns per block of the interleaved grouped layouts (0: not one)
 constexpr int lay_grp(int lay) { return lay == LAY_GRP2 ? 2 : lay == LAY_GRP4 ? 4 : 0; }
 // strided thread mapping (C adjacent lines, threads line-fast) vs position-fast lines
@@ -194,7 +214,7 @@ template <typename T, int H, int LAY> struct PassCfg {
     while (c > 1 && (c * TT > 1024 || lds_bytes_for(c) > LDS_CAP)) c >>= 1;
     return c;
   }
-  static constexpr int ROWT = (LAY == LAY_CONTIG || LAY == LAY_CONTIG_G || LAY == LAY_SEG_C)
+  static constexpr int ROWT = (LAY == LAY_CONTIG || LAY == LAY_CONTIG_G || LAY == LAY_CONTIG_Q || LAY == LAY_SEG_C)
                                   ? (TT >= 128 ? HGP_CONTIG_THREADS_LONG : H <= 512 ? HGP_CONTIG_THREADS_SHORT : HGP_CONTIG_THREADS)
                                   : HGP_ROW_THREADS;
   static constexpr int c_contig() {
@@ -202,7 +222,13 @@ template <typename T, int H, int LAY> struct PassCfg {
     while (c > 1 && (c * TT > 1024 || lds_bytes_for(c) > LDS_CAP / 2)) c >>= 1;
     return c;
   }
-  static constexpr int C = lay_grp(LAY) ? lay_grp(LAY) : lay_smap(LAY) ? c_strided() : c_contig();
+  // quad order: at least the 2 lines of a 64-B half per block where a block can hold them
+  static constexpr int c_quad() {
+    const int c = c_contig();
+    return c >= 2 ? c : ((2 * TT <= 1024 && lds_bytes_for(2) <= LDS_CAP) ? 2 : 1);
+  }
+  static constexpr int C = lay_grp(LAY) ? lay_grp(LAY) : lay_smap(LAY) ? c_strided()
+                           : LAY == LAY_CONTIG_Q ? c_quad() : c_contig();
   // position-fast layouts keep each line inside one wavefront when TT <= 64: exchanges then
   // need no block barrier (hgp_fft.hpp xsync)
   static constexpr bool WAVE = !lay_smap(LAY) && TT <= 64;
@@ -220,8 +246,11 @@ template <typename T, int H, int LAY> struct PassCfg {
                                  : H >= 2048 ? HGP_MINW_CONTIG_LONG : H <= 512 ? HGP_MINW_CONTIG_SHORT : HGP_MINW_CONTIG;
   // a block's waves must fit the SIMDs' share at once: >= WAVES_PER_BLOCK / 4 waves per SIMD
   static constexpr int MINW_BLK = (WAVES_PER_BLOCK + 3) / 4;
+  // quad-order blocks of two 4-wave lines: 4 waves per SIMD, two blocks per CU
+  static constexpr int MINW_Q = (C == 2 && TT == 256) ? HGP_MINW_CONTIG_Q4096 : MINW_CL;
   static constexpr int MINW_SET = lay_grp(LAY) ? (MINW_CL > MINW_BLK ? MINW_CL : MINW_BLK)
                                  : lay_smap(LAY) ? (TT >= 16 ? HGP_MINW_STRIDED : HGP_MINW_STRIDED_SMALL)
+                                 : LAY == LAY_CONTIG_Q ? (MINW_Q > MINW_BLK ? MINW_Q : MINW_BLK)
                                  : (LAY == LAY_CONTIG || LAY == LAY_CONTIG_G || LAY == LAY_SEG_C) ? MINW_CL
                                                                                                   : HGP_MINW_ROW;
   static constexpr int MINW = MINW_SET > 0 ? MINW_SET : MINW_AUTO;
@@ -341,10 +370,11 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
     i = i0 + l;
     valid = i < d.In;               // (q, r, i0) of a launched block are always in range
     lc = valid ? l : 0;             // keep every (unconditional) load in bounds
-  } else if constexpr (LAY == LAY_CONTIG_G) {
+  } else if constexpr (LAY == LAY_CONTIG_G || LAY == LAY_CONTIG_Q) {
     // lines (cg, q, cl), cl fastest: a block's C lines are the G columns of one group (x C / G
-    // RHS); the XCD remap keeps consecutive groups on one XCD
-    const int G = d.grp;
+    // RHS), or (quad, C = 2) one 64-B half of them; the XCD remap keeps consecutive groups on one
+    // XCD (the two halves of a quad group: consecutive logical blocks)
+    const int G = LAY == LAY_CONTIG_Q ? 4 : d.grp;
     const int64_t line = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * C + l;
     const int64_t rest = line / G;
     const int cl = (int)(line - rest * G);
@@ -354,7 +384,8 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
     i = 0;
     valid = r < d.Rn;
     if (!valid) { q = 0; r = 0; }
-    gbase = (int64_t)(r / G) * d.in.r_stride * G + (r % G);
+    if constexpr (LAY == LAY_CONTIG_Q) gbase = (int64_t)(r >> 2) * d.in.r_stride * 4 + ((r >> 1) & 1) * 8 + (r & 1);
+    else gbase = (int64_t)(r / G) * d.in.r_stride * G + (r % G);
   } else if constexpr (LAY == LAY_CONTIG || LAY == LAY_SEG_C) {
     // RHS-fastest: the C lines of a block are the same column r of C right-hand sides, so
     // they share one spectrum line; the XCD remap keeps the blocks of one column (all its
@@ -390,7 +421,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
     in_c = reinterpret_cast<const C2<T>*>(d.in.ptr);   // positions by seg_off (the rank blocks)
   } else if constexpr (LAY == LAY_STRIDED) {
     in_c = reinterpret_cast<const C2<T>*>(d.in.ptr) + (int64_t)q * d.in.q_stride + (int64_t)r * d.in.r_stride + i0;
-  } else if constexpr (LAY == LAY_CONTIG_G || GRP) {
+  } else if constexpr (LAY == LAY_CONTIG_G || LAY == LAY_CONTIG_Q || GRP) {
     in_c = reinterpret_cast<const C2<T>*>(d.in.ptr) + (int64_t)q * d.in.q_stride + gbase;
   } else {
     in_c = reinterpret_cast<const C2<T>*>(d.in.ptr) + (int64_t)q * d.in.q_stride + (int64_t)r * d.in.r_stride;
@@ -409,7 +440,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
     out_c = reinterpret_cast<C2<T>*>(d.out.ptr);
   } else if constexpr (LAY == LAY_STRIDED) {
     out_c = reinterpret_cast<C2<T>*>(d.out.ptr) + (int64_t)q * d.out.q_stride + (int64_t)r * d.out.r_stride + i0;
-  } else if constexpr (LAY == LAY_CONTIG_G || GRP) {
+  } else if constexpr (LAY == LAY_CONTIG_G || LAY == LAY_CONTIG_Q || GRP) {
     out_c = reinterpret_cast<C2<T>*>(d.out.ptr) + (int64_t)q * d.out.q_stride + gbase;
   } else {
     out_c = reinterpret_cast<C2<T>*>(d.out.ptr) + (int64_t)q * d.out.q_stride + (int64_t)r * d.out.r_stride;
@@ -433,10 +464,12 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
   using Off = std::conditional_t<SEG, int64_t, int>;   // 32-bit lane offsets on the fast layouts
   auto in_at = [&](int p) -> Off {
     if constexpr (SEG) return seg_off(p, d.in.len);
+    else if constexpr (LAY == LAY_CONTIG_Q) return quad_pos(p);
     else return (LAY == LAY_STRIDED || GRP) ? lc + p * ips : (LAY == LAY_CONTIG_G) ? p * ips : p;
   };
   auto out_at = [&](int p) -> Off {
     if constexpr (SEG) return seg_off(p, d.out.len);
+    else if constexpr (LAY == LAY_CONTIG_Q) return quad_pos(p);
     else return (LAY == LAY_STRIDED || GRP) ? lc + p * ops : (LAY == LAY_CONTIG_G) ? p * ops : p;
   };
 
@@ -505,15 +538,21 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
 #ifndef HGP_BUF_F64
 #define HGP_BUF_F64 1
 #endif
-  constexpr bool CONTIG = (LAY == LAY_CONTIG || LAY == LAY_CONTIG_G);
+  constexpr bool QUAD = LAY == LAY_CONTIG_Q;
+  constexpr bool CONTIG = (LAY == LAY_CONTIG || LAY == LAY_CONTIG_G || QUAD);
   constexpr bool BUF = (std::is_same<T, float>::value || HGP_BUF_F64) && CONTIG && (TT % 64 == 0);
   // element stride of a line's positions: 1, or G in the grouped layout; the range then ends
-  // one element past the line's last valid position ((len - 1) G + 1 elements)
-  const uint32_t es = (uint32_t)ips * (uint32_t)sizeof(C2<T>);
-  const BufRsrc rin = buf_rsrc(BUF ? (const void*)in_c : nullptr,
-                               (BUF && valid && d.in.len > 0) ? ((uint32_t)(d.in.len - 1) * (uint32_t)ips + 1u) * (uint32_t)sizeof(C2<T>) : 0u);
-  const BufRsrc rout = buf_rsrc(BUF ? (const void*)out_c : nullptr,
-                                (BUF && valid && d.out.len > 0) ? ((uint32_t)(d.out.len - 1) * (uint32_t)ops + 1u) * (uint32_t)sizeof(C2<T>) : 0u);
+  // one element past the line's last valid position ((len - 1) G + 1 elements).  Quad order:
+  // the offset of p = t + x (x a multiple of 4: TT k, H) splits into the lane's quad_pos(t) and
+  // 4 x elements; it grows with p, so the range still crops at quad_pos(len - 1) + 1
+  const uint32_t es = (uint32_t)(QUAD ? 4 : ips) * (uint32_t)sizeof(C2<T>);
+  const uint32_t lane_b = QUAD ? (uint32_t)quad_pos(t) * (uint32_t)sizeof(C2<T>) : (uint32_t)t * es;
+  auto range_b = [&](int len, int st) -> uint32_t {
+    if (QUAD) return ((uint32_t)quad_pos(len - 1) + 1u) * (uint32_t)sizeof(C2<T>);
+    return ((uint32_t)(len - 1) * (uint32_t)st + 1u) * (uint32_t)sizeof(C2<T>);
+  };
+  const BufRsrc rin = buf_rsrc(BUF ? (const void*)in_c : nullptr, (BUF && valid && d.in.len > 0) ? range_b(d.in.len, ips) : 0u);
+  const BufRsrc rout = buf_rsrc(BUF ? (const void*)out_c : nullptr, (BUF && valid && d.out.len > 0) ? range_b(d.out.len, ops) : 0u);
   if constexpr (MODE == PASS_FWD || CONV) {
     const int in_len = d.in.len;
     const int lim = in_len - 1;
@@ -525,14 +564,14 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
         const int p = t + TT * k;
         C2<T> a;
         if constexpr (BUF) {
-          a = buf_ld_c2<T>(rin, (uint32_t)t * es, (uint32_t)(TT * k) * es);
+          a = buf_ld_c2<T>(rin, lane_b, (uint32_t)(TT * k) * es);
         } else {
           a = load_in(p < in_len ? p : lim);
           if (p >= in_len) a = mk<T>(0, 0);
         }
         C2<T> c = mk<T>(0, 0);
         if constexpr (FOLD) {       // beyond in_len the buffer range returns 0
-          if constexpr (BUF) c = buf_ld_c2<T>(rin, (uint32_t)t * es, (uint32_t)(TT * k + H) * es);
+          if constexpr (BUF) c = buf_ld_c2<T>(rin, lane_b, (uint32_t)(TT * k + H) * es);
           else c = load_hi(p);
         }
         va[k] = cadd<T>(a, c);
@@ -676,7 +715,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
               }
             }
           } else if constexpr (BUF) {
-            buf_st_c2<T>(y, rout, (uint32_t)t * es, (uint32_t)(pp - t) * es);
+            buf_st_c2<T>(y, rout, lane_b, (uint32_t)(pp - t) * es);
           } else {
             out_c[out_at(pp)] = y;
           }

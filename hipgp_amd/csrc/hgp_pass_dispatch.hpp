@@ -52,8 +52,10 @@ static hipError_t launch_h(int mode, int lay, const PassDesc& d, int64_t nblocks
     if (lay == LAY_CONTIG) return launch_one<T, H, PASS_CONV, LAY_CONTIG>(d, nblocks, s);
     if (lay == LAY_R1) return launch_one<T, H, PASS_CONV, LAY_R1>(d, nblocks, s);
     // the grouped-column intermediate of long fp32 rows (hgp_rows.hpp RowTCfg::G); any axis-0 H
-    if constexpr (std::is_same<T, float>::value)
+    if constexpr (std::is_same<T, float>::value) {
       if (lay == LAY_CONTIG_G) return launch_one<T, H, PASS_CONV, LAY_CONTIG_G>(d, nblocks, s);
+      if (lay == LAY_CONTIG_Q) return launch_one<T, H, PASS_CONV, LAY_CONTIG_Q>(d, nblocks, s);
+    }
     if (lay == LAY_SEG_C) return launch_one<T, H, PASS_CONV, LAY_SEG_C>(d, nblocks, s);
     if (lay == LAY_SEG_S) return launch_one<T, H, PASS_CONV, LAY_SEG_S>(d, nblocks, s);
     if (lay_grp(lay)) return launch_grp<T, H, PASS_CONV>(lay, d, nblocks, s);
@@ -61,8 +63,10 @@ static hipError_t launch_h(int mode, int lay, const PassDesc& d, int64_t nblocks
     if (lay == LAY_STRIDED) return launch_one<T, H, PASS_CONVC, LAY_STRIDED>(d, nblocks, s);
     if (lay == LAY_CONTIG) return launch_one<T, H, PASS_CONVC, LAY_CONTIG>(d, nblocks, s);
     if (lay == LAY_R1) return launch_one<T, H, PASS_CONVC, LAY_R1>(d, nblocks, s);
-    if constexpr (std::is_same<T, float>::value)
+    if constexpr (std::is_same<T, float>::value) {
       if (lay == LAY_CONTIG_G) return launch_one<T, H, PASS_CONVC, LAY_CONTIG_G>(d, nblocks, s);
+      if (lay == LAY_CONTIG_Q) return launch_one<T, H, PASS_CONVC, LAY_CONTIG_Q>(d, nblocks, s);
+    }
     if (lay == LAY_SEG_C) return launch_one<T, H, PASS_CONVC, LAY_SEG_C>(d, nblocks, s);
     if (lay == LAY_SEG_S) return launch_one<T, H, PASS_CONVC, LAY_SEG_S>(d, nblocks, s);
     if (lay_grp(lay)) return launch_grp<T, H, PASS_CONVC>(lay, d, nblocks, s);
@@ -82,6 +86,7 @@ static PassGeom geom_h(int lay) {
   if (lay == LAY_SEG_S) return geom_one<T, H, LAY_SEG_S>();
   if (lay == LAY_CONTIG) return geom_one<T, H, LAY_CONTIG>();
   if (lay == LAY_CONTIG_G) return geom_one<T, H, LAY_CONTIG_G>();
+  if (lay == LAY_CONTIG_Q) return geom_one<T, H, LAY_CONTIG_Q>();
   if (lay == LAY_SEG_C) return geom_one<T, H, LAY_SEG_C>();
   if (lay == LAY_RP) return geom_one<T, H, LAY_RP>();
   if (lay == LAY_GRP2) return grp_ok<T, H, LAY_GRP2>() ? geom_one<T, H, LAY_GRP2>() : PassGeom{0, 0, 0};

@@ -137,10 +137,16 @@ template <typename T, int H, int G = 1> struct RowTCfg {
   static constexpr int ITER = (MAXGRP * SEG + THREADS - 1) / THREADS;
 };
 
-// element offset of compact column c, row i0 of one RHS's intermediate (column pitch S0)
+// element offset of compact column c, row i0 of one RHS's intermediate (column pitch S0).
+// G = 4 is the "quad" order (hgp_pass.hpp LAY_CONTIG_Q): a group's 128-B unit of 4 rows x 4
+// columns holds two 64-B halves of 2 columns x 4 rows, (row, column) column-fastest in each, so
+// that the axis-0 pass's 2-line blocks write whole halves; the row passes move whole units either
+// way (S0 is a multiple of 16, a block's first row a multiple of 4)
 template <int G>
 __device__ __forceinline__ uint32_t wg_off(int c, int i0, int64_t S0) {
   if constexpr (G == 1) return (uint32_t)c * (uint32_t)S0 + (uint32_t)i0;
+  if constexpr (G == 4 && HGP_QUAD)
+    return (uint32_t)(c >> 2) * (uint32_t)S0 * 4u + (uint32_t)quad_pos(i0) + (uint32_t)((c >> 1) & 1) * 8u + (uint32_t)(c & 1);
   return ((uint32_t)(c / G) * (uint32_t)S0 + (uint32_t)i0) * (uint32_t)G + (uint32_t)(c % G);
 }
 

@@ -162,11 +162,34 @@ class SlabToeplitz:
         return v[:, a * rest:b * rest].contiguous()
 
     # -- the operator ---------------------------------------------------------------------
+    def _check(self, t, name, grid, nrhs=None):
+        """t must be this rank's contiguous slab (nrhs, local size of `grid`) in the engine's dtype
+        on its device: the engine hands raw pointers to the library, which dispatches on the
+        plan's dtype and trusts the sizes."""
+        if not isinstance(t, torch.Tensor):
+            raise TypeError(f"{name} must be a tensor")
+        if t.dtype != self.engine.dtype:
+            raise TypeError(f"{name} has dtype {t.dtype}, the slab plan is {self.engine.dtype}")
+        dev = getattr(self.engine, "device", None)
+        if dev is not None and t.device != torch.device(dev):
+            raise ValueError(f"{name} is on {t.device}, the slab plan on {dev}")
+        size = self.local_size(grid)
+        if t.dim() != 2 or t.shape[1] != size or (nrhs is not None and t.shape[0] != nrhs):
+            want = f"({'nrhs' if nrhs is None else nrhs}, {size})"
+            raise ValueError(f"{name} must be this rank's slab {want}, got {tuple(t.shape)}")
+        if not t.is_contiguous():
+            raise ValueError(f"{name} must be contiguous")
+        return t
+
     def _bufs(self, op, nrhs, dtype, dev):
         """The exchange / all-to-all buffers of (op, nrhs), allocated once and re-used by every
-        apply -- a PCG iteration allocates nothing."""
-        key = (int(op), int(nrhs))
+        apply -- a PCG iteration allocates nothing.  One set per op (the latest nrhs): a caller
+        whose batch size varies re-allocates instead of keeping one set per size alive."""
+        key = int(op)
         b = self._buf.get(key)
+        if b is not None and b["nrhs"] != int(nrhs):
+            del self._buf[key]
+            b = None
         if b is None:
             ws, rk = self.ws, self.rank
             rows_in = self.rows_n if op == _lib.OP_R else self.rows_m
@@ -187,7 +210,7 @@ class SlabToeplitz:
             sizes_rx = [ng * nrhs * (rows_in[r][1] - rows_in[r][0]) * inner for r in range(ws)]
             sizes_tx = [ng * nrhs * (rows_out[r][1] - rows_out[r][0]) * inner for r in range(ws)]
             sizes_back = [(groups[s][1] - groups[s][0]) * nrhs * no * inner for s in range(ws)]
-            b = dict(NG=NG, inner=inner, gs0=gs0, ng=ng, ni=ni, no=no, sizes_in=sizes_in, sizes_rx=sizes_rx,
+            b = dict(nrhs=int(nrhs), NG=NG, inner=inner, gs0=gs0, ng=ng, ni=ni, no=no, sizes_in=sizes_in, sizes_rx=sizes_rx,
                      sizes_tx=sizes_tx, sizes_back=sizes_back,
                      E=torch.empty((NG, nrhs, ni, inner), dtype=cd, device=dev),
                      recv=torch.empty(sum(sizes_rx), dtype=cd, device=dev),
@@ -206,7 +229,15 @@ class SlabToeplitz:
         sum(out * dotv) (fused into the last stage); done: a device flag after which every
         stage is a no-op (the slab PCG's masked iterations)."""
         e = self.engine
+        x = self._check(x.contiguous(), "x", "n" if op == _lib.OP_R else "m")
         nrhs = x.shape[0]
+        if out is not None:
+            self._check(out, "out", "n" if op == _lib.OP_RT else "m", nrhs)
+        if dotv is not None:
+            self._check(dotv, "dotv", "n" if op == _lib.OP_RT else "m", nrhs)
+        if dot_out is not None and (dot_out.dtype != x.dtype or dot_out.numel() != nrhs
+                                    or not dot_out.is_contiguous() or dot_out.device != x.device):
+            raise ValueError(f"dot_out must be a contiguous ({nrhs},) {x.dtype} vector on {x.device}")
         b = self._bufs(op, nrhs, x.dtype, x.device)
         rest_out = self.rest_n if op == _lib.OP_RT else self.rest_m
         E, recv, send, back = b["E"], b["recv"], b["send"], b["back"]
@@ -253,8 +284,8 @@ class SlabToeplitz:
         before the loop.  With a callback (`cg.py:77-78`, after every iteration that did not
         break) the host must look at the flag, so that form synchronises per iteration."""
         e = self.engine
+        b = self._check(b.contiguous(), "b", "m")
         nrhs = b.shape[0]
-        b = b.contiguous()
         x = torch.zeros_like(b)
         r = b.clone()
         z = torch.empty_like(b) if precond else r
@@ -301,3 +332,82 @@ def slab_toeplitz(dims, column, dtype=torch.float32, device=None, group=None, ji
     plan = ToeplitzPlan(dims, dtype=dtype, device=device)
     plan.set_column(column, jitter=jitter, clamp_min=clamp_min)
     return SlabToeplitz(dims, HipSlabEngine(plan), group=group)
+
+
+def _all_gather_cols(local, group):
+    """Concatenate the ranks' column blocks (nrhs, n_r) -> (nrhs, sum n_r) in rank order (the
+    slabs' axis-0 row blocks are contiguous column ranges of the flattened grid).  Blocks may
+    differ in width (balanced splits): each is padded to the widest, gathered, trimmed."""
+    ws = dist.get_world_size(group)
+    widths = torch.tensor([local.shape[1]], dtype=torch.int64)
+    wl = [torch.zeros(1, dtype=torch.int64) for _ in range(ws)]
+    if dist.get_backend(group) == "gloo":
+        dist.all_gather(wl, widths, group=group)
+    else:
+        wd = widths.to(local.device)
+        wg = [torch.zeros(1, dtype=torch.int64, device=local.device) for _ in range(ws)]
+        dist.all_gather(wg, wd, group=group)
+        wl = [w.cpu() for w in wg]
+    wmax = max(int(w) for w in wl)
+    pad = local.new_zeros((local.shape[0], wmax))
+    pad[:, :local.shape[1]] = local
+    gloo = dist.get_backend(group) == "gloo" and pad.is_cuda
+    src = pad.cpu() if gloo else pad
+    parts = [torch.empty_like(src) for _ in range(ws)]
+    dist.all_gather(parts, src, group=group)
+    full = torch.cat([p[:, :int(w)] for p, w in zip(parts, wl)], dim=1)
+    return full.to(local.device) if gloo else full
+
+
+class SlabKmm:
+    """Grid-block sharding behind the reference's duck-typed `Kmm` (`hipgp.py:117-146`:
+    `compute_kn(Knm, maxiter_cg, tol, Kmm=...)` needs `.inv_matmul(R, do_precond, maxiter, tol)`
+    and `._matmul_by_RT(d)`), so an unchanged model can run its solve grid-block sharded
+    (BASELINE config 5: "grid-block shard").
+
+    Every rank of `group` passes the SAME full minibatch rows: `inv_matmul` takes the rank's
+    axis-0 slab of R (B, M), runs the slab PCG (`SlabToeplitz.pcg`: all-reduced per-RHS dots,
+    the all-rank break rule) and all-gathers the solution to (B, M) like ToeplitzTensor's;
+    `_matmul_by_RT` applies R^T on the slabs (all-to-all transposes) and all-gathers the
+    expanded-grid rows, so the caller gets the full (B, M') kn.  Forward only: the solve is not
+    differentiable here (kernel-hyperparameter learning goes through the RHS-sharded
+    `hipgp_amd.dist` path)."""
+
+    def __init__(self, slab, column=None):
+        self.slab = slab
+        self.column = column
+        self.dims = slab.dims
+        self.ndim = len(slab.dims)
+        self.M = int(slab.rest_m * slab.dims[0])
+
+    @classmethod
+    def from_model(cls, model, group=None):
+        """The grid-block Kmm of a Toeplitz model's current kernel parameters: every rank sets
+        the spectrum of the whole grid (replicated, as `model.toeplitz()` would) and owns its
+        axis-0 slab of every vector."""
+        T = model.toeplitz()
+        return cls(SlabToeplitz(T.dims, HipSlabEngine(T._plan), group=group), column=T.column)
+
+    def set_batch_shape(self, batch_shape):
+        self.batch_shape = tuple(batch_shape)
+
+    def _check_grad(self, t):
+        if torch.is_grad_enabled() and t.requires_grad:
+            raise NotImplementedError("SlabKmm is forward-only: differentiate through the RHS-sharded path "
+                                      "(hipgp_amd.dist.sharded_compute_kn) instead")
+
+    def inv_matmul(self, right_tensor, do_precond=True, maxiter=20, tol=1e-8):
+        """K^-1 R for the full rows R (B, M) (`toeplitz_tensor.py:47-52`), solved on the slabs."""
+        self._check_grad(right_tensor)
+        with torch.no_grad():
+            x, _ = self.slab.pcg(self.slab.scatter_rows(right_tensor.contiguous(), "m"), maxiter, tol,
+                                 precond=do_precond)
+            return _all_gather_cols(x, self.slab.group)
+
+    def _matmul_by_RT(self, vec):
+        """R^T d for the full rows d (B, M) -> the full expanded-grid rows (B, M')
+        (`toeplitz_tensor.py:85-97`)."""
+        self._check_grad(vec)
+        with torch.no_grad():
+            y = self.slab.apply(_lib.OP_RT, self.slab.scatter_rows(vec.contiguous(), "m"))
+            return _all_gather_cols(y, self.slab.group)

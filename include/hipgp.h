@@ -42,9 +42,12 @@ enum {
 /* Plan for one gridded inducing mesh m[0..ndim-1] (ndim 1..3, C order, last axis fastest).
  * Replaces the shape/state part of `ToeplitzTensor.__init__` (toeplitz_tensor.py:9-45) and
  * `ToeplitzMatmul.__init__` (toeplitz_expanded.py:82-127).  `hip_stream` may be NULL (null
- * stream).  max_rhs is a capacity hint; workspaces grow on demand.  Axes of up to 8192 points
- * (fp32 and fp64); longer ones give HGP_E_UNSUPPORTED.  fp64 plans whose R / R^T lines exceed
- * 16384 points (axes of 5463..8192) run those two ops on the full fp64 L_R grid (no slab split). */
+ * stream).  max_rhs is a capacity hint; workspaces grow on demand.  Any axis length (fp32 and
+ * fp64 plans): axes of up to 8192 points run the pruned per-axis passes; fp64 plans whose R / R^T
+ * lines exceed 16384 points (axes of 5463..8192) run those two ops on the full fp64 L_R grid, and
+ * a plan with an axis beyond 8192 points runs all four operators on the full fp64 L_K / L_R grid
+ * (recursive radix-2 levels down to an 8192-point base pass; unfused PCG, no slab split).  One
+ * right-hand side's intermediate must stay below 2^31 values, else HGP_E_UNSUPPORTED. */
 int hgp_plan_create(int device, int ndim, const int64_t* m, int dtype, int64_t max_rhs,
                     void* hip_stream, hgp_plan** out);
 

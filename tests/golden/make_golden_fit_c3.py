@@ -73,7 +73,9 @@ def data(case):
     return x, y, s
 
 
-def gen_case(zk, hg, dtype, case):
+def gen_case(zk, hg, dtype, case, perturb=None):
+    """perturb: optional callable on the fresh model (before the fit) -- the self-perturbed
+    re-runs of make_golden_fit_c3_alt.py; the recorded *_init parameters are the unperturbed ones"""
     import ziggy.svi_gp  # noqa: F401  (the reference's module, imported by ziggy.hipgp)
     torch.manual_seed(19)
     (x0, x1), (y0, y1) = BOXES[case]
@@ -86,6 +88,8 @@ def gen_case(zk, hg, dtype, case):
     out = {"grid0": _np(xgrids[0]), "grid1": _np(xgrids[1]), "x": x, "y": y, "s": s,
            "sig2_init": np.array(sig2),
            "theta1_init": _np(mod.global_theta1).copy(), "theta2_init": _np(mod.global_theta2).copy()}
+    if perturb is not None:
+        perturb(mod)
     snaps = []
 
     def batch_cb(m, xb, yb, sb):

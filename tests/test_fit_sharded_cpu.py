@@ -1,0 +1,115 @@
+"""`svigp_fit` sharded over ranks (the multi-GPU fit through the unchanged `ziggy` API,
+hipgp_amd/ziggy/svi_gp.py): gloo world size 2 on the CPU against the same fit in one process,
+on config 3's settings (G19 "box": the reference's own `svigp_fit` trajectory, 64 x 64 grid,
+20 minibatches of 200).  The solve is injected (`compute_kn` fit option) as the NumPy oracle
+(TEST INFRASTRUCTURE: `oracle/ziggy_oracle.py`; the device solve is covered by the GPU tests), so
+this checks the host logic of the sharded loop: the row split of every minibatch, the all-reduced
+natural-gradient sums, identical optimiser steps -- every rank ends with bit-identical
+parameters, equal to the single-process fit's to reduction-order rounding (fp64 1e-10)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from golden_cases import load
+
+
+def _converged_at(T, b, maxiter, tol):
+    """The all-RHS break predicate of `cg.py:69-71` after each iteration n < maxiter, for this
+    rank's rows (the oracle's recurrence, no break)"""
+    x, r = np.zeros_like(b), b.copy()
+    z = T.matmul_Cinv(r)
+    p = z
+    out = []
+    for n in range(maxiter):
+        rs = np.sum(r * z, axis=1)
+        Ap = T.matmul_K(p)
+        alpha = rs / np.sum(p * Ap, axis=1)
+        r = r - alpha[:, None] * Ap
+        out.append(bool(np.all(np.sqrt(np.sum(r * r, axis=1)) < tol)))
+        z = T.matmul_Cinv(r)
+        p = z + (np.sum(z * r, axis=1) / rs)[:, None] * p
+    return out
+
+
+def _oracle_kn(model, Knm, maxiter=20, tol=1e-8):
+    """kn of this rank's rows by the oracle, with the reference's all-RHS break decided over
+    EVERY rank's rows (what the device path does with hgp_pcg_local_flag + an all-reduce): the
+    per-iteration predicates are MIN-reduced, and the solve stops at the first iteration where
+    every rank's rows have converged"""
+    import torch.distributed as dist
+    from oracle import ziggy_oracle as zo
+    grids = [g.cpu().numpy() for g in model.xgrids]
+    params = [float(p) for p in model.get_kernel_params()]
+    col = zo.toeplitz_column(grids, lambda x, y: zo.kernel_eval("matern", x, y, params, nu=1.5), model.jitter_val)
+    T = zo.ToeplitzOracle(col, [len(g) for g in grids])
+    b = Knm.detach().numpy()
+    pred = torch.tensor(_converged_at(T, b, maxiter, tol) if b.shape[0] else [True] * maxiter, dtype=torch.int32)
+    dist.all_reduce(pred, op=dist.ReduceOp.MIN)
+    stop = next((n + 1 for n in range(maxiter) if int(pred[n])), maxiter)
+    if b.shape[0] == 0:
+        return Knm.new_zeros((0, model.Mprime))
+    return torch.tensor(zo.compute_kn(T, b, maxiter_cg=stop, tol=-1.0))
+
+
+def _fit(world_size, rank, nbatch=3):
+    import ziggy.hipgp as hg
+    import ziggy.kernels as zk
+    fx = load("G19", "f64")
+    dt = torch.float64
+    grids = [torch.tensor(fx["box_grid0"], dtype=dt), torch.tensor(fx["box_grid1"], dtype=dt)]
+    mod = hg.MeanFieldToeplitzGP(zk.Matern(nu=1.5, dtype=dt), grids, num_obs=100_000,
+                                 sig2_init=float(fx["box_sig2_init"]), ell_init=.1, init_Svar=.1,
+                                 learn_kernel=False, jitter_val=1e-3, dtype=dt)
+    with torch.no_grad():
+        mod.global_theta1.copy_(torch.tensor(fx["box_theta1_init"], dtype=dt))
+        mod.global_theta2.copy_(torch.tensor(fx["box_theta2_init"], dtype=dt))
+    snaps = []
+    cb = lambda m, xb, yb, sb: snaps.append(m.global_theta1.detach().numpy().copy())
+    x, y, s = (fx[f"box_{k}"][:200 * nbatch] for k in "xys")
+    mod.fit(None, x, y, s, None, None, None, None, None, None, batch_callback=cb, epoch_callback=None,
+            do_cuda=False, lr=1e-2, schedule_lr=False, batch_size=200, epochs=1, maxiter_cg=20,
+            batch_log_interval=1, learn_kernel=False, distributed=True, compute_kn=_oracle_kn)
+    cb(mod, None, None, None)
+    return np.stack(snaps), mod.global_theta2.detach().numpy().copy(), list(mod.fit_trace)
+
+
+def _worker(rank, world_size, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world_size)
+    try:
+        torch.set_num_threads(2)
+        out[rank] = _fit(world_size, rank)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_fit_gloo_matches_single_process():
+    mgr = mp.Manager()
+    res = {}
+    for ws in (1, 2):
+        out = mgr.dict()
+        port = 29800 + os.getpid() % 100 + ws
+        mp.spawn(_worker, args=(ws, port, out), nprocs=ws, join=True)
+        assert len(out) == ws
+        res[ws] = [out[r] for r in range(ws)]
+    (t1_single, t2_single, tr_single), = res[1]
+    for r, (t1, t2, tr) in enumerate(res[2]):
+        # every rank: bit-identical to rank 0
+        assert np.array_equal(t1, res[2][0][0]) and np.array_equal(t2, res[2][0][1]), r
+        rel = np.linalg.norm(t1 - t1_single, axis=1) / np.linalg.norm(t1_single, axis=1)
+        assert float(rel.max()) < 1e-10, rel
+        assert np.linalg.norm(t2 - t2_single) < 1e-10 * np.linalg.norm(t2_single)
+        assert np.allclose(tr, tr_single, rtol=1e-10, atol=0)
+    # and the single-process oracle fit follows the reference's own trajectory (G19 "box"):
+    # within 4x the reference's alternative-FFT spread, as the GPU path is held (test_fit_c3_gpu)
+    fx = load("G19", "f64")
+    for j, k in enumerate(fx["box_steps"]):
+        if k >= len(t1_single):
+            break
+        ref, alt = fx["box_theta1_steps"][j], fx["box_alt_theta1_steps"][j]
+        assert np.linalg.norm(t1_single[k] - ref) <= 4 * np.linalg.norm(alt - ref) + 1e-9 * np.linalg.norm(ref), k

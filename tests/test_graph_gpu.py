@@ -59,3 +59,30 @@ def test_graph_replay_bitwise(dims, dt):
         ref = Q.apply(_lib.OP_K, x)
     s.synchronize()
     assert torch.equal(y, ref)
+
+
+def test_graph_key_tracks_plan_buffers():
+    """on a plan with an axis beyond 8192 points every operator runs the
+    full-grid route in gridA / gridB, sized to prod(L_K) for K and prod(L_R) for R^T.  K, K (the
+    second call is captured), R^T (grows and so reallocates both buffers), then K again with the
+    SAME x / y: the graph key holds every plan buffer an op addresses, so the last K runs
+    directly again instead of replaying a graph on the freed buffers -- its result equals a
+    graph-free plan's bit for bit."""
+    from hipgp_amd import _lib
+    dims = (5, 12000)
+    P, Q = _plans(dims, torch.float32)
+    M = int(np.prod(dims))
+    g = torch.Generator(device=DEV).manual_seed(11)
+    x = torch.randn(2, M, device=DEV, generator=g)
+    y = torch.empty_like(x)
+    ref = Q.apply(_lib.OP_K, x)
+    for _ in range(2):                            # direct, then captured
+        P.apply(_lib.OP_K, x, out=y)
+        assert torch.equal(y, ref)
+    rt = P.apply(_lib.OP_RT, x)                   # full-grid buffers regrown for L_R
+    assert torch.equal(rt, Q.apply(_lib.OP_RT, x))
+    for _ in range(3):                            # K with the captured call's x / y again
+        y.fill_(float("nan"))
+        P.apply(_lib.OP_K, x, out=y)
+        torch.cuda.synchronize()
+        assert torch.equal(y, ref)

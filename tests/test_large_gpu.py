@@ -105,3 +105,50 @@ def test_meanfield_elbo_C3():
     assert abs(e32 - e64) < 1e-4 * abs(e64), (e32, e64)
     for a, b in ((g1_32, g1_64), (g2_32, g2_64)):
         assert float((a - b).norm() / b.norm()) < 1e-4, float((a - b).norm() / b.norm())
+
+
+@pytest.mark.parametrize("m", [2048, 4096], ids=["C3_2048x2048_B200", "C4_4096x4096_B200"])
+def test_configs_own_batch_B200(m):
+    """The configs' own minibatch (C3 / C4: 200 RHS, `run_ukhousing_experiment.py:31`,
+    `run_3droad_experiment.py:48`) through the full chunk / two-stream schedule in fp32:
+    `_solve` and `compute_kn` of all 200 RHS in one call.  A seeded subset of 5 rows (first,
+    last, chunk-boundary neighbours and a middle row) is checked (a) against the fp64 plan of
+    the same problem -- SURVEY §8(c)'s PCG rule in the form the other full-size tests use here
+    (nugget 0.1: fp32 and fp64 differ by the implementation's rounding, ~1e-5; bound 1e-3) -- and
+    (b) against the same rows solved in a batch of 2 (other chunks, other streams, other batch
+    positions): every RHS runs its own FFTs and fixed-order reductions, so a row's result does
+    not depend on the batch around it -- bitwise in practice, held to 1e-6."""
+    B = 200
+    g = torch.Generator(device=DEV).manual_seed(31)
+    b = torch.randn(B, m * m, device=DEV, generator=g, dtype=torch.float32)
+    rows = [0, 1, 7, 101, B - 1]
+    T = _tt(m, torch.float32)
+    x = T._solve(b, do_precond=True, maxiter=20, tol=1e-8)
+    xs = x[rows].double()
+    del x
+    kn = T._matmul_by_RT(T.inv_matmul(b, do_precond=True, maxiter=20, tol=1e-8))
+    assert kn.shape == (B, (2 * m - 2) ** 2)
+    kns = kn[rows].double()
+    del kn
+    # (b) the same rows in batches of 2: batch-position independence
+    for j in range(0, len(rows) - 1, 2):
+        sub = b[rows[j:j + 2]]
+        x2 = T._solve(sub, do_precond=True, maxiter=20, tol=1e-8).double()
+        rel = float(((x2 - xs[j:j + 2]).norm(dim=1) / xs[j:j + 2].norm(dim=1)).max())
+        assert rel < 1e-6, (rows[j:j + 2], rel)
+        kn2 = T._matmul_by_RT(T.inv_matmul(sub, do_precond=True, maxiter=20, tol=1e-8)).double()
+        rel = float(((kn2 - kns[j:j + 2]).norm(dim=1) / kns[j:j + 2].norm(dim=1)).max())
+        assert rel < 1e-6, (rows[j:j + 2], rel)
+    del T
+    torch.cuda.empty_cache()
+    # (a) against the fp64 plan on the subset
+    T64 = _tt(m, torch.float64)
+    b64 = b[rows].double()
+    x64 = T64._solve(b64, do_precond=True, maxiter=20, tol=1e-8)
+    rel = float(((xs - x64).norm(dim=1) / x64.norm(dim=1)).max())
+    assert rel < 1e-3, rel
+    res = (T64._matmul_by_K(xs) - b64).norm(dim=1) / b64.norm(dim=1)
+    assert float(res.max()) < 0.05, res
+    kn64 = T64._matmul_by_RT(T64.inv_matmul(b64, do_precond=True, maxiter=20, tol=1e-8))
+    rel_kn = float(((kns - kn64).norm(dim=1) / kn64.norm(dim=1)).max())
+    assert rel_kn < 1e-3, rel_kn

@@ -129,3 +129,90 @@ def test_slab_ranks_same_device(case, ws):
         res = lambda x: float(torch.linalg.norm(vt[0] - Pd.apply(_lib.OP_K, torch.as_tensor(x, device="cuda").double())[0]))
         r_slab, r_single = res(gat("brk")), res(xb.double())
         assert r_slab <= 1.5 * max(r_single, out[0]["brk_tol"]), (r_slab, r_single, out[0]["brk_tol"])
+
+
+C5_DIMS = (256, 256, 128)
+
+
+def _c5_column(jitter=1e-3):
+    """Config 5's grid and kernel (`run_domain_experiment.py:77-82`: 256 x 256 x 128 over
+    x, y in [-.25, .25], z in [-.05, .05], Matern-5/2 (0.1, 0.1)), jitter 1e-3.  With jitter
+    1e-3 the spectrum is clamped and 20 PCG iterations amplify rounding chaotically (DESIGN §10
+    item 7: the true residual after PCG(20) is several |b| in fp64 and fp32 alike), so the two
+    recurrences are compared on the same geometry and kernel with nugget 0.05, where they agree
+    to rounding"""
+    grids = [np.linspace(-.25, .25, 256), np.linspace(-.25, .25, 256), np.linspace(-.05, .05, 128)]
+    return zo.toeplitz_column(grids, lambda x, y: zo.kernel_eval("matern", x, y, (.1, .1), nu=2.5), jitter)
+
+
+def _c5_worker(rank, ws, port, dtname, backend, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    if backend == "nccl":
+        dist.init_process_group("nccl", rank=rank, world_size=ws, device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        from hipgp_amd import _lib
+        from hipgp_amd.slab import slab_toeplitz
+        dt = getattr(torch, dtname)
+        col = torch.tensor(_c5_column(), device="cuda", dtype=dt)
+        S = slab_toeplitz(C5_DIMS, col, dtype=dt, device="cuda")
+        M = int(np.prod(C5_DIMS))
+        g = torch.Generator(device="cuda").manual_seed(17)
+        v = torch.randn(2, M, device="cuda", generator=g, dtype=torch.float64).to(dt)
+        res = {}
+        for name, op in (("K", _lib.OP_K), ("Cinv", _lib.OP_CINV), ("RT", _lib.OP_RT)):
+            res[name] = S.apply(op, S.scatter_rows(v, "m")).double().cpu().numpy()
+        del S
+        S = slab_toeplitz(C5_DIMS, torch.tensor(_c5_column(.05), device="cuda", dtype=dt), dtype=dt, device="cuda")
+        x, it = S.pcg(S.scatter_rows(v), maxiter=20, tol=1e-8)
+        res["pcg"], res["pcg_it"] = x.double().cpu().numpy(), it
+        torch.cuda.synchronize()
+        out[rank] = res
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("dtname,ws,backend", [("float64", 2, "gloo"), ("float32", 2, "gloo"), ("float64", 1, "nccl")],
+                         ids=["f64_gloo2", "f32_gloo2", "f64_rccl1"])
+def test_slab_C5_geometry(dtname, ws, backend):
+    """Grid-block sharding at config 5's own geometry (256 x 256 x 128, its kernel and settings;
+    `BASELINE.json` configs[4] "grid-block shard"): K, C^-1, R^T and PCG(20, tol 1e-8) of two
+    RHS over axis-0 slabs -- two ranks on one GPU over gloo, and the RCCL transposes / dot
+    all-reduces at world size 1 -- against the single-rank plan (fp64 1e-11 on the ops, the
+    PCG 1e-9; fp32 within FFT rounding: ops 2e-5, PCG(20) 1e-3, two fp32 recurrences --
+    all-reduced dots vs the fused device PCG -- rounding differently).  The ops run config 5's
+    own settings; the PCG its geometry and kernel with nugget 0.05 (_c5_column)."""
+    from hipgp_amd import _lib
+    from hipgp_amd.plan import ToeplitzPlan
+    dt = getattr(torch, dtname)
+    mgr = mp.Manager()
+    out = mgr.dict()
+    port = 29750 + os.getpid() % 100 + ws + (7 if backend == "nccl" else 0)
+    mp.spawn(_c5_worker, args=(ws, port, dtname, backend, out), nprocs=ws, join=True)
+    assert len(out) == ws
+    P = ToeplitzPlan(C5_DIMS, dt, "cuda")
+    P.set_column(torch.tensor(_c5_column(), device="cuda", dtype=dt))
+    M = int(np.prod(C5_DIMS))
+    g = torch.Generator(device="cuda").manual_seed(17)
+    v = torch.randn(2, M, device="cuda", generator=g, dtype=torch.float64).to(dt)
+    gat = lambda k: np.concatenate([out[r][k] for r in range(ws)], axis=1)
+    tol_op = 1e-11 if dt == torch.float64 else 2e-5
+    for name, op in (("K", _lib.OP_K), ("Cinv", _lib.OP_CINV), ("RT", _lib.OP_RT)):
+        ref = P.apply(op, v).double().cpu().numpy()
+        got = gat(name)
+        assert got.shape == ref.shape, name
+        err = float(np.max(np.abs(got - ref)) / np.max(np.abs(ref)))
+        print(dtname, ws, backend, name, "max rel err", err)
+        assert err < tol_op, (name, err)
+    P2 = ToeplitzPlan(C5_DIMS, dt, "cuda")
+    P2.set_column(torch.tensor(_c5_column(.05), device="cuda", dtype=dt))
+    xr = P2.pcg(v, 20, 1e-8, precond=True).double().cpu().numpy()
+    err = float(np.linalg.norm(gat("pcg") - xr) / np.linalg.norm(xr))
+    print(dtname, ws, backend, "PCG(20) rel err", err)
+    assert err < (1e-9 if dt == torch.float64 else 1e-3), err
+    for r in range(ws):
+        assert out[r]["pcg_it"] == 20

@@ -51,8 +51,14 @@ def b_rt(dims, s=4):
 
 
 def floor_rt(dims, L_R, s=4, real_spec=True):
-    """(bytes per RHS, spectrum bytes per chunk) of R^T on the L_R grid (compact last axis)."""
+    """(bytes per RHS, spectrum bytes per chunk) of R^T on the L_R grid (compact last axis).
+    L_R may carry trailing unit entries (hgp_plan_info pads it to three axes): they are dropped,
+    so that the compact last axis is the grid's own last axis."""
     d = len(dims)
+    L_R = list(L_R)
+    if len(L_R) > d:
+        assert all(v == 1 for v in L_R[d:]), L_R
+        L_R = L_R[:d]
     M = _prod(dims)
     n = ngrid(dims)
     Mp = _prod(n)
