@@ -125,7 +125,11 @@
 #ifndef HGP_QUAD
 #define HGP_QUAD 1
 #endif
-// the quad-order (LAY_CONTIG_Q) column pass of 4096-point lines: two 8-wave blocks per CU
+// the quad-order (LAY_CONTIG_Q) column pass of 4096-point lines: lines per block and waves per
+// SIMD (2 lines, 4 waves/SIMD: two 8-wave blocks per CU)
+#ifndef HGP_QUAD_LINES_4096
+#define HGP_QUAD_LINES_4096 2
+#endif
 #ifndef HGP_MINW_CONTIG_Q4096
 #define HGP_MINW_CONTIG_Q4096 4
 #endif
@@ -222,10 +226,13 @@ template <typename T, int H, int LAY> struct PassCfg {
     while (c > 1 && (c * TT > 1024 || lds_bytes_for(c) > LDS_CAP / 2)) c >>= 1;
     return c;
   }
-  // quad order: at least the 2 lines of a 64-B half per block where a block can hold them
+  // quad order: the 2 lines of a 64-B half per block for the 4-wave (4096-point) lines
+  // (HGP_QUAD_LINES_4096); longer lines (the 6144-point R / R^T conv: 8 waves each) keep one
+  // line per block -- two made 16-wave blocks, one per CU (C4 R^T conv 8.5 -> 12.7 ms)
   static constexpr int c_quad() {
     const int c = c_contig();
-    return c >= 2 ? c : ((2 * TT <= 1024 && lds_bytes_for(2) <= LDS_CAP) ? 2 : 1);
+    if (c >= 2) return c;
+    return (TT == 256 && HGP_QUAD_LINES_4096 == 2 && lds_bytes_for(2) <= LDS_CAP) ? 2 : 1;
   }
   static constexpr int C = lay_grp(LAY) ? lay_grp(LAY) : lay_smap(LAY) ? c_strided()
                            : LAY == LAY_CONTIG_Q ? c_quad() : c_contig();
@@ -246,8 +253,8 @@ template <typename T, int H, int LAY> struct PassCfg {
                                  : H >= 2048 ? HGP_MINW_CONTIG_LONG : H <= 512 ? HGP_MINW_CONTIG_SHORT : HGP_MINW_CONTIG;
   // a block's waves must fit the SIMDs' share at once: >= WAVES_PER_BLOCK / 4 waves per SIMD
   static constexpr int MINW_BLK = (WAVES_PER_BLOCK + 3) / 4;
-  // quad-order blocks of two 4-wave lines: 4 waves per SIMD, two blocks per CU
-  static constexpr int MINW_Q = (C == 2 && TT == 256) ? HGP_MINW_CONTIG_Q4096 : MINW_CL;
+  // quad-order blocks of 4096-point lines (4 waves each): HGP_MINW_CONTIG_Q4096 waves per SIMD
+  static constexpr int MINW_Q = TT == 256 ? HGP_MINW_CONTIG_Q4096 : MINW_CL;
   static constexpr int MINW_SET = lay_grp(LAY) ? (MINW_CL > MINW_BLK ? MINW_CL : MINW_BLK)
                                  : lay_smap(LAY) ? (TT >= 16 ? HGP_MINW_STRIDED : HGP_MINW_STRIDED_SMALL)
                                  : LAY == LAY_CONTIG_Q ? (MINW_Q > MINW_BLK ? MINW_Q : MINW_BLK)

@@ -35,18 +35,34 @@ def split(n, parts, k):
     return start, start + base + (1 if k < extra else 0)
 
 
+# largest all-to-all handed to RCCL in one call: a 2.4 GB exchange (config 5's R^T, two fp64
+# RHS, world size 1) came back wrong from one all_to_all_single, so larger exchanges go in pieces
+A2A_MAX_BYTES = 1 << 30
+
+
 def _a2a(out, inp, out_splits, in_splits, group):
-    """all_to_all_single on real views (complex / CUDA through the host for gloo)."""
+    """all_to_all_single on real views (complex / CUDA through the host for gloo).  Exchanges
+    above A2A_MAX_BYTES run as several all_to_all calls over equal parts of every peer's block."""
     gloo = dist.get_backend(group) == "gloo"
     i = torch.view_as_real(inp).reshape(-1) if inp.is_complex() else inp.reshape(-1)
     o = torch.view_as_real(out).reshape(-1) if out.is_complex() else out.reshape(-1)
     f = 2 if inp.is_complex() else 1
+    so, si = [f * s for s in out_splits], [f * s for s in in_splits]
     if gloo and i.is_cuda:
         ih, oh = i.cpu(), torch.empty(o.shape, dtype=o.dtype)
-        dist.all_to_all_single(oh, ih, [f * s for s in out_splits], [f * s for s in in_splits], group=group)
+        dist.all_to_all_single(oh, ih, so, si, group=group)
         o.copy_(oh)
-    else:
-        dist.all_to_all_single(o, i, [f * s for s in out_splits], [f * s for s in in_splits], group=group)
+        return out
+    nbytes = max(sum(so), sum(si)) * i.element_size()
+    if nbytes <= A2A_MAX_BYTES:
+        dist.all_to_all_single(o, i, so, si, group=group)
+        return out
+    parts = -(-nbytes // A2A_MAX_BYTES)
+    oo = [sum(so[:r]) for r in range(len(so))]
+    oi = [sum(si[:r]) for r in range(len(si))]
+    for j in range(parts):
+        piece = lambda t, offs, sizes: [t[a + s * j // parts:a + s * (j + 1) // parts] for a, s in zip(offs, sizes)]
+        dist.all_to_all(piece(o, oo, so), piece(i, oi, si), group=group)
     return out
 
 

@@ -12,10 +12,13 @@ maxiter_cg 20 (`run_ukhousing_experiment.py:22,31,33,49-50,207-208,277`,
 Every natural-gradient step divides by k_n from a 20-iteration PCG that has not converged, so
 the iterates carry the PCG's rounding: two fp64 runs of the reference itself that differ only
 in the FFT implementation (torch.fft vs NumPy's pocketfft in the shim, G19 "{case}_alt_*")
-already differ by ~1e-5 ("box") and ~5e-2 ("fine") after one step.  The fp64 bound is 4x that
-spread of the reference's own (SURVEY §8(c)'s 4x rule with the FFT's rounding as the yardstick);
-fp32 keeps the rule against the reference's own fp32 error.
+already differ by ~1e-5 ("box") and ~1e-2 ("fine") after one step.  The "box" fp64 bound is 4x
+that spread of the reference's own (SURVEY §8(c)'s 4x rule with the FFT's rounding as the
+yardstick); "fine" is held to 10x the largest of nine self-perturbed reference re-runs
+(G19_fine_alt); fp32 keeps the rule against the reference's own fp32 error.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -95,17 +98,31 @@ def test_c3_settings_box_fp32(tmp_path):
     assert np.all(e_me <= 4 * e_ref + 1e-5 * np.abs(t64)), (e_me, e_ref)
 
 
+def _nine_run_bound(fx, alt9, name, j, got, factor=10):
+    """|got - ref| <= factor x max over the nine self-perturbed reference runs of G19_fine_alt
+    (tests/golden/make_golden_fit_c3_alt.py) of |alt - ref|, + 1e-9 |ref|"""
+    ref = fx[f"fine_{name}_steps"][j]
+    e_alt = max(np.linalg.norm(alt9[f"alt{a}_{name}_steps"][j] - ref) for a in range(9))
+    e_me = np.linalg.norm(got - ref)
+    print("fine", name, "step", j, "|me - ref| / |ref|", e_me / np.linalg.norm(ref), "nine-run spread", e_alt / np.linalg.norm(ref))
+    assert e_me <= factor * e_alt + 1e-9 * np.linalg.norm(ref), (name, j, e_me, e_alt)
+
+
 def test_c3_settings_fine_diverges_like_reference_fp64(tmp_path):
     fx = load("G19", "f64")
+    alt9 = np.load(os.path.join(os.path.dirname(__file__), "golden", "G19_fine_alt.npz"))
     snaps, trace = _run(fx, "fine", torch.float64, tmp_path)
-    # the first iterates: within 10x the reference's own FFT-rounding spread.  Here K (ell / h =
+    # the first iterates: within 10x the reference's own rounding spread.  Here K (ell / h =
     # 27 / 37, nugget 1e-3) is so ill-conditioned that the first step's unconverged PCG(20) moves
-    # by 0.9 % between two exact CPU FFTs of the same n-grid (G19 alt); the GPU path transforms a
-    # different grid (L_K = 128 linear convolution, fp64 DCT spectra) and lands 4 % away (measured
-    # on the box; 4.4x the alt spread) -- the same regime, bounded by 10x
+    # by ~1 % between re-runs of the reference that differ only at the rounding level (another
+    # exact FFT, last-place moves of the kernel column, FFT outputs perturbed at an fp FFT's
+    # rounding level: nine runs, G19_fine_alt); the GPU path transforms a different grid (L_K = 128
+    # linear convolution, fp64 DCT spectra) -- the same regime, bounded by 10x the largest of the
+    # nine distances
+    assert np.array_equal(alt9["steps"], fx["fine_steps"])
     for j, k in enumerate(fx["fine_steps"]):
-        _spread_bound(fx, "fine", "theta1", j, snaps[k][0], factor=10)
-        _spread_bound(fx, "fine", "theta2", j, snaps[k][1], factor=10)
+        _nine_run_bound(fx, alt9, "theta1", j, snaps[k][0])
+        _nine_run_bound(fx, alt9, "theta2", j, snaps[k][1])
     # the divergence itself: |theta1| and the ELBO grow batch by batch as the reference's
     n1 = np.array([np.linalg.norm(s[0]) for s in snaps])
     assert np.all(np.abs(np.log(n1 / fx["fine_theta1_norm"])) < np.log(1.5)), (n1, fx["fine_theta1_norm"])
