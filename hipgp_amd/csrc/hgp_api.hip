@@ -138,6 +138,10 @@ struct hgp_plan {
   // 2-D operators run their RHS chunks on `nstreams` streams (the plan's own + side streams),
   // so one chunk's compute-heavy column pass overlaps another's memory-heavy row passes
   int nstreams = 2;
+  // the 2-D preconditioned PCG chains K p and C^-1 r per RHS chunk (pcg_step_t; HGP_CHAIN_PCG=1).
+  // Off by default: measured slower at every 2-D config (PCG(20) C2 14.9 -> 15.2 ms, C3 390 ->
+  // 395 ms, C4 215.4 -> 218 ms; profiles/r5_e_kn_phases_chain.txt)
+  bool chain_pcg = false;
   hipStream_t side[3] = {nullptr, nullptr, nullptr};
   hipEvent_t ev_fork = nullptr, ev_join[3] = {nullptr, nullptr, nullptr};
   // hipGraph of a repeated hgp_toeplitz_apply (same op, buffers, RHS count, workspaces, stream):
@@ -308,6 +312,18 @@ void set_cg_scalar(PassDesc& D, const RowEpi* epi, int64_t q0) {
 // computes the chunk's alpha / beta from the column pass's spectral dots.
 using MidFn = std::function<void(int64_t, int, hipStream_t)>;
 
+// A second operator chained onto a 2-D K op per RHS chunk (the fused PCG iteration, pcg_step_t):
+// K's row-inverse pass runs EPI_RF (r update + the forward row transform of the new r into the
+// chunk's intermediate), then this op's axis-0 pass (spectrum `spec`, spectral dots into
+// `spart`), `mid`, and its row-inverse pass with epilogue `epi` -- K p and C^-1 r of one
+// iteration back to back on each chunk's stream, r never re-read from HBM.
+struct PairOp {
+  const void* spec;
+  void* spart;
+  const RowEpi* epi;
+  const MidFn* mid;
+};
+
 // y = op(x) on RHS [0, nrhs); optional fused dot with `dotv` into partial[b][rn_last].
 // Every RHS is processed on its own (no two RHS share an FFT).  only_pass >= 0 runs a single
 // pass of the sequence (profiling).  2-D only: `spart` receives the column pass's spectral
@@ -372,7 +388,7 @@ bool grid_route(const hgp_plan* P, int op) {
 template <typename T>
 int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void* dotv, void* partial,
            const int* done, int only_pass = -1, void* spart = nullptr, const RowEpi* epi = nullptr,
-           const MidFn* mid = nullptr) {
+           const MidFn* mid = nullptr, const PairOp* pair = nullptr) {
   if (grid_route(P, op)) {
     if (spart != nullptr || epi != nullptr || mid != nullptr || only_pass >= 0)
       return fail(HGP_E_UNSUPPORTED, "internal: the full-grid route has no fused PCG epilogue or pass split");
@@ -398,6 +414,8 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
   if (d == 2) B1 = gen2 ? std::max(g.in[0], g.out[0]) * Sl : (g.L[1] / 2 + G2) / G2 * G2 * S0;
   if (gen2 && (spart != nullptr || epi != nullptr || mid != nullptr))
     return fail(HGP_E_ARG, "internal: the generic 2-D sequence has no fused PCG epilogue");
+  if (pair != nullptr && (d != 2 || gen2 || epi == nullptr || epi->mode != EPI_R || only_pass >= 0))
+    return fail(HGP_E_ARG, "internal: a chained operator needs the 2-D row-pair sequence and an EPI_R epilogue");
   // 3-D (hgp_lines.hpp): the (i1, i2) plane of every (RHS, i0) goes through the 2-D row-pair
   // kernels -> W1 [q][i0][c2][i1] (column pitch S1); transposing axis-1 line passes <->
   // W2 [q][c2][k1][i0] (axis-0 pitch S0), whose axis-0 lines the contiguous conv pass takes.
@@ -528,6 +546,8 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
         Bd.spart = reinterpret_cast<T*>(spart) + q0 * (H1 + 1);
         Bd.spart_mid = (int)(H1 / 2);
       }
+      int b_lay = LAY_CONTIG;
+      int64_t b_lines = 0;
       if (G2 > 1) {     // lines (column group, RHS, column in group): ceil(Rn / G2) G2 per RHS
         Bd.grp = G2;
         // G2 position-fast blocks per group (LAY_CONTIG_G).  HGP_GRP_BLOCKS=1: one block per
@@ -540,11 +560,13 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
         const int glay = G2 == 2 ? LAY_GRP2 : (G2 == 4 && !quad) ? LAY_GRP4 : -1;
         static const bool grp_on = [] { const char* e = std::getenv("HGP_GRP_BLOCKS"); return e && std::atoi(e) == 1; }();
         const bool use_grp = glay >= 0 && grp_on && pass_geom<T>((int)(g.L[0] / 2), glay).C == G2;
-        const int clay = use_grp ? glay : quad ? LAY_CONTIG_Q : LAY_CONTIG_G;
-        HGP_TRY(run((int)(g.L[0] / 2), conv_mode, clay, Bd, (int64_t)qn * ((H1 + G2) / G2) * G2));
+        b_lay = use_grp ? glay : quad ? LAY_CONTIG_Q : LAY_CONTIG_G;
+        b_lines = (int64_t)qn * ((H1 + G2) / G2) * G2;
       } else {
-        HGP_TRY(run((int)(g.L[0] / 2), conv_mode, LAY_CONTIG, Bd, (int64_t)qn * Bd.Rn));
+        b_lay = LAY_CONTIG;
+        b_lines = (int64_t)qn * Bd.Rn;
       }
+      HGP_TRY(run((int)(g.L[0] / 2), conv_mode, b_lay, Bd, b_lines));
       if (mid != nullptr) (*mid)(q0, qn, st);
       // C: INV along axis 1: column-major tiles -> row pairs, crop, fused dot or PCG update
       PassDesc Cd = base_desc();
@@ -563,7 +585,31 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
         Cd.cg_part = epi->part ? reinterpret_cast<T*>(epi->part) + q0 * nrb : nullptr;
         set_cg_scalar<T>(Cd, epi, q0);
       }
-      HGP_TRY(run_rowt(1, Cd, epi_mode));
+      if (pair == nullptr) {
+        HGP_TRY(run_rowt(1, Cd, epi_mode));
+      } else {
+        // K's row inverse also leaves the forward row transform of the new r in w1 (EPI_RF);
+        // the chained op (C^-1, same L_K grid) continues at its axis-0 pass on this stream
+        HGP_TRY(run_rowt(1, Cd, EPI_RF));
+        PassDesc B2 = Bd;
+        B2.spec = pair->spec;
+        B2.spart = pair->spart != nullptr ? reinterpret_cast<T*>(pair->spart) + q0 * (H1 + 1) : nullptr;
+        B2.spart_mid = (int)(H1 / 2);
+        HGP_TRY(run((int)(g.L[0] / 2), conv_mode, b_lay, B2, b_lines));
+        if (pair->mid != nullptr) (*pair->mid)(q0, qn, st);
+        PassDesc C2d = Cd;
+        const RowEpi* e2 = pair->epi;
+        const int nrb = (Cd.Rn + rowt_pairs<T>((int)H1, 1) - 1) / rowt_pairs<T>((int)H1, 1);
+        C2d.dot = nullptr; C2d.partial = nullptr;
+        C2d.cg_r = reinterpret_cast<T*>(e2->r) + q0 * g.out_M;
+        C2d.cg_x = reinterpret_cast<T*>(e2->x) + q0 * g.out_M;
+        C2d.cg_p = reinterpret_cast<T*>(e2->p) + q0 * g.out_M;
+        C2d.cg_coef = reinterpret_cast<const T*>(e2->coef) + q0;
+        C2d.cg_part = e2->part ? reinterpret_cast<T*>(e2->part) + q0 * nrb : nullptr;
+        C2d.cg_sp = nullptr; C2d.cg_np = 0; C2d.cg_rs = nullptr; C2d.cg_rs_out = nullptr;
+        set_cg_scalar<T>(C2d, e2, q0);
+        HGP_TRY(run_rowt(1, C2d, e2->mode));
+      }
     } else if (d == 3 && !gen3) {
       C2<T>* w1 = reinterpret_cast<C2<T>*>(P->ws1.ptr) + (int64_t)slot * Qc * B1;
       C2<T>* w2 = reinterpret_cast<C2<T>*>(P->ws2.ptr) + (int64_t)slot * Qc * B2;
@@ -1315,6 +1361,29 @@ int pcg_step_t(hgp_plan* P, double tol) {
     const bool defer = P->cg_precond != 0;
     RowEpi exr{defer ? EPI_R : EPI_XR, P->r.ptr, P->cg_x, P->p.ptr, alpha, P->part_u.ptr};
     if (inkern) { exr.sp = part_s; exr.np = nps; exr.rs = rs_cur; exr.alpha_out = alpha; }
+    if (P->cg_precond && P->d == 2 && P->chain_pcg) {
+      // 2-D: K p and C^-1 r chained per RHS chunk (run_op PairOp): K's row-inverse pass updates r
+      // and leaves its forward row transform for C^-1 (EPI_RF), C^-1's row-inverse pass does
+      // x += alpha p, p = z + beta p (EPI_XP); then the all-RHS break test.  The x update of the
+      // iteration in which the break fires is the same either way, and the p update after it is
+      // never read, so the C^-1 half no longer waits for the test (cg.py:67-75 arithmetic and
+      // break rule unchanged; the fix-up pass of PassDesc::cg_fix is not needed).
+      const MidFn mid_beta = [&](int64_t q0, int qn, hipStream_t cs) {
+        fold(q0, qn, cs);
+        if (!inkern) cg_beta<T>(part_s + q0 * nps, nps, qn, rs_cur + q0, beta + q0, done, cs);
+      };
+      RowEpi ep{EPI_XP, P->r.ptr, P->cg_x, P->p.ptr, beta, nullptr};
+      ep.coef2 = alpha;
+      ep.fix = -1;
+      if (inkern) { ep.sp = part_s; ep.np = nps; ep.rs = rs_cur; ep.rs_out = rs_nxt; }
+      const PairOp pair{P->specI.ptr, part_o, &ep, (G > 0 || !inkern) ? &mid_beta : nullptr};
+      HGP_TRY(run_op<T>(P, HGP_OP_K, P->p.ptr, P->Ap.ptr, nrhs, nullptr, nullptr, done, -1, part_o, &exr,
+                        (G > 0 || !inkern) ? &mid_alpha : nullptr, &pair));
+      cg_check<T>(P->part_u.ptr, npx, (int)nrhs, tol, rnew, done, iters, s);
+      if (inkern) P->cg_rs_par ^= 1;
+      HIP_TRY(hipGetLastError());
+      return 0;
+    }
     HGP_TRY(run_op<T>(P, HGP_OP_K, P->p.ptr, P->Ap.ptr, nrhs, nullptr, nullptr, done, -1, part_o, &exr,
                       (G > 0 || !inkern) ? &mid_alpha : nullptr));
     cg_check<T>(P->part_u.ptr, npx, (int)nrhs, tol, rnew, done, iters, s);
@@ -1462,6 +1531,8 @@ int hgp_plan_create(int device, int ndim, const int64_t* m, int dtype, int64_t m
   if (hg && std::atoi(hg) == 0) P->use_graphs = false;
   const char* ns = std::getenv("HGP_STREAMS");
   if (ns) P->nstreams = std::max(1, std::min(4, std::atoi(ns)));
+  const char* cp = std::getenv("HGP_CHAIN_PCG");
+  if (cp) P->chain_pcg = std::atoi(cp) != 0;
   int rc = 0;
   for (int a = 0; a < d && rc == 0; ++a) {
     if (dtype == HGP_F64) {

@@ -126,9 +126,12 @@
 #define HGP_QUAD 1
 #endif
 // the quad-order (LAY_CONTIG_Q) column pass of 4096-point lines: lines per block and waves per
-// SIMD (2 lines, 4 waves/SIMD: two 8-wave blocks per CU)
+// SIMD.  One line per block at 4 waves/SIMD (four 4-wave blocks per CU): C4 K op 4.63 -> 4.54 ms
+// (column pass 2.13 -> 2.01 ms against the plain G = 4 order); two lines per block (8-wave blocks,
+// whole 64-B halves per block) cut the pass's HBM writes 5.16 -> 3.64 GB per op but ran 2.27 ms,
+// and one line at 3 waves/SIMD 2.03 ms (profiles/r5_e_quad_variants.txt)
 #ifndef HGP_QUAD_LINES_4096
-#define HGP_QUAD_LINES_4096 2
+#define HGP_QUAD_LINES_4096 1
 #endif
 #ifndef HGP_MINW_CONTIG_Q4096
 #define HGP_MINW_CONTIG_Q4096 4
@@ -148,7 +151,10 @@ constexpr bool lay_smap(int lay) { return lay == LAY_STRIDED || lay == LAY_SEG_S
 enum { SPEC_REAL = 0, SPEC_CPLX = 1, SPEC_CPLX_CONJ = 2 };
 // row-inverse epilogue (hgp_rows.hpp): EPI_XR x/r update (unpreconditioned PCG); with the
 // preconditioner the x update is deferred to the C^-1 pass: EPI_R r update, EPI_XP x and p
-enum { EPI_OUT = 0, EPI_XR = 1, EPI_R = 2, EPI_XP = 3 };
+// EPI_RF: EPI_R, then the forward row transform of the updated r rows (the first pass of the
+// C^-1 r that follows in the same PCG iteration) into the block's rows of the intermediate
+enum { EPI_OUT = 0, EPI_XR = 1, EPI_R = 2, EPI_XP = 3, EPI_RF = 4 };
+constexpr bool epi_r(int e) { return e == EPI_R || e == EPI_RF; }
 
 struct View {
   void* ptr;

@@ -142,6 +142,7 @@ static hipError_t launch_rowt_g(int inv, int epi, const PassDesc& d, hipStream_t
     if (epi == EPI_XR) return launch_rowt_inv<T, H, EPI_XR, G>(d, nb, s);
     if (epi == EPI_R) return launch_rowt_inv<T, H, EPI_R, G>(d, nb, s);
     if (epi == EPI_XP) return launch_rowt_inv<T, H, EPI_XP, G>(d, nb, s);
+    if (epi == EPI_RF) return launch_rowt_inv<T, H, EPI_RF, G>(d, nb, s);
     return launch_rowt_inv<T, H, EPI_OUT, G>(d, nb, s);
   }
   static bool attr_set = false;

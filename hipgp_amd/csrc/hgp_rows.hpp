@@ -28,6 +28,11 @@
 #ifndef HGP_ROW_XCD
 #define HGP_ROW_XCD 1
 #endif
+// the forward transform in the EPI_RF tail: the two halves one after the other (fits the
+// row-inverse kernel's register budget: interleaved, the C2 kernel spilled 28 VGPRs)
+#ifndef HGP_RF_SEQ
+#define HGP_RF_SEQ 1
+#endif
 #ifndef HGP_ROWT_PAIRS_BIG
 #define HGP_ROWT_PAIRS_BIG 16     // the same knob for rows longer than one wave's line (TT > 64)
 #endif
@@ -169,7 +174,7 @@ __device__ __forceinline__ int row_block_id() {
 // twiddled odd half, both halves' FFTs,
 // Hermitian split, and the transposed half spectra out to the intermediate (column pitch S0,
 // grouped by G).  Needs the twiddle table staged in `tab`; uses the LDS area from `lds`.
-template <typename T, int H, int P, int G>
+template <typename T, int H, int P, int G, bool SEQ = false>
 __device__ __forceinline__ void row_fwd_tail(C2<T> (&va)[P], C2<T> (&vb)[P],
                                              C2<T>* lds, const C2<T>* tab, const C2<T>* __restrict__ twg, int t,
                                              int l, int lbase, C2<T>* W, int64_t S0, int row0, int nrow_blk) {
@@ -179,8 +184,9 @@ __device__ __forceinline__ void row_fwd_tail(C2<T> (&va)[P], C2<T> (&vb)[P],
 #pragma unroll
   for (int k = 0; k < P; ++k) vb[k] = cmul<T>(vb[k], tw_at<T, H>(tab, t + TT * k));
   const BufRsrc rW = buf_rsrc(W, 0x7fffffffu);     // one RHS's slab: < 2 GiB (checked on the host)
-  // both frequency halves' transforms, interleaved over the group's exchange image
-  fft_line2<T, H, P, -1, 1, Cfg::WAVE>(va, vb, lds, lbase, t, tab);
+  // both frequency halves' transforms, interleaved over the group's exchange image (SEQ: one
+  // after the other, 32 fewer live VGPRs -- the row-inverse kernel's EPI_RF tail)
+  fft_line2<T, H, P, -1, 1, Cfg::WAVE, SEQ>(va, vb, lds, lbase, t, tab);
   auto do_half = [&](auto half_c, C2<T>(&v)[P]) {
     constexpr int half = decltype(half_c)::value;
     constexpr int C0 = (half == 0) ? 0 : H / 2 + 1;
@@ -334,6 +340,8 @@ __global__ __launch_bounds__((RowTCfg<T, H, G>::THREADS), (RowTCfg<T, H, G>::MIN
 //   EPI_XR (y = A p):     x += a p;  r -= a y;  returns this thread's share of r.r  (cg.py:67-69)
 //   EPI_R  (y = A p):     r -= a y;  returns this thread's share of r.r           (cg.py:68-69)
 //   EPI_XP (y = C^-1 r):  x += a p;  p = y + b p  (the iteration's x update, deferred) (cg.py:67, 75)
+//   EPI_RF (y = A p):     as EPI_R, and the new r values overwrite y in `ys` (the caller then
+//                         transforms them for the C^-1 pass)
 // x is never read by the recurrence, so moving its update from the A p pass to the C^-1 r pass
 // (where p is read anyway) saves one read of p per iteration with the same arithmetic; a
 // break after the r update is finished by the EPI_XP pass alone (PassDesc::cg_fix).
@@ -361,17 +369,18 @@ __device__ __forceinline__ T cg_epilogue(const T* __restrict__ ys, int nrow, int
       const int c = ee - row * out_len;
       g[u] = ((uint32_t)row * (uint32_t)rpitch + (uint32_t)c) * (uint32_t)sizeof(T);
       yv[u] = ys[ee];
-      if constexpr (EPI != EPI_R) pv[u] = buf_ld<T>(rp, g[u]);
+      if constexpr (!epi_r(EPI)) pv[u] = buf_ld<T>(rp, g[u]);
       if constexpr (EPI == EPI_XR || EPI == EPI_XP) xv[u] = buf_ld<T>(rx, g[u]);
-      if constexpr (EPI == EPI_XR || EPI == EPI_R) rv[u] = buf_ld<T>(rr, g[u]);
+      if constexpr (EPI == EPI_XR || epi_r(EPI)) rv[u] = buf_ld<T>(rr, g[u]);
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if (e0 + u * THREADS < nel) {
-        if constexpr (EPI == EPI_XR || EPI == EPI_R) {
+        if constexpr (EPI == EPI_XR || epi_r(EPI)) {
           if constexpr (EPI == EPI_XR) buf_st<T>(xv[u] + coef * pv[u], rx, g[u]);
           const T rn = rv[u] - coef * yv[u];
           buf_st<T>(rn, rr, g[u]);
+          if constexpr (EPI == EPI_RF) const_cast<T*>(ys)[e0 + u * THREADS] = rn;   // this thread's own slot
           s += rn * rn;
         } else {
           buf_st<T>(xv[u] + coef2 * pv[u], rx, g[u]);
@@ -600,9 +609,9 @@ __global__ __launch_bounds__((RowTCfg<T, H, G>::THREADS), (RowTCfg<T, H, G>::MIN
 #pragma unroll
       for (int w = 0; w < Cfg::THREADS / 64; ++w) tot += red2[w];   // wave order: deterministic
       const T rs = reinterpret_cast<const T*>(d.cg_rs)[qc];
-      if constexpr (EPI == EPI_XR || EPI == EPI_R) {
+      if constexpr (EPI == EPI_XR || epi_r(EPI)) {
         coef = rs / tot;
-        if (EPI == EPI_R && d.cg_alpha_out != nullptr && rb == 0 && threadIdx.x == 0 &&
+        if (epi_r(EPI) && d.cg_alpha_out != nullptr && rb == 0 && threadIdx.x == 0 &&
             (d.cg_div <= 1 || q % d.cg_div == 0))
           reinterpret_cast<T*>(d.cg_alpha_out)[qc] = coef;   // for this iteration's EPI_XP
       } else {
@@ -614,11 +623,11 @@ __global__ __launch_bounds__((RowTCfg<T, H, G>::THREADS), (RowTCfg<T, H, G>::MIN
       coef = reinterpret_cast<const T*>(d.cg_coef)[qc];
     }
     T* pg = reinterpret_cast<T*>(d.cg_p) + g0;
-    T* xg = EPI != EPI_R ? reinterpret_cast<T*>(d.cg_x) + g0 : pg;
+    T* xg = !epi_r(EPI) ? reinterpret_cast<T*>(d.cg_x) + g0 : pg;
     T* rg = EPI != EPI_XP ? reinterpret_cast<T*>(d.cg_r) + g0 : pg;
     const T coef2 = EPI == EPI_XP ? reinterpret_cast<const T*>(d.cg_coef2)[qc] : (T)0;
     T s = cg_epilogue<T, EPI, Cfg::THREADS>(ys, nrow_blk, out_len, xg, rg, pg, d.out.r_stride, coef, coef2);
-    if constexpr (EPI == EPI_XR || EPI == EPI_R) {   // deterministic block sum of r.r -> partial [q][rb]
+    if constexpr (EPI == EPI_XR || epi_r(EPI)) {   // deterministic block sum of r.r -> partial [q][rb]
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
       T* red = ys + 2 * C * out_len;   // past the staged rows (2C x out_len <= C x H values)
@@ -629,6 +638,27 @@ __global__ __launch_bounds__((RowTCfg<T, H, G>::THREADS), (RowTCfg<T, H, G>::MIN
         for (int w = 0; w < Cfg::THREADS / 64; ++w) tot += red[w];
         reinterpret_cast<T*>(d.cg_part)[(int64_t)q * nrb + rb] = tot;
       }
+    }
+    if constexpr (EPI == EPI_RF) {
+      // C^-1 r of the same iteration starts with the forward row transform of r: run it here on
+      // the block's rows of the updated r (staged in ys by cg_epilogue), writing them into the
+      // same rows of this RHS's intermediate -- this block read those rows' tiles above and no
+      // other block touches them, so in place is safe.  The C^-1 op then starts at its axis-0
+      // pass, and r is not read back from HBM.  (out_len = the row length: K's output rows are
+      // C^-1's input rows, both on the m-grid, at most H values, no fold.)
+      C2<T> fa[P], fb[P];
+      const T* ra = ys + (2 * l) * out_len;
+#pragma unroll
+      for (int k = 0; k < P; ++k) {
+        const int p = t + TT * k;
+        const bool in = pvalid && p < out_len;
+        const T a = in ? ra[p] : (T)0;
+        const T b = (in && has2) ? ra[out_len + p] : (T)0;
+        fa[k] = mk<T>(a, b);
+        fb[k] = fa[k];
+      }
+      __syncthreads();   // ys consumed: the exchange images overlay it
+      row_fwd_tail<T, H, P, G, HGP_RF_SEQ>(fa, fb, lds, tab, twg, t, l, lbase, const_cast<C2<T>*>(W), S0, row0, nrow_blk);
     }
     return;
   }
