@@ -142,6 +142,9 @@ struct hgp_plan {
   // Off by default: measured slower at every 2-D config (PCG(20) C2 14.9 -> 15.2 ms, C3 390 ->
   // 395 ms, C4 215.4 -> 218 ms; profiles/r5_e_kn_phases_chain.txt)
   bool chain_pcg = false;
+  // pack the 2-D K / C^-1 intermediate's real DC and Nyquist columns into one (PassDesc::dcny;
+  // HGP_DCNY=0: off)
+  bool dcny_pack = true;
   hipStream_t side[3] = {nullptr, nullptr, nullptr};
   hipEvent_t ev_fork = nullptr, ev_join[3] = {nullptr, nullptr, nullptr};
   // hipGraph of a repeated hgp_toeplitz_apply (same op, buffers, RHS count, workspaces, stream):
@@ -529,12 +532,21 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
         if (e != hipSuccess) return fail(HGP_E_HIP, std::string("row pass launch: ") + hipGetErrorString(e));
         return 0;
       };
+      // packed DC / Nyquist columns (PassDesc::dcny): K / C^-1 (real spectra) on the plain
+      // layout, axis-0 lines of one wave, rows of >= 512 points (where the axis-0 pass's line
+      // count per RHS decides its rounds of resident blocks; small grids keep every column)
+      int dcny = 0;
+      if (P->dcny_pack && G2 == 1 && (op == HGP_OP_K || op == HGP_OP_CINV) && H1 >= 256) {
+        const PassGeom pg0 = pass_geom<T>((int)(g.L[0] / 2), LAY_CONTIG);
+        if (pg0.C > 0 && pg0.threads / pg0.C <= 64) dcny = (int)(H1 / 2);
+      }
       // A: FWD along axis 1, row pairs of each RHS -> column-major half spectra w1 [q][c1][i0]
       //    (grouped by G2 columns: w1 [q][c1 / G2][i0][c1 % G2])
       PassDesc A = base_desc();
       A.in = View{(void*)xi, g.in_M, g.in[1], 1, (int)g.in[1]};
       A.out = View{w1, B1, S0, 1, 0};
       A.tw = g.tw[1].ptr; A.Q = qn; A.Rn = (int)((g.in[0] + 1) / 2); A.nrows = (int)g.in[0]; A.done = done;
+      A.dcny = dcny;
       HGP_TRY(run_rowt(0, A, EPI_OUT));
       // B: CONV along axis 0 = contiguous lines (q, c1), in place; spectrum [c1][k0]
       PassDesc Bd = base_desc();
@@ -542,6 +554,7 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
       Bd.out = View{w1, B1, S0, 1, (int)g.out[0]};
       Bd.spec = g.spec; Bd.spec_kind = g.spec_kind; Bd.spec_i = 0; Bd.spec_p = 1; Bd.spec_r = g.L[0];
       Bd.tw = g.tw[0].ptr; Bd.Q = qn; Bd.Rn = (int)(H1 + 1); Bd.In = 1; Bd.done = done;
+      Bd.dcny = dcny;
       if (spart != nullptr) {
         Bd.spart = reinterpret_cast<T*>(spart) + q0 * (H1 + 1);
         Bd.spart_mid = (int)(H1 / 2);
@@ -564,7 +577,7 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
         b_lines = (int64_t)qn * ((H1 + G2) / G2) * G2;
       } else {
         b_lay = LAY_CONTIG;
-        b_lines = (int64_t)qn * Bd.Rn;
+        b_lines = (int64_t)qn * (dcny > 0 ? Bd.Rn - 1 : Bd.Rn);
       }
       HGP_TRY(run((int)(g.L[0] / 2), conv_mode, b_lay, Bd, b_lines));
       if (mid != nullptr) (*mid)(q0, qn, st);
@@ -574,6 +587,7 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
       Cd.out = View{yo, g.out_M, g.out[1], 1, (int)g.out[1]};
       Cd.dot = dvc; Cd.partial = pc;
       Cd.tw = g.tw[1].ptr; Cd.Q = qn; Cd.Rn = (int)((g.out[0] + 1) / 2); Cd.nrows = (int)g.out[0]; Cd.done = done;
+      Cd.dcny = dcny;
       int epi_mode = EPI_OUT;
       if (epi != nullptr) {
         epi_mode = epi->mode;
@@ -1533,6 +1547,8 @@ int hgp_plan_create(int device, int ndim, const int64_t* m, int dtype, int64_t m
   if (ns) P->nstreams = std::max(1, std::min(4, std::atoi(ns)));
   const char* cp = std::getenv("HGP_CHAIN_PCG");
   if (cp) P->chain_pcg = std::atoi(cp) != 0;
+  const char* dn = std::getenv("HGP_DCNY");
+  if (dn) P->dcny_pack = std::atoi(dn) != 0;
   int rc = 0;
   for (int a = 0; a < d && rc == 0; ++a) {
     if (dtype == HGP_F64) {

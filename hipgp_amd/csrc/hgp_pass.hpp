@@ -120,6 +120,9 @@
 #ifndef HGP_MINW_CONTIG_TRI
 #define HGP_MINW_CONTIG_TRI HGP_MINW_CONTIG_LONG
 #endif
+#ifndef HGP_DCNY_CONV
+#define HGP_DCNY_CONV 1
+#endif
 // the G = 4 grouped intermediate in the quad order (LAY_CONTIG_Q; 0: the plain G = 4 order,
 // one column per axis-0 block, LAY_CONTIG_G)
 #ifndef HGP_QUAD
@@ -177,6 +180,11 @@ struct PassDesc {
   int nrows;                  // LAY_RP: real rows per RHS (the pair (2r, 2r+1) needs 2r+1 < nrows)
   int grp;                    // LAY_CONTIG_G: columns per group G (r_stride = S0, the group's pitch / G)
   int seg_ws;                 // LAY_SEG_*: ranks the rows are split over
+  // 2-D K / C^-1 with the plain column-major intermediate (G = 1): the real DC (c = 0) and
+  // Nyquist (c = dcny = H1 / 2) compact columns packed as one complex column at c = 0 (row passes
+  // k_row_fwd_t / k_row_inv_t), so the axis-0 pass runs H1 lines per RHS instead of H1 + 1 (a
+  // C2 chunk of 8 RHS: 8192 lines = exactly two rounds of resident blocks).  0: not packed.
+  int dcny;
   const int* done;            // optional device flag: skip the pass when *done != 0
   // CONV passes: spectral dot of the transformed line with itself weighted by the real
   // spectrum, sum_k S_k |X_k|^2 = <x, op x> by Parseval (the crop is exact: x is zero outside
@@ -402,13 +410,15 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
   } else if constexpr (LAY == LAY_CONTIG || LAY == LAY_SEG_C) {
     // RHS-fastest: the C lines of a block are the same column r of C right-hand sides, so
     // they share one spectrum line; the XCD remap keeps the blocks of one column (all its
-    // RHS) on one XCD, so the line is fetched into that L2 once
+    // RHS) on one XCD, so the line is fetched into that L2 once.  Packed DC / Nyquist
+    // (d.dcny > 0): Rn - 1 lines per RHS, line r >= dcny is column r + 1
     const int64_t line = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * C + l;
     r = (int)(line / d.Q);
     q = (int)(line - (int64_t)r * d.Q);
     i = 0;
-    valid = r < d.Rn;
+    valid = r < (d.dcny > 0 ? d.Rn - 1 : d.Rn);
     if (!valid) { q = 0; r = 0; }
+    if (d.dcny > 0 && r >= d.dcny) ++r;
   } else {
     const int64_t line = (int64_t)blockIdx.x * C + l;
     q = (int)(line / d.Rn);
@@ -637,34 +647,70 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
     // transforms run interleaved over one exchange image (hgp_fft.hpp fft_line2)
     if constexpr (MODE == PASS_CONV) {
       fft_line2<T, H, P, -1, LSTRIDE, Cfg::WAVE, (HGP_SEQ_PASS == 2 || ((HGP_SEQ_PASS || HGP_SEQ_MULTIWAVE || (HGP_SEQ_PASS_2048 && TT == 128)) && !Cfg::WAVE))>(va, vb, lds, lbase, t, tab);
-      // the line's real spectrum, loaded after the forward transforms (no registers held across
-      // them); L2-resident: every line of a block shares it (RHS-fastest map, XCD-grouped)
-      T sre1[P];
-      if constexpr (BUF) {
-        const BufRsrc rspec = buf_rsrc(sb, 0x7fffffffu);
+      // the packed DC + i Nyquist line (wave-uniform: one line per wave where the host packs):
+      // z = a + i b with a, b the two real columns, each with its own real spectrum S0 / S1:
+      // A = (Z + conj Z(-f)) / 2, B = (Z - conj Z(-f)) / 2i (herm_split through this line's LDS
+      // image, one frequency half at a time), Y = S0 A + i S1 B, the spectral dot
+      // sum S0 |A|^2 + S1 |B|^2 (both columns have Hermitian weight 1).  The spectra are read per
+      // position here, so this rarely taken branch (one line in H1) holds no more registers than
+      // the common one.
+      const bool packed = HGP_DCNY_CONV && (LAY == LAY_CONTIG) && Cfg::WAVE && d.dcny > 0 && r == 0 && valid;
+      if constexpr (HGP_DCNY_CONV && (LAY == LAY_CONTIG) && Cfg::WAVE) {
+        if (packed) {
+          const T* sn = sb + (int64_t)d.dcny * d.spec_r;      // the Nyquist column's spectrum
 #pragma unroll
-        for (int k = 0; k < P; ++k) {
-          sre[k] = buf_ld<T>(rspec, (uint32_t)so * (uint32_t)sizeof(T), (uint32_t)(TT * k * sp) * (uint32_t)sizeof(T));
-          sre1[k] = buf_ld<T>(rspec, (uint32_t)so * (uint32_t)sizeof(T), (uint32_t)((H + TT * k) * sp) * (uint32_t)sizeof(T));
-        }
-      } else {
+          for (int half = 0; half < 2; ++half) {
+            xsync<true>();
 #pragma unroll
-        for (int k = 0; k < P; ++k) {
-          sre[k] = sb[so + TT * k * sp];
-          sre1[k] = sb[so + (H + TT * k) * sp];
+            for (int k = 0; k < P; ++k) lds[lds_phys(lbase + t + TT * k)] = half ? vb[k] : va[k];
+            xsync<true>();
+#pragma unroll
+            for (int k = 0; k < P; ++k) {
+              const int p = t + TT * k;
+              const int pp = (half == 0) ? herm_partner0<H>(p) : (H - 1 - p);
+              const T s0 = sb[so + (half * H + TT * k) * sp];
+              const T s1 = sn[so + (half * H + TT * k) * sp];
+              C2<T> A, B;
+              herm_split<T>(half ? vb[k] : va[k], lds[lds_phys(lbase + pp)], A, B);
+              sdot += s0 * (A.x * A.x + A.y * A.y) + s1 * (B.x * B.x + B.y * B.y);
+              const C2<T> y = herm_join<T>(cscale<T>(A, s0), cscale<T>(B, s1));
+              if (half) vb[k] = y; else va[k] = y;
+            }
+          }
+          xsync<true>();   // partners read before the inverse transform reuses the image
+          if (d.spart == nullptr) sdot = 0;
         }
       }
-      if (d.spart != nullptr) {   // uniform: spectral dot sum_k S_k |X_k|^2 of this line
+      if (!packed) {
+        // the line's real spectrum, loaded after the forward transforms (no registers held across
+        // them); L2-resident: every line of a block shares it (RHS-fastest map, XCD-grouped)
+        T sre1[P];
+        if constexpr (BUF) {
+          const BufRsrc rspec = buf_rsrc(sb, 0x7fffffffu);
+#pragma unroll
+          for (int k = 0; k < P; ++k) {
+            sre[k] = buf_ld<T>(rspec, (uint32_t)so * (uint32_t)sizeof(T), (uint32_t)(TT * k * sp) * (uint32_t)sizeof(T));
+            sre1[k] = buf_ld<T>(rspec, (uint32_t)so * (uint32_t)sizeof(T), (uint32_t)((H + TT * k) * sp) * (uint32_t)sizeof(T));
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < P; ++k) {
+            sre[k] = sb[so + TT * k * sp];
+            sre1[k] = sb[so + (H + TT * k) * sp];
+          }
+        }
+        if (d.spart != nullptr) {   // uniform: spectral dot sum_k S_k |X_k|^2 of this line
+#pragma unroll
+          for (int k = 0; k < P; ++k) {
+            sdot += sre[k] * (va[k].x * va[k].x + va[k].y * va[k].y);
+            sdot += sre1[k] * (vb[k].x * vb[k].x + vb[k].y * vb[k].y);
+          }
+        }
 #pragma unroll
         for (int k = 0; k < P; ++k) {
-          sdot += sre[k] * (va[k].x * va[k].x + va[k].y * va[k].y);
-          sdot += sre1[k] * (vb[k].x * vb[k].x + vb[k].y * vb[k].y);
+          va[k] = mk<T>(va[k].x * sre[k], va[k].y * sre[k]);
+          vb[k] = mk<T>(vb[k].x * sre1[k], vb[k].y * sre1[k]);
         }
-      }
-#pragma unroll
-      for (int k = 0; k < P; ++k) {
-        va[k] = mk<T>(va[k].x * sre[k], va[k].y * sre[k]);
-        vb[k] = mk<T>(vb[k].x * sre1[k], vb[k].y * sre1[k]);
       }
     } else if constexpr (MODE == PASS_CONVC) {
       fft_line2<T, H, P, -1, LSTRIDE, Cfg::WAVE, (HGP_SEQ_PASS == 2 || ((HGP_SEQ_PASS || HGP_SEQ_MULTIWAVE || (HGP_SEQ_PASS_2048 && TT == 128)) && !Cfg::WAVE))>(va, vb, lds, lbase, t, tab);
@@ -748,6 +794,8 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
           const int col = d.spart_div > 1 ? r / d.spart_div : r;
           const T w = (d.spart_mid < 0 || col == 0 || col == d.spart_mid) ? (T)1 : (T)2;
           reinterpret_cast<T*>(d.spart)[(int64_t)q * d.Rn + r] = w * s;
+          // packed: the Nyquist column's dot is in column 0's; its own slot reads 0
+          if (d.dcny > 0 && r == 0) reinterpret_cast<T*>(d.spart)[(int64_t)q * d.Rn + d.dcny] = (T)0;
         }
       }
     } else if constexpr (MODE == PASS_CONV) {

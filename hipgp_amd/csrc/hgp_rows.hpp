@@ -177,7 +177,8 @@ __device__ __forceinline__ int row_block_id() {
 template <typename T, int H, int P, int G, bool SEQ = false>
 __device__ __forceinline__ void row_fwd_tail(C2<T> (&va)[P], C2<T> (&vb)[P],
                                              C2<T>* lds, const C2<T>* tab, const C2<T>* __restrict__ twg, int t,
-                                             int l, int lbase, C2<T>* W, int64_t S0, int row0, int nrow_blk) {
+                                             int l, int lbase, C2<T>* W, int64_t S0, int row0, int nrow_blk,
+                                             bool dcny = false) {
   using Cfg = RowTCfg<T, H, G>;
   constexpr int TT = Cfg::TT, C = Cfg::C, PITCH = Cfg::PITCH, NCH = Cfg::NCH, CHC = Cfg::CHC, SEG = Cfg::SEG;
   static_assert(P == Cfg::P, "row_fwd_tail: P");
@@ -202,6 +203,14 @@ __device__ __forceinline__ void row_fwd_tail(C2<T> (&va)[P], C2<T> (&vb)[P],
       const int pp = (half == 0) ? herm_partner0<H>(p) : (H - 1 - p);
       const C2<T> zp = lds[lds_phys(lbase + pp)];
       herm_split<T>(v[k], zp, A[k], B[k]);
+    }
+    if constexpr (half == 0) {
+      // packed DC / Nyquist (PassDesc::dcny): both real, both held by thread 0 (positions 0 and
+      // H / 2 = TT P / 2): column 0 carries DC + i Nyquist (column H / 2 is stored but unread)
+      if (dcny && t == 0) {
+        A[0] = mk<T>(A[0].x, A[P / 2].x);
+        B[0] = mk<T>(B[0].x, B[P / 2].x);
+      }
     }
     __syncthreads();   // every group done with its exchange image: the tile overlays them
 #pragma unroll
@@ -328,7 +337,7 @@ __global__ __launch_bounds__((RowTCfg<T, H, G>::THREADS), (RowTCfg<T, H, G>::MIN
   C2<T>* W = reinterpret_cast<C2<T>*>(d.out.ptr) + (int64_t)q * d.out.q_stride;
   const int row0 = 2 * rb * C;                     // first row of this block's tile
   const int nrow_blk = d.nrows - row0 < 2 * C ? d.nrows - row0 : 2 * C;
-  row_fwd_tail<T, H, P, G>(va, vb, lds, tab, twg, t, l, lbase, W, d.out.r_stride, row0, nrow_blk);
+  row_fwd_tail<T, H, P, G>(va, vb, lds, tab, twg, t, l, lbase, W, d.out.r_stride, row0, nrow_blk, d.dcny > 0);
 }
 
 // Column-major compact half spectra -> real row pairs (crop), optional fused dot.
@@ -510,8 +519,16 @@ __global__ __launch_bounds__((RowTCfg<T, H, G>::THREADS), (RowTCfg<T, H, G>::MIN
       else { cj = p >= H / 2; c = cj ? H - 1 - p : p; }
       if (NCH == 1 || (c >= ca && c < cb)) {
         const int li = l < C ? l : 0;
-        C2<T> A = lds[(c - ca) * PITCH + 2 * li];
-        C2<T> B = lds[(c - ca) * PITCH + 2 * li + 1];
+        // packed DC / Nyquist (PassDesc::dcny, NCH = 1): positions 0 and H / 2 of the even half
+        // both read column 0, the DC as its real and the Nyquist as its imaginary part
+        const bool pk = NCH == 1 && d.dcny > 0 && half == 0 && (p == 0 || p == H / 2);
+        const int cc = pk ? 0 : c;
+        C2<T> A = lds[(cc - ca) * PITCH + 2 * li];
+        C2<T> B = lds[(cc - ca) * PITCH + 2 * li + 1];
+        if (pk) {
+          A = p == 0 ? mk<T>(A.x, (T)0) : mk<T>(A.y, (T)0);
+          B = p == 0 ? mk<T>(B.x, (T)0) : mk<T>(B.y, (T)0);
+        }
         if (!has2) B = mk<T>(0, 0);
         if (cj) { A.y = -A.y; B.y = -B.y; }
         v[k] = herm_join<T>(A, B);
@@ -658,7 +675,8 @@ __global__ __launch_bounds__((RowTCfg<T, H, G>::THREADS), (RowTCfg<T, H, G>::MIN
         fb[k] = fa[k];
       }
       __syncthreads();   // ys consumed: the exchange images overlay it
-      row_fwd_tail<T, H, P, G, HGP_RF_SEQ>(fa, fb, lds, tab, twg, t, l, lbase, const_cast<C2<T>*>(W), S0, row0, nrow_blk);
+      row_fwd_tail<T, H, P, G, HGP_RF_SEQ>(fa, fb, lds, tab, twg, t, l, lbase, const_cast<C2<T>*>(W), S0, row0, nrow_blk,
+                                           d.dcny > 0);
     }
     return;
   }

@@ -102,7 +102,7 @@ def _nine_run_bound(fx, alt9, name, j, got, factor=10):
     """|got - ref| <= factor x max over the nine self-perturbed reference runs of G19_fine_alt
     (tests/golden/make_golden_fit_c3_alt.py) of |alt - ref|, + 1e-9 |ref|"""
     ref = fx[f"fine_{name}_steps"][j]
-    e_alt = max(np.linalg.norm(alt9[f"alt{a}_{name}_steps"][j] - ref) for a in range(9))
+    e_alt = max(np.linalg.norm(alt9[f"alt{a}_{name}_diff"][j].astype(np.float64)) for a in range(9))
     e_me = np.linalg.norm(got - ref)
     print("fine", name, "step", j, "|me - ref| / |ref|", e_me / np.linalg.norm(ref), "nine-run spread", e_alt / np.linalg.norm(ref))
     assert e_me <= factor * e_alt + 1e-9 * np.linalg.norm(ref), (name, j, e_me, e_alt)

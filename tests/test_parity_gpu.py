@@ -9,6 +9,8 @@ CPU oracle.  Tolerances:
               own spread over nine self-perturbed re-runs (tests/golden/make_golden_clamp_alt.py),
               plus the true-residual check
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -418,3 +420,41 @@ def test_shape_sweep_vs_oracle(dims, tag):
         if not np.isfinite(e32):    # the fp32 reference itself hit 0/0 on a nearly exhausted Krylov space
             e32 = 2.5e-5
         assert e <= 4 * e32 + 1e-6, (e, e32)
+
+
+@pytest.mark.parametrize("dims,dt,tol", [((400, 300), torch.float64, 1e-10), ((1024, 1000), torch.float32, 2e-6),
+                                         ((300, 900), torch.float32, 2e-6)],
+                         ids=["f64_400x300", "f32_1024x1000", "f32_300x900"])
+def test_dcny_packed_columns(dims, dt, tol):
+    """Round 5: the 2-D K / C^-1 intermediate packs its real DC and Nyquist compact columns as one
+    complex column (PassDesc::dcny: one axis-0 line fewer per RHS, split again by Hermitian
+    symmetry inside the axis-0 pass).  The same operator: against a plan without the packing
+    (HGP_DCNY=0) to rounding, K against the oracle, and the fused PCG (spectral dots of the
+    packed line) against the unpacked plan's."""
+    from hipgp_amd import _lib
+    from hipgp_amd.plan import ToeplitzPlan
+    grids = [np.linspace(-1, 1, m) for m in dims]
+    col_np = zo.toeplitz_column(grids, lambda x, y: zo.kernel_eval("matern", x, y, (1., .05), nu=1.5), 1e-2)
+    col = torch.tensor(col_np, device=DEV, dtype=dt)
+    plans = {}
+    for pk in ("1", "0"):
+        os.environ["HGP_DCNY"] = pk
+        try:
+            P = ToeplitzPlan(dims, dt, DEV)
+        finally:
+            del os.environ["HGP_DCNY"]
+        P.set_column(col)
+        plans[pk] = P
+    M = int(np.prod(dims))
+    g = torch.Generator(device=DEV).manual_seed(13)
+    v = torch.randn(5, M, device=DEV, generator=g, dtype=torch.float64).to(dt)
+    for op in (_lib.OP_K, _lib.OP_CINV):
+        a, b = plans["1"].apply(op, v).double(), plans["0"].apply(op, v).double()
+        err = float((a - b).abs().max() / b.abs().max())
+        assert err < tol, (op, err)
+    ref = zo.ToeplitzOracle(col_np, dims).matmul_K(v.double().cpu().numpy())
+    got = plans["1"].apply(_lib.OP_K, v).double().cpu().numpy()
+    assert float(np.max(np.abs(got - ref)) / np.max(np.abs(ref))) < (1e-9 if dt == torch.float64 else 1e-5)
+    xa = plans["1"].pcg(v, 10, 1e-30, precond=True).double()
+    xb = plans["0"].pcg(v, 10, 1e-30, precond=True).double()
+    assert float((xa - xb).norm() / xb.norm()) < (1e-9 if dt == torch.float64 else 1e-4)
