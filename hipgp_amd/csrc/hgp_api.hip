@@ -132,7 +132,9 @@ struct hgp_plan {
   bool cg_active = false;
   int cg_rs_par = 0;                      // which of the two rs buffers the next step reads
   int cg_step = 0;                        // steps queued since hgp_pcg_begin
-  int64_t ws_budget = (int64_t)1 << 30;
+  // 2-D RHS-chunk budget: 2 GiB measured best at C4 (PCG(20) 213 -> 205 ms vs 1 GiB; C3 and the C4
+  // single ops flat; profiles/r5_i_ws_budget.txt)
+  int64_t ws_budget = (int64_t)2 << 30;
   int64_t ws3_budget = (int64_t)4 << 30;  // 3-D default (hgp_plan_create: from the device's memory)
   bool ws_explicit = false;               // HGP_WS_MB given: the byte budget alone sets the chunks
   // 2-D operators run their RHS chunks on `nstreams` streams (the plan's own + side streams),

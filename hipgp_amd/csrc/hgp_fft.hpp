@@ -218,17 +218,19 @@ template <typename T, int H> struct PFor {
 template <int H, int P> struct Stages {
   static constexpr bool TRI = !is_pow2(H);
   static constexpr int RMAX = P < 16 ? P : 16;   // in-register DFTs up to 16 points (P = 32: two per stage)
+  // tri lengths: radix-4 stages with P = 12 (three butterflies a thread), radix-8 with P = 24
+  static constexpr int RTRI = P % 8 == 0 ? 8 : 4;
   static constexpr int last_tri() { return 3 * (H / 3 >= 4 ? 4 : H / 3); }
   static constexpr int count() {
     if (!TRI) { int n = 0, rem = H; while (rem > 1) { int r = rem >= RMAX ? RMAX : rem; rem /= r; ++n; } return n; }
     int n = 1, rem = H / last_tri();
-    while (rem > 1) { rem /= (rem >= 4 ? 4 : rem); ++n; }
+    while (rem > 1) { rem /= (rem >= RTRI ? RTRI : rem); ++n; }
     return n;
   }
   static constexpr int radix(int s) {
     if (!TRI) { int rem = H; for (int i = 0; i < s; ++i) rem /= (rem >= RMAX ? RMAX : rem); return rem >= RMAX ? RMAX : rem; }
     int rem = H / last_tri(), i = 0;
-    while (rem > 1) { const int r = rem >= 4 ? 4 : rem; if (i == s) return r; rem /= r; ++i; }
+    while (rem > 1) { const int r = rem >= RTRI ? RTRI : rem; if (i == s) return r; rem /= r; ++i; }
     return last_tri();
   }
   static constexpr int ns(int s) { int v = 1; for (int i = 0; i < s; ++i) v *= radix(i); return v; }

@@ -220,8 +220,20 @@ constexpr int LDS_CAP = 160 * 1024;
 // cg_np <= CG_LOADS x THREADS, else it passes cg_coef from a k_cg_alpha / k_cg_beta launch)
 constexpr int CG_LOADS = 8;
 
+// points per thread of the fp32 contiguous-line passes at tri lengths of >= 1536 points
+// (HGP_TRI_P_CONV; 12 = PFor's): 24 runs radix-8 stages (three exchanges for a 6144-point half
+// transform instead of five radix-4 ones) with lines of TT = H / 24 threads
+#ifndef HGP_TRI_P_CONV
+#define HGP_TRI_P_CONV 24
+#endif
+template <typename T, int H, int LAY> struct PassP {
+  static constexpr bool CONTIG_LINE = LAY == LAY_CONTIG || LAY == LAY_CONTIG_G || LAY == LAY_CONTIG_Q;
+  static constexpr int v = (std::is_same<T, float>::value && is_tri(H) && H >= 1536 && CONTIG_LINE)
+                               ? HGP_TRI_P_CONV : PFor<T, H>::v;
+};
+
 template <typename T, int H, int LAY> struct PassCfg {
-  static constexpr int P = PFor<T, H>::v;
+  static constexpr int P = PassP<T, H, LAY>::v;
   static constexpr int TT = H / P;
   // LDS: exchange image of C lines (H complex each, 1 pad slot per 16) + twiddle half table
   static constexpr int ex_elems(int c) { return c * H + ((c * H) >> 4); }
@@ -262,13 +274,13 @@ template <typename T, int H, int LAY> struct PassCfg {
   static constexpr int MINW_LDS = (BLOCKS_BY_LDS * WAVES_PER_BLOCK) / 4;
   static constexpr int MINW_AUTO = MINW_LDS < 1 ? 1 : (MINW_LDS > 4 ? 4 : MINW_LDS);
   // (3 waves per SIMD only for lines of 4 waves: 3 whole blocks per CU)
-  static constexpr int MINW_CL = (!is_pow2(H) && TT >= 256) ? HGP_MINW_CONTIG_TRI
+  static constexpr int MINW_CL = (P == 24) ? 3 : (!is_pow2(H) && TT >= 256) ? HGP_MINW_CONTIG_TRI
                                  : (H >= 4096 && TT == 256) ? HGP_MINW_CONTIG_4096
                                  : H >= 2048 ? HGP_MINW_CONTIG_LONG : H <= 512 ? HGP_MINW_CONTIG_SHORT : HGP_MINW_CONTIG;
   // a block's waves must fit the SIMDs' share at once: >= WAVES_PER_BLOCK / 4 waves per SIMD
   static constexpr int MINW_BLK = (WAVES_PER_BLOCK + 3) / 4;
   // quad-order blocks of 4096-point lines (4 waves each): HGP_MINW_CONTIG_Q4096 waves per SIMD
-  static constexpr int MINW_Q = TT == 256 ? HGP_MINW_CONTIG_Q4096 : MINW_CL;
+  static constexpr int MINW_Q = P == 24 ? 3 : TT == 256 ? HGP_MINW_CONTIG_Q4096 : MINW_CL;
   static constexpr int MINW_SET = lay_grp(LAY) ? (MINW_CL > MINW_BLK ? MINW_CL : MINW_BLK)
                                  : lay_smap(LAY) ? (TT >= 16 ? HGP_MINW_STRIDED : HGP_MINW_STRIDED_SMALL)
                                  : LAY == LAY_CONTIG_Q ? (MINW_Q > MINW_BLK ? MINW_Q : MINW_BLK)
