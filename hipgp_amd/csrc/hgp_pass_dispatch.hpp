@@ -119,8 +119,10 @@ static PassGeom geom_h(int lay) {
   }
 
 template <typename T, int H, int EPI, int G>
-static hipError_t launch_rowt_inv(const PassDesc& d, int64_t nb, hipStream_t s) {
-  using Cfg = RowTCfg<T, H, G>;
+static hipError_t launch_rowt_inv(const PassDesc& d, hipStream_t s) {
+  using Cfg = RowTCfg<T, H, G, true>;
+  const int64_t nb = (int64_t)d.Q * ((d.Rn + Cfg::C - 1) / Cfg::C);
+  if (nb <= 0) return hipSuccess;
   static bool attr_set = false;   // opt in to > 64 KB dynamic LDS once per instance
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)k_row_inv_t<T, H, EPI, G>,
@@ -135,16 +137,17 @@ static hipError_t launch_rowt_inv(const PassDesc& d, int64_t nb, hipStream_t s) 
 template <typename T, int H, int G>
 static hipError_t launch_rowt_g(int inv, int epi, const PassDesc& d, hipStream_t s) {
   using Cfg = RowTCfg<T, H, G>;
-  if constexpr (Cfg::LDS > LDS_CAP) return hipErrorNotSupported;   // e.g. fp64 rows of H = 8192
+  if constexpr (Cfg::LDS > LDS_CAP || RowTCfg<T, H, G, true>::LDS > LDS_CAP)
+    return hipErrorNotSupported;   // e.g. fp64 rows of H = 8192
+  if (inv) {
+    if (epi == EPI_XR) return launch_rowt_inv<T, H, EPI_XR, G>(d, s);
+    if (epi == EPI_R) return launch_rowt_inv<T, H, EPI_R, G>(d, s);
+    if (epi == EPI_XP) return launch_rowt_inv<T, H, EPI_XP, G>(d, s);
+    if (epi == EPI_RF) return launch_rowt_inv<T, H, EPI_RF, G>(d, s);
+    return launch_rowt_inv<T, H, EPI_OUT, G>(d, s);
+  }
   const int64_t nb = (int64_t)d.Q * ((d.Rn + Cfg::C - 1) / Cfg::C);
   if (nb <= 0) return hipSuccess;
-  if (inv) {
-    if (epi == EPI_XR) return launch_rowt_inv<T, H, EPI_XR, G>(d, nb, s);
-    if (epi == EPI_R) return launch_rowt_inv<T, H, EPI_R, G>(d, nb, s);
-    if (epi == EPI_XP) return launch_rowt_inv<T, H, EPI_XP, G>(d, nb, s);
-    if (epi == EPI_RF) return launch_rowt_inv<T, H, EPI_RF, G>(d, nb, s);
-    return launch_rowt_inv<T, H, EPI_OUT, G>(d, nb, s);
-  }
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)k_row_fwd_t<T, H, G>, hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS);
@@ -199,17 +202,23 @@ hipError_t launch_linet(int H, int inv, const PassDesc& d, hipStream_t s) {
   return hipErrorInvalidValue;
 }
 
+// pairs / threads per block of the ROW-INVERSE pass (its per-block partials and epilogue loads)
 template <typename T, int H>
-static int rowt_pairs_h(int grouped) { return grouped ? RowTCfg<T, H, RowGroup<T, H>::G>::C : RowTCfg<T, H>::C; }
+static int rowt_pairs_h(int grouped) {
+  return grouped ? RowTCfg<T, H, RowGroup<T, H>::G, true>::C : RowTCfg<T, H, 1, true>::C;
+}
 
 template <typename T, int H>
 static int rowt_threads_h(int grouped) {
-  return grouped ? RowTCfg<T, H, RowGroup<T, H>::G>::THREADS : RowTCfg<T, H>::THREADS;
+  return grouped ? RowTCfg<T, H, RowGroup<T, H>::G, true>::THREADS : RowTCfg<T, H, 1, true>::THREADS;
 }
 
 template <typename T, int H>
 static int rowt_fits_h(int grouped) {
-  return (grouped ? RowTCfg<T, H, RowGroup<T, H>::G>::LDS : RowTCfg<T, H>::LDS) <= LDS_CAP ? 1 : 0;
+  constexpr int G = RowGroup<T, H>::G;
+  const int lf = grouped ? RowTCfg<T, H, G>::LDS : RowTCfg<T, H>::LDS;
+  const int li = grouped ? RowTCfg<T, H, G, true>::LDS : RowTCfg<T, H, 1, true>::LDS;
+  return (lf <= LDS_CAP && li <= LDS_CAP) ? 1 : 0;
 }
 
 template <typename T, int H>

@@ -90,6 +90,21 @@ __device__ __forceinline__ void row_stagger() {
 #ifndef HGP_ROWG_TRI
 #define HGP_ROWG_TRI 4
 #endif
+// pairs per block of the ROW-INVERSE pass over those grouped 3 * 2^k rows (0: 8 / G).  Two
+// 6144-point pairs (106 KB of LDS) leave one 16-wave block per CU, whose load / transform / store
+// phases then run in step; one pair is a 53 KB block, three per CU, at 64-B column segments (the
+// two blocks of a 128-B unit land in the same XCD, XCD_INV).  C4 (profiles/r5_l_tri_pairs.txt):
+// R^T row inverse 5.96 -> 3.70 ms, R row inverse 2.77 -> 1.83 ms.  The forward pass keeps two
+// pairs: its partial-unit WRITES do not merge (R^T row forward 2.63 -> 3.96 ms, R 5.81 -> 9.13).
+#ifndef HGP_ROWG_PAIRS_TRI_INV
+#define HGP_ROWG_PAIRS_TRI_INV 1
+#endif
+// threads per ROW-INVERSE block of the ungrouped 3 * 2^k rows longer than a wave (0: as the
+// forward pass, HGP_ROWT_PAIRS_BIG pairs of 64 threads' worth = 1024 threads, ~104 KB of LDS,
+// one block per CU)
+#ifndef HGP_ROWT_THREADS_TRI_INV
+#define HGP_ROWT_THREADS_TRI_INV 0
+#endif
 template <typename T, int H> struct RowGroup {
   static constexpr int G = !std::is_same<T, float>::value ? 1
                          : !is_pow2(H) ? (H >= 6144 ? HGP_ROWG_TRI : 1)
@@ -102,7 +117,7 @@ template <typename T, int H> struct RowGroup {
 #ifndef HGP_ROW_P_LONG
 #define HGP_ROW_P_LONG 0
 #endif
-template <typename T, int H, int G = 1> struct RowTCfg {
+template <typename T, int H, int G = 1, bool INV = false> struct RowTCfg {
   static constexpr int P = (std::is_same<T, float>::value && is_pow2(H) && H >= 4096 && HGP_ROW_P_LONG > 0)
                                ? HGP_ROW_P_LONG : PFor<T, H>::v;
   static constexpr int TT = H / P;
@@ -116,9 +131,11 @@ template <typename T, int H, int G = 1> struct RowTCfg {
   static constexpr int area(int c) { return ex_elems(c) > tile_elems(c) ? ex_elems(c) : tile_elems(c); }
   static constexpr int lds_bytes_for(int c) { return area(c) * (int)sizeof(C2<T>) + TwTab<T, H>::BYTES; }
   static constexpr int c_pairs() {
-    if (G > 1) return (H >= 4096 && HGP_ROWG_PAIRS_LONG > 0) ? HGP_ROWG_PAIRS_LONG
+    if (G > 1) return (INV && !is_pow2(H) && HGP_ROWG_PAIRS_TRI_INV > 0) ? HGP_ROWG_PAIRS_TRI_INV
+                      : (H >= 4096 && HGP_ROWG_PAIRS_LONG > 0) ? HGP_ROWG_PAIRS_LONG
                                                               : 8 / G;   // 2C rows x G columns = 128 B (fp32)
     int c = (TT > 64 ? HGP_ROWT_PAIRS_BIG : HGP_ROWT_PAIRS) * 64 / TT;   // 512 threads at the default
+    if (INV && !is_pow2(H) && TT > 64 && HGP_ROWT_THREADS_TRI_INV > 0) c = HGP_ROWT_THREADS_TRI_INV / TT;
     if (c < 1) c = 1;
     if (c > 64) c = 64;                            // tiny rows: cap the tile height
     while (c > 1 && (c * TT > 1024 || lds_bytes_for(c) > LDS_CAP)) c >>= 1;
@@ -174,12 +191,11 @@ __device__ __forceinline__ int row_block_id() {
 // twiddled odd half, both halves' FFTs,
 // Hermitian split, and the transposed half spectra out to the intermediate (column pitch S0,
 // grouped by G).  Needs the twiddle table staged in `tab`; uses the LDS area from `lds`.
-template <typename T, int H, int P, int G, bool SEQ = false>
+template <typename T, int H, int P, int G, bool SEQ = false, typename Cfg = RowTCfg<T, H, G>>
 __device__ __forceinline__ void row_fwd_tail(C2<T> (&va)[P], C2<T> (&vb)[P],
                                              C2<T>* lds, const C2<T>* tab, const C2<T>* __restrict__ twg, int t,
                                              int l, int lbase, C2<T>* W, int64_t S0, int row0, int nrow_blk,
                                              bool dcny = false) {
-  using Cfg = RowTCfg<T, H, G>;
   constexpr int TT = Cfg::TT, C = Cfg::C, PITCH = Cfg::PITCH, NCH = Cfg::NCH, CHC = Cfg::CHC, SEG = Cfg::SEG;
   static_assert(P == Cfg::P, "row_fwd_tail: P");
 #pragma unroll
@@ -415,8 +431,8 @@ __device__ __forceinline__ void cg_fix_x(int nrow, int out_len, T* __restrict__ 
 }
 
 template <typename T, int H, int EPI = EPI_OUT, int G = 1>
-__global__ __launch_bounds__((RowTCfg<T, H, G>::THREADS), (RowTCfg<T, H, G>::MINW)) void k_row_inv_t(const PassDesc d) {
-  using Cfg = RowTCfg<T, H, G>;
+__global__ __launch_bounds__((RowTCfg<T, H, G, true>::THREADS), (RowTCfg<T, H, G, true>::MINW)) void k_row_inv_t(const PassDesc d) {
+  using Cfg = RowTCfg<T, H, G, true>;
   constexpr int P = Cfg::P, TT = Cfg::TT, C = Cfg::C, PITCH = Cfg::PITCH, NCH = Cfg::NCH, CHC = Cfg::CHC;
   constexpr int SEG = Cfg::SEG;
   // staged rows (2C x out_len <= 2C x H values) + two wave-sum areas fit the LDS area
@@ -675,7 +691,7 @@ __global__ __launch_bounds__((RowTCfg<T, H, G>::THREADS), (RowTCfg<T, H, G>::MIN
         fb[k] = fa[k];
       }
       __syncthreads();   // ys consumed: the exchange images overlay it
-      row_fwd_tail<T, H, P, G, HGP_RF_SEQ>(fa, fb, lds, tab, twg, t, l, lbase, const_cast<C2<T>*>(W), S0, row0, nrow_blk,
+      row_fwd_tail<T, H, P, G, HGP_RF_SEQ, Cfg>(fa, fb, lds, tab, twg, t, l, lbase, const_cast<C2<T>*>(W), S0, row0, nrow_blk,
                                            d.dcny > 0);
     }
     return;
