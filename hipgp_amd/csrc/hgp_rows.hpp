@@ -101,9 +101,17 @@ __device__ __forceinline__ void row_stagger() {
 #endif
 // threads per ROW-INVERSE block of the ungrouped 3 * 2^k rows longer than a wave (0: as the
 // forward pass, HGP_ROWT_PAIRS_BIG pairs of 64 threads' worth = 1024 threads, ~104 KB of LDS,
-// one block per CU)
+// one block per CU).  512: ~52 KB, three blocks per CU (C3 R^T row inverse 11.9 -> 9.0 ms, op
+// 30.3 -> 27.8 ms; C2 R^T 1.23 -> 1.17 ms; profiles/r5_n_tri_inv_threads.txt).  HGP_ROWT_THREADS_
+// TRI_FWD: the same for the forward pass (0: 1024), only where the block's column segments stay
+// >= 64 B: its partial-segment WRITES do not merge (C3, 3072-point rows at 2 pairs = 32 B: R^T row
+// forward 4.82 -> 11.9 ms; C2, 1536-point rows at 4 pairs = 64 B: 0.203 -> 0.151 ms, R 0.455 ->
+// 0.324 ms; profiles/r5_o_tri_fwd_threads.txt)
 #ifndef HGP_ROWT_THREADS_TRI_INV
-#define HGP_ROWT_THREADS_TRI_INV 0
+#define HGP_ROWT_THREADS_TRI_INV 512
+#endif
+#ifndef HGP_ROWT_THREADS_TRI_FWD
+#define HGP_ROWT_THREADS_TRI_FWD 512
 #endif
 template <typename T, int H> struct RowGroup {
   static constexpr int G = !std::is_same<T, float>::value ? 1
@@ -136,6 +144,9 @@ template <typename T, int H, int G = 1, bool INV = false> struct RowTCfg {
                                                               : 8 / G;   // 2C rows x G columns = 128 B (fp32)
     int c = (TT > 64 ? HGP_ROWT_PAIRS_BIG : HGP_ROWT_PAIRS) * 64 / TT;   // 512 threads at the default
     if (INV && !is_pow2(H) && TT > 64 && HGP_ROWT_THREADS_TRI_INV > 0) c = HGP_ROWT_THREADS_TRI_INV / TT;
+    if (!INV && !is_pow2(H) && TT > 64 && HGP_ROWT_THREADS_TRI_FWD > 0 &&
+        (HGP_ROWT_THREADS_TRI_FWD / TT) * 2 * (int)sizeof(C2<T>) >= 64)
+      c = HGP_ROWT_THREADS_TRI_FWD / TT;
     if (c < 1) c = 1;
     if (c > 64) c = 64;                            // tiny rows: cap the tile height
     while (c > 1 && (c * TT > 1024 || lds_bytes_for(c) > LDS_CAP)) c >>= 1;
