@@ -3,8 +3,8 @@ and the mean-field ELBO / natural gradient at full grid size in fp32, against th
 of the same problem, plus residual checks.  At these sizes the rows are longer than one wave's
 line (16-pair row blocks, the fused PCG epilogues k_row_inv_t<float, 2048 | 4096, EPI_XR | EPI_P>
 with the alpha / beta mid-pass), the 4096^2 fp32 twiddles are two-level LDS tables, and the RHS
-run in several workspace chunks over the two streams (the 1 GiB budget: 4 RHS per chunk at
-4096^2 fp32, 2 in fp64).  Nugget 0.1 keeps the problems well conditioned, so fp32 and fp64
+run in several workspace chunks over the two streams (the 2 GiB budget: 8 RHS per chunk at
+4096^2 fp32, 4 in fp64).  Nugget 0.1 keeps the problems well conditioned, so fp32 and fp64
 agree to ~1e-4 (a difference of the implementations, not of the chaos of a clamped solve)."""
 import numpy as np
 import pytest
