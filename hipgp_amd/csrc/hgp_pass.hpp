@@ -220,15 +220,20 @@ constexpr int LDS_CAP = 160 * 1024;
 // cg_np <= CG_LOADS x THREADS, else it passes cg_coef from a k_cg_alpha / k_cg_beta launch)
 constexpr int CG_LOADS = 8;
 
-// points per thread of the fp32 contiguous-line passes at tri lengths of >= 1536 points
-// (HGP_TRI_P_CONV; 12 = PFor's): 24 runs radix-8 stages (three exchanges for a 6144-point half
-// transform instead of five radix-4 ones) with lines of TT = H / 24 threads
+// points per thread of the fp32 contiguous-line passes at tri lengths of >= HGP_TRI_P_CONV_MIN
+// points (HGP_TRI_P_CONV; 12 = PFor's): 24 runs radix-8 stages (three exchanges for a 6144-point
+// half transform instead of five radix-4 ones) with lines of TT = H / 24 threads.  Measured per
+// length (profiles/r5_r_tri_p.txt, R^T conv pass): 6144 (C4) 9.29 -> 7.97 ms; 3072 (C3) 12.37 ->
+// 13.80 ms, i.e. slower; 1536 (C2) 0.554 -> 0.547 ms.  So from 6144 points up.
 #ifndef HGP_TRI_P_CONV
 #define HGP_TRI_P_CONV 24
 #endif
+#ifndef HGP_TRI_P_CONV_MIN
+#define HGP_TRI_P_CONV_MIN 6144
+#endif
 template <typename T, int H, int LAY> struct PassP {
   static constexpr bool CONTIG_LINE = LAY == LAY_CONTIG || LAY == LAY_CONTIG_G || LAY == LAY_CONTIG_Q;
-  static constexpr int v = (std::is_same<T, float>::value && is_tri(H) && H >= 1536 && CONTIG_LINE)
+  static constexpr int v = (std::is_same<T, float>::value && is_tri(H) && H >= HGP_TRI_P_CONV_MIN && CONTIG_LINE)
                                ? HGP_TRI_P_CONV : PFor<T, H>::v;
 };
 
