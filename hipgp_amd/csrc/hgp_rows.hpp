@@ -83,6 +83,12 @@ __device__ __forceinline__ void row_stagger() {
 #ifndef HGP_ROWG_PAIRS_LONG
 #define HGP_ROWG_PAIRS_LONG 0
 #endif
+// the same for the ROW-INVERSE pass alone (0: as the forward pass).  1: 35 KB blocks, four per
+// CU instead of two (C4 row inverse 1.09 -> 1.01 ms, K op 4.48 -> 4.46 ms, PCG(20) 210.6 ->
+// 208 ms on one box; profiles/r5_t_rowinv4096.txt); the forward pass keeps 128-B segments
+#ifndef HGP_ROWG_PAIRS_LONG_INV
+#define HGP_ROWG_PAIRS_LONG_INV 1
+#endif
 // G for the fp32 3 * 2^k rows of >= 6144 points (the 2-D R / R^T of 4096-point axes, L_R = 12288):
 // their row-pair blocks hold 2 pairs (123 KB of LDS), i.e. 32-B column segments with G = 1; G = 4
 // makes them 128 B (C4 R^T 21.0 -> 17.8 ms, R 21.6 -> 18.1 ms: row forward 5.3 -> 2.7 ms, row
@@ -140,6 +146,7 @@ template <typename T, int H, int G = 1, bool INV = false> struct RowTCfg {
   static constexpr int lds_bytes_for(int c) { return area(c) * (int)sizeof(C2<T>) + TwTab<T, H>::BYTES; }
   static constexpr int c_pairs() {
     if (G > 1) return (INV && !is_pow2(H) && HGP_ROWG_PAIRS_TRI_INV > 0) ? HGP_ROWG_PAIRS_TRI_INV
+                      : (INV && is_pow2(H) && H >= 4096 && HGP_ROWG_PAIRS_LONG_INV > 0) ? HGP_ROWG_PAIRS_LONG_INV
                       : (H >= 4096 && HGP_ROWG_PAIRS_LONG > 0) ? HGP_ROWG_PAIRS_LONG
                                                               : 8 / G;   // 2C rows x G columns = 128 B (fp32)
     int c = (TT > 64 ? HGP_ROWT_PAIRS_BIG : HGP_ROWT_PAIRS) * 64 / TT;   // 512 threads at the default

@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--dims", default="256,256,128")
     ap.add_argument("--rhs", type=int, default=25)
     ap.add_argument("--op", default="K", choices=["K", "CINV", "RT", "R"])
+    ap.add_argument("--ell", type=float, default=0.1, help="Matern-5/2 lengthscale of the grid kernel")
     ap.add_argument("--op-only", type=int, default=0, help="only run the op this many times (PMC passes)")
     ap.add_argument("--pcg-only", type=int, default=0,
                     help="only run this many batched PCG(20) solves (the fused iteration's kernels, PMC passes)")
@@ -28,7 +29,7 @@ def main():
     dev = torch.device("cuda", 0)
     dims = [int(v) for v in a.dims.split(",")]
     k = zk.Matern(nu=2.5, dtype=torch.float32)
-    kf = lambda x, y: k.forward(x, y, params=(0.1, 0.1))
+    kf = lambda x, y: k.forward(x, y, params=(a.ell, 0.1))
     grids = [torch.linspace(-.25, .25, m, device=dev) for m in dims]
     T = ToeplitzTensor(grids, kf, batch_shape=(a.rhs,), jitter_val=1e-3)
     plan = T._plan
