@@ -83,6 +83,19 @@ __device__ __forceinline__ void row_stagger() {
 #ifndef HGP_ROWG_PAIRS_LONG
 #define HGP_ROWG_PAIRS_LONG 0
 #endif
+// pairs per ROW-INVERSE block of the grouped 2048-point rows (0: as the forward pass, 8 / G).
+// 2: 35 KB blocks, four per CU (C3 row inverse 2.08 -> 1.92 ms, K op 8.04 -> 8.00 ms, PCG(20)
+// equal; profiles/r5_w_rowinv_small.txt)
+#ifndef HGP_ROWG_PAIRS_2048_INV
+#define HGP_ROWG_PAIRS_2048_INV 2
+#endif
+// pairs per ROW-INVERSE block of the ungrouped power-of-two rows of one wave (TT = 64, the C2
+// 1024-point rows; 0: as the forward pass, HGP_ROWT_PAIRS).  4 measured slower (three 45 KB
+// blocks per CU, 12 waves instead of 16: C2 bench op 0.281 -> 0.285-0.287 ms, PCG(20) 14.8 ->
+// 15.8 ms; profiles/r5_w_rowinv_small.txt)
+#ifndef HGP_ROWT_PAIRS_INV
+#define HGP_ROWT_PAIRS_INV 0
+#endif
 // the same for the ROW-INVERSE pass alone (0: as the forward pass).  1: 35 KB blocks, four per
 // CU instead of two (C4 row inverse 1.09 -> 1.01 ms, K op 4.48 -> 4.46 ms, PCG(20) 210.6 ->
 // 208 ms on one box; profiles/r5_t_rowinv4096.txt); the forward pass keeps 128-B segments
@@ -147,9 +160,11 @@ template <typename T, int H, int G = 1, bool INV = false> struct RowTCfg {
   static constexpr int c_pairs() {
     if (G > 1) return (INV && !is_pow2(H) && HGP_ROWG_PAIRS_TRI_INV > 0) ? HGP_ROWG_PAIRS_TRI_INV
                       : (INV && is_pow2(H) && H >= 4096 && HGP_ROWG_PAIRS_LONG_INV > 0) ? HGP_ROWG_PAIRS_LONG_INV
+                      : (INV && H == 2048 && HGP_ROWG_PAIRS_2048_INV > 0) ? HGP_ROWG_PAIRS_2048_INV
                       : (H >= 4096 && HGP_ROWG_PAIRS_LONG > 0) ? HGP_ROWG_PAIRS_LONG
                                                               : 8 / G;   // 2C rows x G columns = 128 B (fp32)
     int c = (TT > 64 ? HGP_ROWT_PAIRS_BIG : HGP_ROWT_PAIRS) * 64 / TT;   // 512 threads at the default
+    if (INV && is_pow2(H) && H >= 1024 && TT == 64 && HGP_ROWT_PAIRS_INV > 0) c = HGP_ROWT_PAIRS_INV;
     if (INV && !is_pow2(H) && TT > 64 && HGP_ROWT_THREADS_TRI_INV > 0) c = HGP_ROWT_THREADS_TRI_INV / TT;
     if (!INV && !is_pow2(H) && TT > 64 && HGP_ROWT_THREADS_TRI_FWD > 0 &&
         (HGP_ROWT_THREADS_TRI_FWD / TT) * 2 * (int)sizeof(C2<T>) >= 64)
