@@ -231,10 +231,22 @@ constexpr int CG_LOADS = 8;
 #ifndef HGP_TRI_P_CONV_MIN
 #define HGP_TRI_P_CONV_MIN 6144
 #endif
+// points per thread of the fp32 1024-point contiguous-line passes (0: PFor's 16).  8: lines of
+// two waves at ~71 VGPRs, HGP_MINW_CONTIG_P8 waves per SIMD -- measured slower (C2 column pass
+// 0.17 -> 0.19-0.20 ms, bench op 0.278 -> 0.319 ms: block barriers and a fourth exchange, and
+// no DC / Nyquist packing on lines of more than one wave; profiles/r5_y_conv1024_p8.txt)
+#ifndef HGP_P_CONV_1024
+#define HGP_P_CONV_1024 0
+#endif
+#ifndef HGP_MINW_CONTIG_P8
+#define HGP_MINW_CONTIG_P8 6
+#endif
 template <typename T, int H, int LAY> struct PassP {
   static constexpr bool CONTIG_LINE = LAY == LAY_CONTIG || LAY == LAY_CONTIG_G || LAY == LAY_CONTIG_Q;
-  static constexpr int v = (std::is_same<T, float>::value && is_tri(H) && H >= HGP_TRI_P_CONV_MIN && CONTIG_LINE)
-                               ? HGP_TRI_P_CONV : PFor<T, H>::v;
+  static constexpr bool F32 = std::is_same<T, float>::value;
+  static constexpr int v = (F32 && is_tri(H) && H >= HGP_TRI_P_CONV_MIN && CONTIG_LINE) ? HGP_TRI_P_CONV
+                         : (F32 && H == 1024 && CONTIG_LINE && HGP_P_CONV_1024 > 0) ? HGP_P_CONV_1024
+                                                                                    : PFor<T, H>::v;
 };
 
 template <typename T, int H, int LAY> struct PassCfg {
@@ -279,7 +291,8 @@ template <typename T, int H, int LAY> struct PassCfg {
   static constexpr int MINW_LDS = (BLOCKS_BY_LDS * WAVES_PER_BLOCK) / 4;
   static constexpr int MINW_AUTO = MINW_LDS < 1 ? 1 : (MINW_LDS > 4 ? 4 : MINW_LDS);
   // (3 waves per SIMD only for lines of 4 waves: 3 whole blocks per CU)
-  static constexpr int MINW_CL = (P == 24) ? 3 : (!is_pow2(H) && TT >= 256) ? HGP_MINW_CONTIG_TRI
+  static constexpr int MINW_CL = (P == 24) ? 3 : (H == 1024 && P == 8) ? HGP_MINW_CONTIG_P8
+                                 : (!is_pow2(H) && TT >= 256) ? HGP_MINW_CONTIG_TRI
                                  : (H >= 4096 && TT == 256) ? HGP_MINW_CONTIG_4096
                                  : H >= 2048 ? HGP_MINW_CONTIG_LONG : H <= 512 ? HGP_MINW_CONTIG_SHORT : HGP_MINW_CONTIG;
   // a block's waves must fit the SIMDs' share at once: >= WAVES_PER_BLOCK / 4 waves per SIMD
