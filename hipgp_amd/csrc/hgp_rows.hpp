@@ -144,9 +144,17 @@ template <typename T, int H> struct RowGroup {
 #ifndef HGP_ROW_P_LONG
 #define HGP_ROW_P_LONG 0
 #endif
+// points per thread of the grouped fp32 3 * 2^k rows (>= 6144 points; 0: PFor's 12).  24: radix-8
+// stages, as the column pass (HGP_TRI_P_CONV): C4 R^T row forward 2.63 -> 2.34 ms, row inverse
+// 3.71 -> 3.60, op 14.65 -> 14.21 ms; R 15.04 -> 14.07 ms (profiles/r5_aa_rows_p24.txt)
+#ifndef HGP_ROW_P_TRI
+#define HGP_ROW_P_TRI 24
+#endif
 template <typename T, int H, int G = 1, bool INV = false> struct RowTCfg {
-  static constexpr int P = (std::is_same<T, float>::value && is_pow2(H) && H >= 4096 && HGP_ROW_P_LONG > 0)
-                               ? HGP_ROW_P_LONG : PFor<T, H>::v;
+  static constexpr bool F32 = std::is_same<T, float>::value;
+  static constexpr int P = (F32 && is_pow2(H) && H >= 4096 && HGP_ROW_P_LONG > 0) ? HGP_ROW_P_LONG
+                         : (F32 && !is_pow2(H) && G > 1 && HGP_ROW_P_TRI > 0) ? HGP_ROW_P_TRI
+                                                                            : PFor<T, H>::v;
   static constexpr int TT = H / P;
   // tile chunks per frequency half (the grouped blocks keep a chunk of columns in LDS at a time)
   static constexpr int NCH = G > 1 ? 2 : 1;
