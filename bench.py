@@ -18,7 +18,10 @@ SqExp(sig2=1, ell=0.01), jitter 1e-3, fp32, B = 32 right-hand sides per GPU = ro
 The compute_kn timing and the per-pass event timing run BEFORE the timed steps (untimed for
 the metric), so the timed steps see the GPU at its steady clock.
 
-Multi-GPU: one process per GPU (torchrun); RHS are sharded (each rank its own 32), no
+Multi-GPU: one process per GPU.  Under torchrun (WORLD_SIZE set) WORLD_SIZE must equal --gpus;
+`python bench.py --gpus N` with no torch.distributed environment starts the N ranks itself (a
+torchrun child launched before this process touches the GPU; it exits with the child's code).
+n_gpus is the world size of the initialised process group.  RHS are sharded (each rank its own 32), no
 collective inside the timed region apart from the barriers; max-over-ranks timing.  Beside the
 weak K-matvec line, two legs measured at every N (untimed for the metric, max over ranks) that
 CAN fail to scale:
@@ -32,8 +35,9 @@ CAN fail to scale:
   strong_c4     = config 4's own multi-GPU workload (BASELINE configs[3]):
                   compute_kn for its fixed global batch of 200 RHS on the 4096^2 grid
                   (Matern-3/2, sig2 0.1, ell 0.1, jitter 1e-3), split 200/N per rank -- 25 per GPU
-                  at N = 8 -- with the same all-RHS break; one timed repetition (~2 s at N = 1,
-                  ~130 GB of HBM there); an error is recorded in the line instead of failing it
+                  at N = 8 -- with the same all-RHS break; one warm-up call, then the median and
+                  min of --c4-reps timed calls (~1.7 s each at N = 1) with the set-up / PCG / R^T
+                  split of every call; an error is recorded in the line instead of failing it
 """
 import argparse
 import json
@@ -71,6 +75,7 @@ def parse():
     ap.add_argument("--no-legs", action="store_true", help="skip the strong-scaling / ELBO-step legs")
     ap.add_argument("--legs-reps", type=int, default=3)
     ap.add_argument("--no-c4-leg", action="store_true", help="skip the config-4 (200 RHS at 4096^2) strong leg")
+    ap.add_argument("--c4-reps", type=int, default=3, help="timed repetitions of the config-4 leg")
     return ap.parse_args()
 
 
@@ -221,18 +226,27 @@ def _all_ok(ok, dist, device, backend):
     return bool(int(t.item()))
 
 
-def c4_strong_leg(args, device, dist, world, rank):
+def c4_strong_leg(args, device, dist, world, rank, reps=3):
     """Config 4 (4096^2, Matern-3/2, 200 RHS global) compute_kn split over the ranks: the
     workload the 8-GPU configuration is quoted on (25 RHS per GPU at N = 8).
+
+    One untimed warm-up call (plan creation, workspace and CG-vector allocation, twiddle tables),
+    then `reps` timed calls, each barrier + synchronise bracketed, max over ranks: the median and
+    the min, every repetition, and the phase split of each -- set-up (ToeplitzTensor: pooled plan
+    + spectrum), PCG(20), R^T -- with a synchronise (and a barrier) after every phase, so the
+    phases sum to the call.  The plan's device scratch and the peak torch allocation are reported
+    beside it (a plan trimmed from the idle pool re-allocates its scratch inside the next call).
 
     The set-up (model, Knm) holds no collective: a failure there (e.g. out of device memory on
     a smaller card) is agreed on by every rank (one all-reduce of an ok flag) and the leg is
     skipped on all of them together, so no rank waits in a collective another one left.  The
     timed solve all-reduces every PCG iteration; an error there is recorded only at N = 1 and
     re-raised otherwise (torchrun then stops every rank instead of leaving them blocked)."""
+    import torch.distributed as tdist
     import ziggy.hipgp as hg
     import ziggy.kernels as zk
     from hipgp_amd import dist as hdist
+    from hipgp_amd import plan as hplan
     G, m4 = 200, 4096
     sl = hdist.rhs_shard(G, world, rank)
     grids4 = [torch.linspace(-1, 1, m4, device=device) for _ in range(2)]
@@ -256,10 +270,60 @@ def c4_strong_leg(args, device, dist, world, rank):
         del mod, Knm_local
         torch.cuda.empty_cache()
         return out
+
+    def sync():
+        torch.cuda.synchronize()
+        if dist:
+            tdist.barrier()
+
+    def one_call(phases):
+        t = [time.perf_counter()]
+
+        def tick(name):
+            sync()
+            now = time.perf_counter()
+            phases[name] = (now - t[0]) * 1e3
+            t[0] = now
+        kn = hdist.sharded_compute_kn(mod, Knm_local, maxiter_cg=20, tol=1e-8, exact_break=dist, on_phase=tick)
+        del kn
+
+    def reduce_max(v):
+        if not dist:
+            return v
+        tt = torch.tensor(v, device=device if args.backend == "nccl" else "cpu", dtype=torch.float64)
+        tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
+        return tt.tolist()
+
     try:
-        ms = _timed_max(lambda: hdist.sharded_compute_kn(mod, Knm_local, maxiter_cg=20, tol=1e-8, exact_break=dist),
-                        1, dist, device, args.backend)
-        out.update({"ms": ms, "rhs_per_s": G / (ms * 1e-3)})
+        torch.cuda.reset_peak_memory_stats(device)
+        sync()
+        t0 = time.perf_counter()
+        warm = {}
+        one_call(warm)
+        sync()
+        warm_ms = (time.perf_counter() - t0) * 1e3
+        runs = []
+        for _ in range(reps):
+            ph = {}
+            sync()
+            t0 = time.perf_counter()
+            one_call(ph)
+            sync()
+            total = (time.perf_counter() - t0) * 1e3
+            runs.append(reduce_max([total, ph.get("setup", 0.0), ph.get("pcg", 0.0), ph.get("rt", 0.0)]))
+        warm = reduce_max([warm_ms, warm.get("setup", 0.0), warm.get("pcg", 0.0), warm.get("rt", 0.0)])
+        tot = [r[0] for r in runs]
+        med = float(np.median(tot))
+        idle = hplan._POOL.get(((m4, m4), torch.float32, device.index), [])
+        scratch = [hplan._scratch_bytes(h) for h in idle]
+        out.update({"ms": med, "ms_min": float(min(tot)), "reps": reps, "rhs_per_s": G / (med * 1e-3),
+                    "runs_ms": [dict(zip(("total", "setup", "pcg", "rt"), [round(v, 2) for v in r])) for r in runs],
+                    "warmup_ms": dict(zip(("total", "setup", "pcg", "rt"), [round(v, 2) for v in warm])),
+                    "phase_median_ms": {k: float(np.median([r[i] for r in runs]))
+                                        for i, k in enumerate(("total", "setup", "pcg", "rt"))},
+                    "plan_scratch_bytes": max(scratch) if scratch else None,
+                    "torch_peak_bytes": int(torch.cuda.max_memory_allocated(device)),
+                    "note": "phases max over ranks each, synchronised (and barriered) after every phase"})
     except RuntimeError as e:
         if dist:
             raise
@@ -324,8 +388,48 @@ def multi_gpu_legs(args, m, grids, kf, device, dist, world, rank, reps):
                           "stats_allreduce_bytes": 2 * Mp * 4, "backend": args.backend if dist else None}}
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_launch_cmd(argv, gpus, port):
+    """The torchrun command that starts `gpus` rank processes of this script (same arguments),
+    one per GPU, rendezvous on 127.0.0.1."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+
+
+def launch_plan(args, env):
+    """What main() does with --gpus N in environment `env`: ("run", None) in a rank process
+    (WORLD_SIZE == N, or N = 1 with no torch.distributed environment), ("launch", cmd) for N > 1
+    without one (this process starts the N ranks as a torchrun child BEFORE touching the GPU,
+    and exits with its code), ("refuse", why) when WORLD_SIZE and --gpus disagree."""
+    ws = env.get("WORLD_SIZE")
+    if args.gpus < 1:
+        return "refuse", f"--gpus must be >= 1, got {args.gpus}"
+    if ws is None:
+        if args.gpus == 1:
+            return "run", None
+        return "launch", rank_launch_cmd(sys.argv[1:], args.gpus, _free_port())
+    if int(ws) != args.gpus:
+        return "refuse", (f"WORLD_SIZE={ws} but --gpus {args.gpus}: launch {args.gpus} ranks "
+                          f"(torchrun --nproc-per-node {args.gpus}) or pass --gpus {ws}")
+    return "run", None
+
+
 def main():
     args = parse()
+    what, detail = launch_plan(args, os.environ)
+    if what == "refuse":
+        print(f"bench.py: refusing to run: {detail}", file=sys.stderr)
+        sys.exit(2)
+    if what == "launch":
+        # no GPU call has happened in this process: the ranks are children, never an exec
+        import subprocess
+        sys.exit(subprocess.call(detail))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -338,6 +442,8 @@ def main():
             tdist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
         else:
             tdist.init_process_group(args.backend)
+        world = tdist.get_world_size()           # as the initialised process group sees it
+        rank = tdist.get_rank()
     device = torch.device("cuda", dev_index)
     torch.cuda.set_device(device)
 
@@ -418,7 +524,7 @@ def main():
         legs = multi_gpu_legs(args, m, grids, kf, device, dist, world, rank, args.legs_reps)
         torch.cuda.empty_cache()
         if not args.no_c4_leg:
-            legs["strong_c4"] = c4_strong_leg(args, device, dist, world, rank)
+            legs["strong_c4"] = c4_strong_leg(args, device, dist, world, rank, reps=args.c4_reps)
 
     # ---- the metric: W warmup + K timed batched K matvec steps --------------------------------
     settle()
@@ -466,6 +572,8 @@ def main():
         "value": value,
         "unit": "RHS-matvecs/s",
         "n_gpus": world,
+        "process_group": ({"world_size": world, "backend": tdist.get_backend(), "same_device": bool(args.same_device)}
+                          if dist else None),
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,

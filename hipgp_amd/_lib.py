@@ -31,6 +31,7 @@ EXPORTS = (
     "hgp_plan_dqf", "hgp_pcg_local_flag", "hgp_pcg_set_done", "hgp_pcg_iters",
     "hgp_slab_info", "hgp_slab_pass", "hgp_plan_mem", "hgp_plan_trim",
     "hgp_slab_pass_ex", "hgp_slab_cg_xr", "hgp_slab_cg_check", "hgp_slab_cg_p",
+    "hgp_meanfield_rowdots", "hgp_meanfield_cols",
 )
 KERN_SQEXP, KERN_MATERN12, KERN_MATERN32, KERN_MATERN52, KERN_GNEITING = 0, 1, 2, 3, 4
 
@@ -74,6 +75,8 @@ def lib():
         "hgp_kuf_semi_sqexp": (i32, [i32, i32, pi64, ctypes.POINTER(vp), vp, i64, dbl, dbl, vp, vp]),
         "hgp_knn_doubly_diag": (i32, [i32, i32, vp, i64, dbl, dbl, vp, i32, vp, vp]),
         "hgp_meanfield_stats": (i32, [i32, vp, i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+        "hgp_meanfield_rowdots": (i32, [i32, vp, i64, i64, vp, vp, vp, vp]),
+        "hgp_meanfield_cols": (i32, [i32, vp, i64, i64, vp, vp, vp, vp, vp]),
         "hgp_block_stats": (i32, [i32, i32, pi64, pi64, vp, i64, vp, vp, vp, vp, vp, vp]),
         "hgp_sym_toeplitz_dqf": (i32, [i32, vp, vp, i64, i64, vp, vp]),
         "hgp_plan_column_grad": (i32, [vp, i32, vp, vp, i64, vp]),

@@ -1268,11 +1268,16 @@ int pcg_begin_t(hgp_plan* P, const void* b, void* x, int64_t nrhs, int use_preco
   hipStream_t s = P->stream;
   const int64_t M = P->M;
   const size_t vb = (size_t)(nrhs * M) * sizeof(T);
-  HGP_TRY(P->r.ensure(vb));
-  HGP_TRY(P->z.ensure(vb));
-  HGP_TRY(P->p.ensure(vb));
-  HGP_TRY(P->Ap.ensure(vb));
   const bool fused = fused_pcg<T>(P);
+  HGP_TRY(P->r.ensure(vb));
+  HGP_TRY(P->p.ensure(vb));
+  // the fused iteration never stores Ap or z (the row-inverse epilogues consume them in LDS), so
+  // only the unfused one holds them: at C4's B = 200 that is 27 GB of scratch less, and the
+  // plan then fits the idle-pool budget instead of being trimmed and re-allocated per solve
+  if (!fused) {
+    HGP_TRY(P->z.ensure(vb));
+    HGP_TRY(P->Ap.ensure(vb));
+  }
   const int npo = fused ? std::max(rn_last<T>(P), spec_np(P)) : rn_last<T>(P);
   const int npu = fused ? std::max(update_np(M), xr_np<T>(P)) : update_np(M);
   HGP_TRY(P->part_op.ensure((size_t)(nrhs * npo) * sizeof(T)));
@@ -1393,14 +1398,14 @@ int pcg_step_t(hgp_plan* P, double tol) {
       ep.fix = -1;
       if (inkern) { ep.sp = part_s; ep.np = nps; ep.rs = rs_cur; ep.rs_out = rs_nxt; }
       const PairOp pair{P->specI.ptr, part_o, &ep, (G > 0 || !inkern) ? &mid_beta : nullptr};
-      HGP_TRY(run_op<T>(P, HGP_OP_K, P->p.ptr, P->Ap.ptr, nrhs, nullptr, nullptr, done, -1, part_o, &exr,
+      HGP_TRY(run_op<T>(P, HGP_OP_K, P->p.ptr, nullptr, nrhs, nullptr, nullptr, done, -1, part_o, &exr,
                         (G > 0 || !inkern) ? &mid_alpha : nullptr, &pair));
       cg_check<T>(P->part_u.ptr, npx, (int)nrhs, tol, rnew, done, iters, s);
       if (inkern) P->cg_rs_par ^= 1;
       HIP_TRY(hipGetLastError());
       return 0;
     }
-    HGP_TRY(run_op<T>(P, HGP_OP_K, P->p.ptr, P->Ap.ptr, nrhs, nullptr, nullptr, done, -1, part_o, &exr,
+    HGP_TRY(run_op<T>(P, HGP_OP_K, P->p.ptr, nullptr, nrhs, nullptr, nullptr, done, -1, part_o, &exr,
                       (G > 0 || !inkern) ? &mid_alpha : nullptr));
     cg_check<T>(P->part_u.ptr, npx, (int)nrhs, tol, rnew, done, iters, s);
     if (P->cg_precond) {
@@ -1412,7 +1417,7 @@ int pcg_step_t(hgp_plan* P, double tol) {
       ep.coef2 = alpha;
       ep.fix = step + 1;           // the done value this step's break test writes
       if (inkern) { ep.sp = part_s; ep.np = nps; ep.rs = rs_cur; ep.rs_out = rs_nxt; }
-      HGP_TRY(run_op<T>(P, HGP_OP_CINV, P->r.ptr, P->Ap.ptr, nrhs, nullptr, nullptr, done, -1, part_o, &ep,
+      HGP_TRY(run_op<T>(P, HGP_OP_CINV, P->r.ptr, nullptr, nrhs, nullptr, nullptr, done, -1, part_o, &ep,
                         (G > 0 || !inkern) ? &mid_beta : nullptr));
       if (inkern) P->cg_rs_par ^= 1;
     } else {
@@ -1893,6 +1898,28 @@ int hgp_meanfield_stats(int dtype, const void* kn, int64_t nrhs, int64_t Mp, con
   hipError_t e = meanfield_stats(dtype, kn, nrhs, Mp, qm, qS, y, ivar, Knn_diag, log_sd, an, lam, dm,
                                  reinterpret_cast<hipStream_t>(hip_stream));
   if (e != hipSuccess) return fail(HGP_E_HIP, std::string("hgp_meanfield_stats: ") + hipGetErrorString(e));
+  return 0;
+}
+
+int hgp_meanfield_rowdots(int dtype, const void* kn, int64_t nrhs, int64_t Mp, const void* qm, const void* qS,
+                          void* out3, void* hip_stream) {
+  if (dtype != HGP_F32 && dtype != HGP_F64) return fail(HGP_E_ARG, "dtype must be HGP_F32 or HGP_F64");
+  if (nrhs < 0 || Mp < 0) return fail(HGP_E_ARG, "nrhs >= 0 and Mp >= 0 required");
+  if (nrhs > 0 && (out3 == nullptr || (Mp > 0 && (kn == nullptr || qm == nullptr || qS == nullptr))))
+    return fail(HGP_E_ARG, "null pointer");
+  hipError_t e = meanfield_rowdots(dtype, kn, nrhs, Mp, qm, qS, out3, reinterpret_cast<hipStream_t>(hip_stream));
+  if (e != hipSuccess) return fail(HGP_E_HIP, std::string("hgp_meanfield_rowdots: ") + hipGetErrorString(e));
+  return 0;
+}
+
+int hgp_meanfield_cols(int dtype, const void* kn, int64_t nrhs, int64_t Mp, const void* ivar, const void* bdiff,
+                       void* lam, void* dm, void* hip_stream) {
+  if (dtype != HGP_F32 && dtype != HGP_F64) return fail(HGP_E_ARG, "dtype must be HGP_F32 or HGP_F64");
+  if (nrhs < 0 || Mp < 0) return fail(HGP_E_ARG, "nrhs >= 0 and Mp >= 0 required");
+  if (Mp > 0 && (lam == nullptr || dm == nullptr || (nrhs > 0 && (kn == nullptr || ivar == nullptr || bdiff == nullptr))))
+    return fail(HGP_E_ARG, "null pointer");
+  hipError_t e = meanfield_cols(dtype, kn, nrhs, Mp, ivar, bdiff, lam, dm, reinterpret_cast<hipStream_t>(hip_stream));
+  if (e != hipSuccess) return fail(HGP_E_HIP, std::string("hgp_meanfield_cols: ") + hipGetErrorString(e));
   return 0;
 }
 

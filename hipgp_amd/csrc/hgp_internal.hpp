@@ -90,6 +90,10 @@ hipError_t doubly_diag(int dtype, int ndim, const void* x, int64_t nobs, double 
 hipError_t meanfield_stats(int dtype, const void* kn, int64_t nrhs, int64_t Mp, const void* qm, const void* qS,
                            const void* y, const void* iv, const void* knn, const void* lsd, void* an, void* lam,
                            void* dm, hipStream_t s);
+hipError_t meanfield_rowdots(int dtype, const void* kn, int64_t nrhs, int64_t Mp, const void* qm, const void* qS,
+                             void* out3, hipStream_t s);
+hipError_t meanfield_cols(int dtype, const void* kn, int64_t nrhs, int64_t Mp, const void* iv, const void* bdiff,
+                          void* lam, void* dm, hipStream_t s);
 // expanded grid n[a] tiled by blocks of side b[a] (nb[a] per axis); bs points per block, nbw
 // blocks per workgroup
 struct BlockGeom {

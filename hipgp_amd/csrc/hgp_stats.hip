@@ -140,6 +140,69 @@ hipError_t meanfield_stats(int dtype, const void* kn, int64_t nrhs, int64_t Mp, 
   return meanfield_stats_t<float>(kn, nrhs, Mp, qm, qS, y, iv, knn, lsd, an, lam, dm, s);
 }
 
+// ---- the two passes apart, for kn held in column slabs (grid-block sharding, hipgp_amd/slab.py):
+// each rank runs pass 1 on its columns (qm, qS its slices), the (nrhs, 3) row dots are all-reduced
+// (B values per dot instead of the B x M' kn), a_n and bdiff_n come from the reduced dots, and
+// pass 2 gives the rank's slice of lam / dm.
+template <typename T>
+__global__ void k_rowdots_finish(const T* __restrict__ part, int np, int nrhs, T* __restrict__ out3) {
+  const int b = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (b >= nrhs) return;
+  T s[3] = {0, 0, 0};
+  for (int g = lane; g < np; g += 64)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) s[c] += part[((int64_t)b * np + g) * 3 + c];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) s[c] += __shfl_xor(s[c], off, 64);
+  if (lane < 3) out3[(int64_t)b * 3 + lane] = lane == 0 ? s[0] : lane == 1 ? s[1] : s[2];
+}
+
+template <typename T>
+hipError_t meanfield_rowdots_t(const void* kn, int64_t nrhs, int64_t Mp, const void* qm, const void* qS, void* out3,
+                               hipStream_t s) {
+  if (nrhs == 0) return hipSuccess;
+  if (Mp == 0) return hipMemsetAsync(out3, 0, (size_t)(3 * nrhs) * sizeof(T), s);
+  const int np = (int)((Mp + ST_CHUNK - 1) / ST_CHUNK);
+  T* part = nullptr;
+  hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&part), (size_t)(nrhs * np * 3) * sizeof(T), s);
+  if (e != hipSuccess) return e;
+  for (int64_t b0 = 0; b0 < nrhs; b0 += 65535) {
+    const int64_t nb0 = std::min<int64_t>(65535, nrhs - b0);
+    hipLaunchKernelGGL((k_stats_rows<T>), dim3((unsigned)np, (unsigned)nb0), dim3(ST_THREADS), 0, s,
+                       (const T*)kn + b0 * Mp, (const T*)qm, (const T*)qS, Mp, np, part + b0 * np * 3);
+  }
+  hipLaunchKernelGGL((k_rowdots_finish<T>), dim3((unsigned)((nrhs + 3) / 4)), dim3(256), 0, s, (const T*)part, np,
+                     (int)nrhs, (T*)out3);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  return hipFreeAsync(part, s);
+}
+
+template <typename T>
+hipError_t meanfield_cols_t(const void* kn, int64_t nrhs, int64_t Mp, const void* iv, const void* bdiff, void* lam,
+                            void* dm, hipStream_t s) {
+  if (Mp == 0) return hipSuccess;
+  const int64_t nb = (Mp + ST_THREADS * 4 - 1) / (ST_THREADS * 4);
+  hipLaunchKernelGGL((k_stats_cols<T>), dim3((unsigned)nb), dim3(ST_THREADS), 0, s, (const T*)kn, Mp, (int)nrhs,
+                     (const T*)iv, (const T*)bdiff, (T*)lam, (T*)dm);
+  return hipGetLastError();
+}
+
+hipError_t meanfield_rowdots(int dtype, const void* kn, int64_t nrhs, int64_t Mp, const void* qm, const void* qS,
+                             void* out3, hipStream_t s) {
+  if (dtype == HGP_F64) return meanfield_rowdots_t<double>(kn, nrhs, Mp, qm, qS, out3, s);
+  return meanfield_rowdots_t<float>(kn, nrhs, Mp, qm, qS, out3, s);
+}
+
+hipError_t meanfield_cols(int dtype, const void* kn, int64_t nrhs, int64_t Mp, const void* iv, const void* bdiff,
+                          void* lam, void* dm, hipStream_t s) {
+  if (dtype == HGP_F64) return meanfield_cols_t<double>(kn, nrhs, Mp, iv, bdiff, lam, dm, s);
+  return meanfield_cols_t<float>(kn, nrhs, Mp, iv, bdiff, lam, dm, s);
+}
+
 
 // ---- block-diagonal family (BlockToeplitzGP, hipgp.py:527-691) ---------------------------------
 // Blocks tile the expanded grid (dims n_a, block sides b_a, util.py:79-119): block beta enumerates

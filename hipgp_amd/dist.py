@@ -106,13 +106,16 @@ def _allranks_solve(tt, b, maxiter, tol, group):
         return x
 
 
-def sharded_compute_kn(model, Knm_local, maxiter_cg=10, tol=1e-8, exact_break=None, group=None, Kmm=None):
+def sharded_compute_kn(model, Knm_local, maxiter_cg=10, tol=1e-8, exact_break=None, group=None, Kmm=None,
+                       on_phase=None):
     """kn = R^T K^{-1} Knm^T for this rank's rows (`hipgp.py:117-146`).  exact_break applies
     the all-RHS break rule across ranks (see module docstring); default: on for fp64 (where
     tol = 1e-8 can be met) and off for fp32 (where it never is at these sizes).  The exact-break
     solve is differentiable (AllRanksInvMatmul), like the reference's InvMatmul.  A rank whose
     shard is empty returns a (0, M') kn and still joins the break rule's all-reduces (and, when
-    kn carries a graph, the backward solve's)."""
+    kn carries a graph, the backward solve's).  on_phase(name) is called after the set-up
+    ("setup"), the solve ("pcg") and R^T ("rt") -- the bench's phase split."""
+    tick = on_phase if on_phase is not None else (lambda name: None)
     if exact_break is None:
         exact_break = Knm_local.dtype == torch.float64
     # the solve carries a graph iff the kernel parameters are learned (column and Knm need grad);
@@ -126,15 +129,19 @@ def sharded_compute_kn(model, Knm_local, maxiter_cg=10, tol=1e-8, exact_break=No
         return Knm_local.new_zeros((0, model.Mprime))
     if Kmm is None:
         Kmm = model.toeplitz()
+    tick("setup")
     if exact_break:
         d0 = AllRanksInvMatmul.apply(Kmm, Kmm.column, Knm_local, maxiter_cg, tol, group)
     else:
         d0 = Kmm.inv_matmul(Knm_local, do_precond=True, maxiter=maxiter_cg, tol=tol)
+    tick("pcg")
     if Knm_local.shape[0] == 0:
         # keep the solve in the graph (its backward joins the other ranks' all-reduces)
         return Knm_local.new_zeros((0, model.Mprime)) + 0 * d0.sum()
     Kmm.set_batch_shape(d0.shape[:-1])
-    return Kmm._matmul_by_RT(d0)
+    kn = Kmm._matmul_by_RT(d0)
+    tick("rt")
+    return kn
 
 
 def sharded_elbo_and_grad(model, xbatch, ybatch, noise_std_batch=None, maxiter_cg=10, tol=1e-8,

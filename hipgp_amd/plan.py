@@ -22,10 +22,12 @@ def expanded_dims(dims):
 # compute_kn call (`hipgp.py:143`); re-using an idle plan of the same grid keeps its twiddle /
 # DCT tables, so only the spectrum is recomputed (hgp_plan_set_column).  Idle plans also keep
 # their scratch (workspaces, CG vectors: the next solve needs the same sizes) while all idle
-# scratch on a device stays under HGP_POOL_MB (default: an eighth of the device's memory, the
-# same share as the 3-D workspace budget of hgp_api.hip -- 36 GB of the 288 GB: one C5 plan's
-# R^T workspace is 26 GB, and re-allocating it per compute_kn would cost more than it saves);
-# beyond that a plan is trimmed to its tables when it goes idle (hgp_plan_trim).
+# scratch on a device stays under HGP_POOL_MB (default: a quarter of the device's memory, 72 GB
+# of the 288 GB: one C5 plan's R^T workspace is 26 GB, and config 4's 200-RHS solve holds 35 GB
+# of CG vectors and workspaces -- re-allocating those per compute_kn costs more than it saves;
+# with an eighth, round 5's C4 plan (62 GB then, before the fused PCG stopped allocating Ap / z)
+# was trimmed after every call); beyond that a plan is trimmed to its tables when it
+# goes idle (hgp_plan_trim).
 # release_pool() frees every idle plan, e.g. before a large torch allocation (this memory is
 # outside torch's caching allocator).
 _POOL = {}
@@ -37,12 +39,12 @@ _ws_warned = False
 
 
 def pool_budget(device_index):
-    """Idle-plan scratch cap of one device in bytes (HGP_POOL_MB, else 1/8 of its memory)."""
+    """Idle-plan scratch cap of one device in bytes (HGP_POOL_MB, else 1/4 of its memory)."""
     if _POOL_ENV is not None:
         return int(_POOL_ENV) << 20
     b = _POOL_DEV.get(device_index)
     if b is None:
-        b = _POOL_DEV[device_index] = torch.cuda.get_device_properties(device_index).total_memory // 8
+        b = _POOL_DEV[device_index] = torch.cuda.get_device_properties(device_index).total_memory // 4
     return b
 
 

@@ -37,32 +37,61 @@ def split(n, parts, k):
 
 # largest all-to-all handed to RCCL in one call: a 2.4 GB exchange (config 5's R^T, two fp64
 # RHS, world size 1) came back wrong from one all_to_all_single, so larger exchanges go in pieces
+# (tools/a2a_limit.py measures where a single call breaks)
 A2A_MAX_BYTES = 1 << 30
 
 
-def _a2a(out, inp, out_splits, in_splits, group):
-    """all_to_all_single on real views (complex / CUDA through the host for gloo).  Exchanges
-    above A2A_MAX_BYTES run as several all_to_all calls over equal parts of every peer's block."""
+def a2a_parts(totals_bytes):
+    """Number of pieces an exchange is split into.  `totals_bytes`: every rank's send and
+    receive totals of this exchange.  It must be the SAME on every rank -- a rank that issued
+    one all-to-all while a peer issued several would hang or pair mismatched pieces -- so it
+    comes from the largest total of any rank, which every rank computes from the shared
+    partition (SlabToeplitz._bufs), never from its own byte count alone."""
+    biggest = max([0] + [int(t) for t in totals_bytes])
+    return max(1, -(-biggest // A2A_MAX_BYTES))
+
+
+def _pieces(t, offs, sizes, j, parts):
+    """Piece j (of `parts`) of every peer block [a, a + s) of the flat tensor t: contiguous views."""
+    return [t[a + s * j // parts:a + s * (j + 1) // parts] for a, s in zip(offs, sizes)]
+
+
+def _a2a(out, inp, out_splits, in_splits, group, parts=1):
+    """all_to_all_single on real views (complex / CUDA through the host for gloo), in `parts`
+    pieces (a2a_parts: the same count on every rank): piece j moves the j-th equal part of every
+    peer's block.  RCCL takes the pieces as list all-to-alls over views (no copies); gloo, which
+    has no list all-to-all, packs each piece of its host copy into one all_to_all_single."""
     gloo = dist.get_backend(group) == "gloo"
     i = torch.view_as_real(inp).reshape(-1) if inp.is_complex() else inp.reshape(-1)
     o = torch.view_as_real(out).reshape(-1) if out.is_complex() else out.reshape(-1)
     f = 2 if inp.is_complex() else 1
     so, si = [f * s for s in out_splits], [f * s for s in in_splits]
-    if gloo and i.is_cuda:
-        ih, oh = i.cpu(), torch.empty(o.shape, dtype=o.dtype)
-        dist.all_to_all_single(oh, ih, so, si, group=group)
-        o.copy_(oh)
-        return out
-    nbytes = max(sum(so), sum(si)) * i.element_size()
-    if nbytes <= A2A_MAX_BYTES:
-        dist.all_to_all_single(o, i, so, si, group=group)
-        return out
-    parts = -(-nbytes // A2A_MAX_BYTES)
     oo = [sum(so[:r]) for r in range(len(so))]
     oi = [sum(si[:r]) for r in range(len(si))]
+    if gloo:
+        ih = i.cpu()
+        oh = torch.empty(o.shape, dtype=o.dtype) if o.is_cuda else o
+        if parts == 1:
+            dist.all_to_all_single(oh, ih, so, si, group=group)
+        else:
+            for j in range(parts):
+                src = _pieces(ih, oi, si, j, parts)
+                dst = _pieces(oh, oo, so, j, parts)
+                buf = torch.empty(sum(d.numel() for d in dst), dtype=oh.dtype)
+                dist.all_to_all_single(buf, torch.cat(src), [d.numel() for d in dst], [p.numel() for p in src],
+                                       group=group)
+                k = 0
+                for d in dst:
+                    d.copy_(buf[k:k + d.numel()])
+                    k += d.numel()
+        if oh is not o:
+            o.copy_(oh)
+        return out
+    if parts == 1:
+        dist.all_to_all_single(o, i, so, si, group=group)
+        return out
     for j in range(parts):
-        piece = lambda t, offs, sizes: [t[a + s * j // parts:a + s * (j + 1) // parts] for a, s in zip(offs, sizes)]
-        dist.all_to_all(piece(o, oo, so), piece(i, oi, si), group=group)
+        dist.all_to_all(_pieces(o, oo, so, j, parts), _pieces(i, oi, si, j, parts), group=group)
     return out
 
 
@@ -222,12 +251,24 @@ class SlabToeplitz:
             # rows [a_r, a_r + cnt_r)); the conv writes the return all-to-all's send buffer as
             # rank blocks [r][g][q][o - b_r][c] (HGP_SLAB_CONV_A2A: no line buffer, no gather /
             # scatter copies); the return all-to-all delivers my output rows of every group
-            sizes_in = [(groups[s][1] - groups[s][0]) * nrhs * ni * inner for s in range(ws)]
-            sizes_rx = [ng * nrhs * (rows_in[r][1] - rows_in[r][0]) * inner for r in range(ws)]
-            sizes_tx = [ng * nrhs * (rows_out[r][1] - rows_out[r][0]) * inner for r in range(ws)]
-            sizes_back = [(groups[s][1] - groups[s][0]) * nrhs * no * inner for s in range(ws)]
+            cnt = lambda rows, r: rows[r][1] - rows[r][0]
+            gcnt = lambda r: groups[r][1] - groups[r][0]
+
+            def sizes(r):    # rank r's (sizes_in, sizes_rx, sizes_tx, sizes_back), in elements
+                return ([gcnt(s) * nrhs * cnt(rows_in, r) * inner for s in range(ws)],
+                        [gcnt(r) * nrhs * cnt(rows_in, s) * inner for s in range(ws)],
+                        [gcnt(r) * nrhs * cnt(rows_out, s) * inner for s in range(ws)],
+                        [gcnt(s) * nrhs * cnt(rows_out, r) * inner for s in range(ws)])
+            sizes_in, sizes_rx, sizes_tx, sizes_back = sizes(rk)
+            # piece counts of the two exchanges from EVERY rank's totals (a2a_parts): identical
+            # on all ranks even where uneven splits put the ranks' own totals on either side of
+            # a multiple of A2A_MAX_BYTES
+            esz = torch.empty((), dtype=self.engine.cdtype).element_size()
+            every = [sizes(r) for r in range(ws)]
+            parts_fwd = a2a_parts([sum(v) * esz for e in every for v in (e[0], e[1])])
+            parts_back = a2a_parts([sum(v) * esz for e in every for v in (e[2], e[3])])
             b = dict(nrhs=int(nrhs), NG=NG, inner=inner, gs0=gs0, ng=ng, ni=ni, no=no, sizes_in=sizes_in, sizes_rx=sizes_rx,
-                     sizes_tx=sizes_tx, sizes_back=sizes_back,
+                     sizes_tx=sizes_tx, sizes_back=sizes_back, parts_fwd=parts_fwd, parts_back=parts_back,
                      E=torch.empty((NG, nrhs, ni, inner), dtype=cd, device=dev),
                      recv=torch.empty(sum(sizes_rx), dtype=cd, device=dev),
                      send=torch.empty(sum(sizes_tx), dtype=cd, device=dev),
@@ -262,12 +303,12 @@ class SlabToeplitz:
         if ni > 0:
             e.fwd(op, x, ni, E, done=done)
         # 2. all-to-all: my rows of every group -> all rows of my groups
-        _a2a(recv, E.reshape(-1), b["sizes_rx"], b["sizes_in"], self.group)
+        _a2a(recv, E.reshape(-1), b["sizes_rx"], b["sizes_in"], self.group, b["parts_fwd"])
         # 3. the axis-0 convolution of my groups, receive buffer -> send buffer
         if ng > 0:
             e.conv_a2a(op, recv, send, b["gs0"], ng, nrhs, self.ws, done=done)
         # 4. all-to-all back: all rows of my groups -> my output rows of every group
-        _a2a(back, send, b["sizes_back"], b["sizes_tx"], self.group)
+        _a2a(back, send, b["sizes_back"], b["sizes_tx"], self.group, b["parts_back"])
         E2 = back.view(b["NG"], nrhs, no, b["inner"])      # groups arrive in rank order = group order
         # 5. local inverse transforms over my output rows (+ fused dot)
         y = torch.empty((nrhs, no * rest_out), dtype=x.dtype, device=x.device) if out is None else out

@@ -188,12 +188,27 @@ def _fit_options(kw):
     return o
 
 
-def _fit_world(o):
+def _fit_world(o, mod=None):
     """(sharded?, world size, rank) of a fit under torch.distributed (see _fit_options).  An
     unchanged experiment script launched by torchrun (WORLD_SIZE > 1 in the environment) has
     not initialised a process group: it is initialised here -- RCCL ("nccl") on cuda:LOCAL_RANK,
-    gloo when the fit runs on the CPU."""
+    gloo when the fit runs on the CPU.
+
+    Only the Toeplitz ("ziggy") whitening shards: a cholesky-whitened model (`hipgp.py:120-128`,
+    a dense M x M factor, M' = M) has no RHS / grid-block split here, so with distributed="auto"
+    every rank runs the whole single-process fit (as before sharding existed; a warning says
+    so), and distributed=True refuses it."""
     import torch.distributed as dist
+    if mod is not None and getattr(mod, "whitened_type", "ziggy") != "ziggy":
+        if o["distributed"] is True:
+            raise NotImplementedError("sharded fits need whitened_type='ziggy' (the Toeplitz operators); "
+                                      f"this model is whitened_type={mod.whitened_type!r}")
+        if o["distributed"] == "auto" and ((dist.is_available() and dist.is_initialized())
+                                           or int(os.environ.get("WORLD_SIZE", "1")) > 1):
+            import warnings
+            warnings.warn(f"whitened_type={mod.whitened_type!r} does not shard: every rank runs the whole fit",
+                          RuntimeWarning, stacklevel=3)
+        return False, 1, 0
     up = dist.is_available() and dist.is_initialized()
     if (not up and o["distributed"] is not False and dist.is_available()
             and int(os.environ.get("WORLD_SIZE", "1")) > 1):
@@ -232,7 +247,7 @@ def svigp_fit(mod, odir, xtrain, ytrain, noise_std_train, xtest, ftest, etest, x
     epoch callback and writes `time_report.csv`."""
     import pandas as pd
     o = _fit_options(fit_kwargs)
-    sharded, world_size, rank = _fit_world(o)
+    sharded, world_size, rank = _fit_world(o, mod)
     if sharded and "LOCAL_RANK" in os.environ:
         o["cuda_num"] = int(os.environ["LOCAL_RANK"])
     if sharded and o["shard"] == "grid" and (o["learn_kernel"] or o["learn_noise"] or o["integrated_obs"]):

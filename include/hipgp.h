@@ -226,6 +226,17 @@ int hgp_meanfield_stats(int dtype, const void* kn, int64_t nrhs, int64_t Mp, con
                         const void* qS, const void* y, const void* ivar, const void* Knn_diag,
                         const void* log_sd, void* an, void* lam, void* dm, void* hip_stream);
 
+/* The two passes of hgp_meanfield_stats apart, for kn held in column slabs over ranks (grid-block
+ * sharding, hipgp_amd/slab.py; same reference lines).  hgp_meanfield_rowdots: for the Mp columns
+ * of kn given (qm, qS: the matching slices), out3[n*3 + c] = (kn_n.qm, |kn_n|^2, kn_n^2.qS),
+ * fixed reduction order.  A caller all-reduces out3 over the slabs and forms
+ * bdiff_n = ivar_n (kn_n.qm - y_n) and a_n from the totals; hgp_meanfield_cols then writes the
+ * slab's lam[j] = sum_n ivar_n kn_nj^2 and dm[j] = -sum_n bdiff_n kn_nj (Mp = 0: nothing). */
+int hgp_meanfield_rowdots(int dtype, const void* kn, int64_t nrhs, int64_t Mp, const void* qm,
+                          const void* qS, void* out3, void* hip_stream);
+int hgp_meanfield_cols(int dtype, const void* kn, int64_t nrhs, int64_t Mp, const void* ivar,
+                       const void* bdiff, void* lam, void* dm, void* hip_stream);
+
 /* Block-diagonal variational family (BlockToeplitzGP, ziggy/hipgp.py:527-691), SURVEY §8(f) row 3.
  * The expanded grid dims[ndim] (ndim 2 or 3, n_a = 2 m_a - 2) is tiled by blocks[ndim] (each n_a
  * divisible by blocks[a]; points per block bs = prod blocks <= 128), blocks enumerated C-order

@@ -113,3 +113,59 @@ def test_sharded_fit_gloo_matches_single_process():
             break
         ref, alt = fx["box_theta1_steps"][j], fx["box_alt_theta1_steps"][j]
         assert np.linalg.norm(t1_single[k] - ref) <= 4 * np.linalg.norm(alt - ref) + 1e-9 * np.linalg.norm(ref), k
+
+
+def _chol_fit(distributed):
+    """A cholesky-whitened mean-field fit (M' = M, `hipgp.py:120-128`) on a 6 x 5 grid, two
+    minibatches; returns theta1 after the fit."""
+    import ziggy.hipgp as hg
+    import ziggy.kernels as zk
+    dt = torch.float64
+    grids = [torch.linspace(-1, 1, 6, dtype=dt), torch.linspace(-1, 1, 5, dtype=dt)]
+    mod = hg.MeanFieldToeplitzGP(zk.Matern(nu=1.5, dtype=dt), grids, num_obs=40, sig2_init=1., ell_init=.5,
+                                 learn_kernel=False, jitter_val=1e-3, dtype=dt, whitened_type="cholesky")
+    torch.manual_seed(0)
+    with torch.no_grad():
+        mod.global_theta1.copy_(torch.randn(mod.Mprime, 1, dtype=dt))
+    rs = np.random.RandomState(1)
+    x = rs.uniform(-1, 1, (40, 2))
+    y = np.sin(2 * x[:, :1]) + 0.1 * rs.randn(40, 1)
+    s = np.full((40, 1), 0.1)
+    mod.fit(None, x, y, s, None, None, None, None, None, None, do_cuda=False, lr=1e-2, schedule_lr=False,
+            batch_size=20, epochs=1, maxiter_cg=5, batch_log_interval=False, distributed=distributed)
+    return mod.global_theta1.detach().numpy().copy()
+
+
+def _chol_worker(rank, world_size, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import warnings
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world_size)
+    try:
+        torch.set_num_threads(2)
+        with warnings.catch_warnings(record=True) as w:
+            warnings.simplefilter("always")
+            t1 = _chol_fit("auto")
+        refused = False
+        try:
+            _chol_fit(True)
+        except NotImplementedError:
+            refused = True
+        out[rank] = (t1, any("does not shard" in str(x.message) for x in w), refused)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_cholesky_model_does_not_shard_gloo():
+    """a cholesky-whitened model under torch.distributed (world size 2) is not sent
+    down the Toeplitz sharding paths: distributed="auto" runs the whole fit on every rank (with a
+    warning) and equals the single-process fit; distributed=True refuses it."""
+    single = _chol_fit(False)
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_chol_worker, args=(2, 29650 + os.getpid() % 90, out), nprocs=2, join=True)
+    for r in range(2):
+        t1, warned, refused = out[r]
+        assert warned and refused, r
+        assert np.array_equal(t1, single), r

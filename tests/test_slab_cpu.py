@@ -23,7 +23,7 @@ def _oracle(case):
     return zo.ToeplitzOracle(col, dims)
 
 
-def _worker(rank, ws, port, case, out):
+def _worker(rank, ws, port, case, out, a2a_max=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch.distributed as dist
@@ -31,7 +31,10 @@ def _worker(rank, ws, port, case, out):
     try:
         from slab_cpu_engine import CpuSlabEngine
         from hipgp_amd import _lib
+        from hipgp_amd import slab
         from hipgp_amd.slab import SlabToeplitz
+        if a2a_max is not None:
+            slab.A2A_MAX_BYTES = a2a_max     # exchanges in pieces (same count on every rank)
         T = _oracle(case)
         S = SlabToeplitz(T.dims, CpuSlabEngine(T))
         rs = np.random.RandomState(4)
@@ -47,6 +50,8 @@ def _worker(rank, ws, port, case, out):
         x2, it2 = S.pcg(S.scatter_rows(v), maxiter=200, tol=1e-3, callback=lambda n, xx: calls.append(n))
         res["brk"], res["brk_it"], res["brk_calls"] = x2.numpy(), it2, len(calls)
         res["kn"] = S.compute_kn(S.scatter_rows(v), maxiter=8, tol=1e-8).numpy()
+        res["parts"] = sorted((op, b["parts_fwd"], b["parts_back"]) for op, b in S._buf.items())
+        res["own_bytes"] = sorted((op, max(sum(b["sizes_in"]), sum(b["sizes_rx"])) * 16) for op, b in S._buf.items())
         out[rank] = res
     finally:
         dist.destroy_process_group()
@@ -81,3 +86,31 @@ def test_slab_ops_and_pcg_gloo(case, ws):
     assert np.max(np.abs(_gather(out, ws, "brk") - ref2)) <= 1e-9 * np.max(np.abs(ref2))
     kn = zo.compute_kn(T, v, maxiter_cg=8, tol=1e-8)
     assert np.max(np.abs(_gather(out, ws, "kn") - kn)) <= 1e-9 * np.max(np.abs(kn))
+
+
+def test_slab_split_exchanges_uneven_gloo():
+    """Exchanges split into pieces (A2A_MAX_BYTES lowered to 2 KiB) with uneven row splits (13
+    rows, 24 expanded rows over 3 ranks): every rank must issue the same number of pieces --
+    the count comes from the largest rank's total, not the rank's own -- and the results stay
+    the oracle's (hipgp_amd/slab.py a2a_parts)."""
+    case, ws = "2d", 3
+    T = _oracle(case)
+    rs = np.random.RandomState(4)
+    v = rs.randn(3, T.M)
+    w = rs.randn(3, T.Mp)
+    mgr = mp.Manager()
+    out = mgr.dict()
+    port = 29700 + os.getpid() % 90
+    mp.spawn(_worker, args=(ws, port, case, out, 2048), nprocs=ws, join=True)
+    assert len(out) == ws
+    parts = [out[r]["parts"] for r in range(ws)]
+    assert all(p == parts[0] for p in parts), parts
+    assert all(pf > 1 and pb > 1 for _, pf, pb in parts[0]), parts[0]
+    # the ranks' own totals differ (so a per-rank count could have differed)
+    own = [dict(out[r]["own_bytes"]) for r in range(ws)]
+    assert any(len({o[k] for o in own}) > 1 for k in own[0]), own
+    for name, ref in (("K", T.matmul_K(v)), ("Cinv", T.matmul_Cinv(v)), ("RT", T.matmul_RT(v)), ("R", T.matmul_R(w))):
+        got = _gather(out, ws, name)
+        assert np.max(np.abs(got - ref)) <= 1e-11 * np.max(np.abs(ref)), name
+    ref = T.solve(v, True, 8, 1e-8)
+    assert np.max(np.abs(_gather(out, ws, "pcg") - ref)) <= 1e-9 * np.max(np.abs(ref))

@@ -90,6 +90,12 @@ int main() {
          HGP_E_ARG);
   EXPECT(hgp_meanfield_stats(HGP_F32, buf, 2, 16, buf, nullptr, buf, buf, buf, buf, buf, buf, buf, nullptr) ==
          HGP_E_ARG);
+  EXPECT(hgp_meanfield_rowdots(HGP_F32, buf, -1, 16, buf, buf, buf, nullptr) == HGP_E_ARG);
+  EXPECT(hgp_meanfield_rowdots(HGP_F32, buf, 2, 16, buf, nullptr, buf, nullptr) == HGP_E_ARG);
+  EXPECT(hgp_meanfield_rowdots(HGP_F64, nullptr, 0, 0, nullptr, nullptr, nullptr, nullptr) == 0);
+  EXPECT(hgp_meanfield_cols(7, buf, 2, 16, buf, buf, buf, buf, nullptr) == HGP_E_ARG);
+  EXPECT(hgp_meanfield_cols(HGP_F32, buf, 2, 16, buf, nullptr, buf, buf, nullptr) == HGP_E_ARG);
+  EXPECT(hgp_meanfield_cols(HGP_F32, nullptr, 2, 0, nullptr, nullptr, nullptr, nullptr, nullptr) == 0);
   EXPECT(hgp_sym_toeplitz_dqf(HGP_F32, buf, buf, 1, 0, buf, nullptr) == HGP_E_ARG);
   EXPECT(hgp_sym_toeplitz_dqf(HGP_F32, nullptr, buf, 1, 4, buf, nullptr) == HGP_E_ARG);
 
