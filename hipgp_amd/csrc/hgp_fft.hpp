@@ -424,6 +424,9 @@ __device__ __forceinline__ C2<T> tw_at(const C2<T>* __restrict__ tab, int q) {
 #endif
 template <typename T, int H, int R, int DIR, int NS>
 __device__ __forceinline__ void stage_twiddle(C2<T>* a, int kk, const C2<T>* __restrict__ tab) {
+#ifdef HGP_DIAG_NO_STAGE_TW
+  return;   // DIAGNOSTIC BUILD ONLY (wrong results): tools/isa_mix.py counts what the stage twiddles cost
+#endif
   const C2<T> w = tw_at<T, H>(tab, (2 * (H / (NS * R))) * kk);
   if constexpr (HGP_TW_CHAIN) {
     C2<T> wr = w;

@@ -144,14 +144,33 @@ def sharded_compute_kn(model, Knm_local, maxiter_cg=10, tol=1e-8, exact_break=No
     return kn
 
 
+def shared_mc_offset(dtype, device, group=None):
+    """The MC line-integral estimator's one offset draw per minibatch (`kernels.py:28-29`,
+    `torch.rand(1)` in the kernel dtype on the observations' device), the same on every rank:
+    each rank draws it exactly as the single process does (so every rank's RNG stream advances
+    alike) and then takes rank 0's value by a broadcast -- ranks agree without relying on being
+    seeded alike (the reference's domain script seeds only NumPy)."""
+    u = torch.rand(1, dtype=dtype, device=device)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        src = dist.get_global_rank(group, 0) if group is not None else 0
+        if dist.get_backend(group) == "gloo" and u.is_cuda:
+            h = u.cpu()
+            dist.broadcast(h, src, group=group)
+            u.copy_(h)
+        else:
+            dist.broadcast(u, src, group=group)
+    return u
+
+
 def sharded_elbo_and_grad(model, xbatch, ybatch, noise_std_batch=None, maxiter_cg=10, tol=1e-8,
                           exact_break=None, group=None, compute_kn=None, integrated_obs=False,
                           semi_integrated_estimator="analytic", semi_integrated_samps=10):
     """`elbo_and_grad` (mean-field or block family) with the minibatch sharded by rows over the
     ranks of `group`; every rank passes the SAME full minibatch and gets the same ELBO and theta
     grads.  `compute_kn(model, Knm_local)` may be injected (tests run the host logic on CPU).
-    Line-integral observations ("mc-biased") draw the reference's one torch.rand(1) offset per
-    rank: ranks seeded alike draw the same offset, as the single-process reference does.
+    Line-integral observations ("mc-biased"): the reference's one torch.rand(1) offset per
+    minibatch is drawn once and broadcast from rank 0 (shared_mc_offset), so every rank's rows
+    use the offset the single process would use for the whole minibatch.
 
     Hyper-parameter learning (learn_kernel / learn_noise): the returned ELBO's value is the
     global one and its graph holds this rank's share of sum_n a_n / bsz; after backward(),
@@ -159,9 +178,12 @@ def sharded_elbo_and_grad(model, xbatch, ybatch, noise_std_batch=None, maxiter_c
     ws = dist.get_world_size(group) if dist.is_initialized() else 1
     rk = dist.get_rank(group) if dist.is_initialized() else 0
     sl = rhs_shard(xbatch.shape[0], ws, rk)
+    u = None
+    if integrated_obs and semi_integrated_estimator == "mc-biased":
+        u = shared_mc_offset(model.kernel.dtype, xbatch.device, group)
     Knm, Knn_diag = model._make_grams(xbatch[sl], integrated_obs=integrated_obs,
                                       semi_integrated_estimator=semi_integrated_estimator,
-                                      semi_integrated_samps=semi_integrated_samps)
+                                      semi_integrated_samps=semi_integrated_samps, mc_offset=u)
     if compute_kn is None:
         kn = sharded_compute_kn(model, Knm, maxiter_cg=maxiter_cg, tol=tol, exact_break=exact_break, group=group)
     else:

@@ -122,6 +122,11 @@ class ToeplitzPlan:
         check(lib().hgp_plan_mem(self._h, ctypes.byref(sb), ctypes.byref(tb)))
         return {"scratch": sb.value, "tables": tb.value}
 
+    def trim(self):
+        """Free the plan's scratch (workspaces, CG vectors, the set-up transforms' buffers) and keep
+        its tables and spectra (hgp_plan_trim); scratch is re-allocated on demand."""
+        check(lib().hgp_plan_trim(self._h))
+
     def _report_ws(self):
         """The first time in a process that a plan's scratch passes 4 GiB, say so once: the 3-D
         operators size their workspace from the device memory (an eighth, at most 32 GiB, so the

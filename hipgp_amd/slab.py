@@ -191,6 +191,9 @@ class SlabToeplitz:
         self.rows_m = [split(dims[0], self.ws, k) for k in range(self.ws)]
         self.rows_n = [split(self.ndims[0], self.ws, k) for k in range(self.ws)]
         self._buf = {}
+        self._arena = None
+        import os
+        self.xchg_budget = int(os.environ.get("HGP_SLAB_XCHG_MB", "4096")) << 20
 
     # -- partition ------------------------------------------------------------------------
     def my_rows(self, grid="m"):
@@ -226,15 +229,11 @@ class SlabToeplitz:
             raise ValueError(f"{name} must be contiguous")
         return t
 
-    def _bufs(self, op, nrhs, dtype, dev):
-        """The exchange / all-to-all buffers of (op, nrhs), allocated once and re-used by every
-        apply -- a PCG iteration allocates nothing.  One set per op (the latest nrhs): a caller
-        whose batch size varies re-allocates instead of keeping one set per size alive."""
-        key = int(op)
+    def _geom(self, op, nrhs):
+        """The exchange geometry of (op, nrhs) (cached; no tensors): group split, row counts, the
+        two all-to-alls' split sizes and piece counts, element counts of the buffers."""
+        key = (int(op), int(nrhs))
         b = self._buf.get(key)
-        if b is not None and b["nrhs"] != int(nrhs):
-            del self._buf[key]
-            b = None
         if b is None:
             ws, rk = self.ws, self.rank
             rows_in = self.rows_n if op == _lib.OP_R else self.rows_m
@@ -245,7 +244,6 @@ class SlabToeplitz:
             ng = gs1 - gs0
             ni = rows_in[rk][1] - rows_in[rk][0]
             no = rows_out[rk][1] - rows_out[rk][0]
-            cd = self.engine.cdtype
             # E[g][q][i][c] over my input rows; the first all-to-all sends my rows of every group
             # and receives all rows of my groups as rank blocks [r][g][q][i - a_r][c] (rank r's
             # rows [a_r, a_r + cnt_r)); the conv writes the return all-to-all's send buffer as
@@ -263,29 +261,59 @@ class SlabToeplitz:
             # piece counts of the two exchanges from EVERY rank's totals (a2a_parts): identical
             # on all ranks even where uneven splits put the ranks' own totals on either side of
             # a multiple of A2A_MAX_BYTES
-            esz = torch.empty((), dtype=self.engine.cdtype).element_size()
+            esz = self._csize()
             every = [sizes(r) for r in range(ws)]
             parts_fwd = a2a_parts([sum(v) * esz for e in every for v in (e[0], e[1])])
             parts_back = a2a_parts([sum(v) * esz for e in every for v in (e[2], e[3])])
-            b = dict(nrhs=int(nrhs), NG=NG, inner=inner, gs0=gs0, ng=ng, ni=ni, no=no, sizes_in=sizes_in, sizes_rx=sizes_rx,
-                     sizes_tx=sizes_tx, sizes_back=sizes_back, parts_fwd=parts_fwd, parts_back=parts_back,
-                     E=torch.empty((NG, nrhs, ni, inner), dtype=cd, device=dev),
-                     recv=torch.empty(sum(sizes_rx), dtype=cd, device=dev),
-                     send=torch.empty(sum(sizes_tx), dtype=cd, device=dev),
-                     back=torch.empty(NG * nrhs * no * inner, dtype=cd, device=dev))
+            nE, nback = NG * nrhs * ni * inner, NG * nrhs * no * inner
+            b = dict(nrhs=int(nrhs), NG=NG, inner=inner, gs0=gs0, ng=ng, ni=ni, no=no, sizes_in=sizes_in,
+                     sizes_rx=sizes_rx, sizes_tx=sizes_tx, sizes_back=sizes_back, parts_fwd=parts_fwd,
+                     parts_back=parts_back, nE=nE, nback=nback, nrecv=sum(sizes_rx), nsend=sum(sizes_tx))
             self._buf[key] = b
         return b
 
+    def _csize(self):
+        return torch.empty((), dtype=self.engine.cdtype).element_size()
+
+    def xchg_bytes_per_rhs(self, op):
+        """Device bytes of one apply's exchange buffers per right-hand side."""
+        b = self._geom(op, 1)
+        return (max(b["nE"], b["nback"]) + b["nrecv"] + b["nsend"]) * self._csize()
+
+    def _arena_views(self, b, dev):
+        """The buffers of one apply as views of ONE arena shared by every op and chunk (applies
+        run one after another on the stream; nothing in them outlives the apply):
+        [E | back] (E is consumed by the first all-to-all before the second one writes back, so
+        they share storage) + recv + send.  The arena grows to the largest apply and is
+        allocated once: a PCG iteration allocates nothing."""
+        cd = self.engine.cdtype
+        n0 = max(b["nE"], b["nback"])
+        need = n0 + b["nrecv"] + b["nsend"]
+        a = self._arena
+        if a is None or a.numel() < need or a.device != torch.device(dev):
+            self._arena = a = None
+            self._arena = a = torch.empty(need, dtype=cd, device=dev)
+        E = a[:b["nE"]].view(b["NG"], b["nrhs"], b["ni"], b["inner"])
+        back = a[:b["nback"]]
+        recv = a[n0:n0 + b["nrecv"]]
+        send = a[n0 + b["nrecv"]:need]
+        return E, back, recv, send
+
     def release(self):
-        """Drop the cached exchange / all-to-all buffers (they are re-allocated on the next apply)."""
+        """Drop the exchange arena (re-allocated on the next apply)."""
         self._buf.clear()
+        self._arena = None
 
     def apply(self, op, x, out=None, dotv=None, dot_out=None, done=None):
         """op (libhipgp OP_*) on this rank's slab x (nrhs, local in-size) -> local out slab
         (written into `out` when given).  dotv / dot_out: also this rank's per-RHS dots
         sum(out * dotv) (fused into the last stage); done: a device flag after which every
-        stage is a no-op (the slab PCG's masked iterations)."""
-        e = self.engine
+        stage is a no-op (the slab PCG's masked iterations).
+
+        The right-hand sides go through the exchange in chunks of at most `xchg_budget` bytes of
+        buffers (default HGP_SLAB_XCHG_MB = 4096), so the device memory of the exchange does not
+        grow with the batch (config 5's R^T at B = 25 would need 19 GB in one piece); every rank
+        has the same chunking (the geometry is shared), so the collectives line up."""
         x = self._check(x.contiguous(), "x", "n" if op == _lib.OP_R else "m")
         nrhs = x.shape[0]
         if out is not None:
@@ -295,9 +323,23 @@ class SlabToeplitz:
         if dot_out is not None and (dot_out.dtype != x.dtype or dot_out.numel() != nrhs
                                     or not dot_out.is_contiguous() or dot_out.device != x.device):
             raise ValueError(f"dot_out must be a contiguous ({nrhs},) {x.dtype} vector on {x.device}")
-        b = self._bufs(op, nrhs, x.dtype, x.device)
         rest_out = self.rest_n if op == _lib.OP_RT else self.rest_m
-        E, recv, send, back = b["E"], b["recv"], b["send"], b["back"]
+        y = torch.empty((nrhs, self.local_size("n" if op == _lib.OP_RT else "m")), dtype=x.dtype,
+                        device=x.device) if out is None else out
+        if nrhs == 0:
+            return y
+        qc = max(1, min(nrhs, int(self.xchg_budget // max(1, self.xchg_bytes_per_rhs(op)))))
+        for q0 in range(0, nrhs, qc):
+            q1 = min(nrhs, q0 + qc)
+            self._apply_chunk(op, x[q0:q1], y[q0:q1], None if dotv is None else dotv[q0:q1],
+                              None if dot_out is None else dot_out[q0:q1], done, rest_out)
+        return y
+
+    def _apply_chunk(self, op, x, y, dotv, dot_out, done, rest_out):
+        e = self.engine
+        nrhs = x.shape[0]
+        b = self._geom(op, nrhs)
+        E, back, recv, send = self._arena_views(b, x.device)
         ni, no, ng = b["ni"], b["no"], b["ng"]
         # 1. local transforms along the other axes over my input rows
         if ni > 0:
@@ -307,16 +349,14 @@ class SlabToeplitz:
         # 3. the axis-0 convolution of my groups, receive buffer -> send buffer
         if ng > 0:
             e.conv_a2a(op, recv, send, b["gs0"], ng, nrhs, self.ws, done=done)
-        # 4. all-to-all back: all rows of my groups -> my output rows of every group
+        # 4. all-to-all back: all rows of my groups -> my output rows of every group (into E's storage)
         _a2a(back, send, b["sizes_back"], b["sizes_tx"], self.group, b["parts_back"])
         E2 = back.view(b["NG"], nrhs, no, b["inner"])      # groups arrive in rank order = group order
         # 5. local inverse transforms over my output rows (+ fused dot)
-        y = torch.empty((nrhs, no * rest_out), dtype=x.dtype, device=x.device) if out is None else out
         if no > 0:
             e.inv(op, E2, no, y, dotv=dotv, dot_out=dot_out, done=done)
         elif dot_out is not None:
             dot_out.zero_()
-        return y
 
     # -- PCG -------------------------------------------------------------------------------
     def dot(self, a, b):
@@ -443,6 +483,7 @@ class SlabKmm:
         the spectrum of the whole grid (replicated, as `model.toeplitz()` would) and owns its
         axis-0 slab of every vector."""
         T = model.toeplitz()
+        T._plan.trim()                         # the set-up's fp64 transform buffers (GBs at C5)
         return cls(SlabToeplitz(T.dims, HipSlabEngine(T._plan), group=group), column=T.column)
 
     def set_batch_shape(self, batch_shape):
@@ -468,3 +509,63 @@ class SlabKmm:
         with torch.no_grad():
             y = self.slab.apply(_lib.OP_RT, self.slab.scatter_rows(vec.contiguous(), "m"))
             return _all_gather_cols(y, self.slab.group)
+
+
+class SlabFit:
+    """One natural-gradient minibatch of a mean-field model with the inducing grid split into
+    axis-0 slabs over the ranks of `group` and kn KEPT in slabs (`hipgp.py:194-276` with the
+    solve of `hipgp.py:117-146` on SlabToeplitz): per minibatch every rank
+
+    * evaluates only its slab's Knm columns (`_make_grams(grid_rows=...)`: the fused Kuf kernels
+      on the sub-grid xgrids[0][a:b] -- point or line-integral observations; the MC estimator's
+      offset is drawn once and broadcast, `hipgp_amd.dist.shared_mc_offset`);
+    * runs the slab PCG and R^T (`SlabToeplitz.compute_kn`): kn stays (B, its M' slab);
+    * forms the statistics from B-length all-reduced dot partials and its own columns
+      (`MeanFieldToeplitzGP.batch_stats_slab`), summed once over the ranks (`allreduce_stats`:
+      2 M' values), after which every rank takes the same natural-gradient step.
+
+    Nothing of size B x M' is gathered (the `SlabKmm` adapter behind `compute_kn(Kmm=)` gathers
+    d and kn to full rows on every rank); per rank the minibatch holds B x M'/ws of kn.  The
+    plan (spectra of the whole grid, replicated) and the exchange buffers are built once per fit:
+    the grid mode runs with fixed kernel hyper-parameters."""
+
+    def __init__(self, model, group=None, slab=None):
+        if getattr(model, "name", None) != "mean-field" or not hasattr(model, "batch_stats_slab"):
+            raise NotImplementedError("SlabFit keeps kn in slabs for the mean-field family; other families "
+                                      "use SlabKmm (gathered kn)")
+        self.model = model
+        self.group = group
+        if slab is None:
+            T = model.toeplitz()
+            self._T = T                        # keeps the plan (and its spectrum) alive
+            T._plan.trim()                     # the set-up's fp64 transform buffers (GBs at C5)
+            slab = SlabToeplitz(T.dims, HipSlabEngine(T._plan), group=group)
+        self.slab = slab
+        axes = [len(g) for g in model.xgrids]
+        if axes[0] <= 1 or len(slab.dims) != sum(1 for m in axes if m > 1):
+            raise NotImplementedError("grid-block sharding splits axis 0: it needs more than one point there")
+
+    def elbo_and_grad(self, xbatch, ybatch, noise_std_batch=None, maxiter_cg=10, tol=1e-8, integrated_obs=False,
+                      semi_integrated_estimator="analytic", semi_integrated_samps=10, kn_out=None):
+        """ELBO (the same on every rank) and theta1 / theta2 .grad set to minus the natural
+        gradient, as `MeanFieldToeplitzGP.elbo_and_grad`.  kn_out: a list that receives this
+        rank's kn slab and its first expanded-grid column (tests)."""
+        from hipgp_amd.dist import allreduce_stats, shared_mc_offset
+        m, S = self.model, self.slab
+        u = None
+        if integrated_obs and semi_integrated_estimator == "mc-biased":
+            u = shared_mc_offset(m.kernel.dtype, xbatch.device, self.group)
+        a, b = S.my_rows("m")
+        Knm, Knn_diag = m._make_grams(xbatch, integrated_obs=integrated_obs,
+                                      semi_integrated_estimator=semi_integrated_estimator,
+                                      semi_integrated_samps=semi_integrated_samps, mc_offset=u, grid_rows=(a, b))
+        with torch.no_grad():
+            kn = S.compute_kn(Knm.detach().contiguous(), maxiter=maxiter_cg, tol=tol)
+        j0 = S.my_rows("n")[0] * S.rest_n
+        if kn_out is not None:
+            kn_out.extend([kn, j0])
+        stats = m.batch_stats_slab(kn, j0, ybatch, Knn_diag, noise_std_batch,
+                                   reduce=lambda t: _allreduce(t, self.group), lead=S.rank == 0)
+        del kn
+        stats = allreduce_stats(stats, group=self.group)
+        return m.apply_stats(stats, xbatch.shape[0])

@@ -182,14 +182,14 @@ class ToeplitzInducingGP(SviGP):
 
     def elbo_and_grad(self, xbatch, ybatch, noise_std_batch=None, maxiter_cg=10, integrated_obs=False,
                       semi_integrated_estimator="analytic", semi_integrated_samps=10,
-                      print_debug_info=False, Kmm=None):
+                      print_debug_info=False, Kmm=None, mc_offset=None):
         """ELBO estimate; sets theta1.grad / theta2.grad to minus the natural gradient
-        (`hipgp.py:194-276`)."""
+        (`hipgp.py:194-276`).  mc_offset: see `SviGP._make_grams` (sharded fits)."""
         assert self.parameterization == 'expectation-family', \
             "need parameterization=expectation-family when performing natural gradient descent"
         Knm, Knn_diag = self._make_grams(xbatch, integrated_obs=integrated_obs,
                                          semi_integrated_estimator=semi_integrated_estimator,
-                                         semi_integrated_samps=semi_integrated_samps)
+                                         semi_integrated_samps=semi_integrated_samps, mc_offset=mc_offset)
         kn = self.compute_kn(Knm, maxiter_cg=maxiter_cg, Kmm=Kmm)
         stats = self.batch_stats(kn, ybatch, Knn_diag, noise_std_batch)
         elbo = self.apply_stats(stats, xbatch.shape[0])
@@ -398,6 +398,53 @@ class MeanFieldToeplitzGP(ToeplitzInducingGP):
         _lib.check(_lib.lib().hgp_meanfield_stats(_lib.dtype_code(dt), p(knc), B, Mp, p(qmv), p(qSv), p(y), p(iv),
                                                   p(kd), p(lsd), p(an), p(lam), p(dm), _lib.stream_ptr(dev)))
         return {"an_sum": an.sum(), "lam_sum": lam, "dm_sum": dm, "n": B}
+
+    def batch_stats_slab(self, kn, j0, ybatch, Knn_diag, noise_std_batch=None, reduce=None, lead=True):
+        """`batch_stats` of a minibatch whose kn is held in column slabs over ranks (grid-block
+        sharding, `hipgp_amd.slab.SlabFit`): kn (B, w) are this rank's expanded-grid columns
+        [j0, j0 + w).  The per-observation dots kn.qm, |kn|^2 and kn^2.qS are sums over the
+        slabs: this rank's partials (hgp_meanfield_rowdots) go through `reduce` (an in-place SUM
+        all-reduce of the (B, 3) tensor, B values per dot), then a_n and the slab's columns of
+        lam_sum / dm_sum follow as in `batch_stats` (hgp_meanfield_cols), written into zero
+        M'-vectors: summed over the ranks (allreduce_stats) they give the single-process sums.
+        an_sum and n are counted on the `lead` rank only, so that sum is not multiplied."""
+        B, w = kn.shape
+        Mp = self.Mprime
+        with torch.no_grad():
+            qm, qS = self.standard_variational_params()
+            ivar, log_sd = self.noise_terms(noise_std_batch)
+            dev, dt = kn.device, kn.dtype
+            col = lambda v: torch.as_tensor(v, dtype=dt, device=dev).reshape(-1).expand(B).contiguous()
+            qmv = qm.detach().reshape(-1)[j0:j0 + w].to(dt).contiguous()
+            qSv = qS.detach().reshape(-1)[j0:j0 + w].to(dt).contiguous()
+            knc = kn.detach().contiguous()
+            y, iv, kd, lsd = col(ybatch), col(ivar), col(Knn_diag), col(log_sd)
+            if kn.is_cuda:
+                import ctypes
+                from hipgp_amd import _lib
+                p = lambda t: ctypes.c_void_p(t.data_ptr())
+                dots = torch.zeros((B, 3), dtype=dt, device=dev)
+                _lib.check(_lib.lib().hgp_meanfield_rowdots(_lib.dtype_code(dt), p(knc), B, w, p(qmv), p(qSv), p(dots),
+                                                            _lib.stream_ptr(dev)))
+            else:       # CPU tensors only in the gloo host-logic tests
+                kk = knc * knc
+                dots = torch.stack([knc.matmul(qmv), kk.sum(-1), kk.matmul(qSv)], dim=1).contiguous()
+            if reduce is not None:
+                reduce(dots)
+            knm, knkn, knSkn = dots[:, 0], dots[:, 1], dots[:, 2]
+            an = -0.5 * iv * ((knm - y) ** 2 + kd - knkn + knSkn) - lsd - 0.5 * LN_2PI
+            bdiff = (iv * (knm - y)).contiguous()
+            lam = torch.zeros(Mp, dtype=dt, device=dev)
+            dm = torch.zeros(Mp, dtype=dt, device=dev)
+            if kn.is_cuda:
+                ls, ds = lam[j0:j0 + w], dm[j0:j0 + w]
+                _lib.check(_lib.lib().hgp_meanfield_cols(_lib.dtype_code(dt), p(knc), B, w, p(iv), p(bdiff), p(ls), p(ds),
+                                                         _lib.stream_ptr(dev)))
+            else:
+                lam[j0:j0 + w] = torch.sum(iv[:, None] * knc * knc, dim=0)
+                dm[j0:j0 + w] = -(bdiff[None, :].matmul(knc)).reshape(-1)
+            an_sum = an.sum() if lead else an.new_zeros(())
+        return {"an_sum": an_sum, "lam_sum": lam, "dm_sum": dm, "n": B if lead else 0}
 
     def apply_stats(self, stats, bsz):
         """ELBO estimate and theta grads from (all-reduced) batch sums of `bsz` observations."""

@@ -91,13 +91,16 @@ class Kernel(nn.Module):
     def k_semi(self, xpoint, xintegrated, params):
         raise NotImplementedError
 
-    def k_semi_mc(self, xpoint, xintegrated, params, npts=5):
-        """`kernels.py:19-39`: (Np, Ni) = |x_i| mean_a k(xpoint_p, alpha_a x_i)."""
+    def k_semi_mc(self, xpoint, xintegrated, params, npts=5, u=None):
+        """`kernels.py:19-39`: (Np, Ni) = |x_i| mean_a k(xpoint_p, alpha_a x_i).  `u`: the offset
+        draw to use instead of the reference's own torch.rand(1) (sharded fits share rank 0's)."""
         Np, D = xpoint.shape
         Ni, D = xintegrated.shape
         delta = 1. / npts
+        if u is None:
+            u = torch.rand(1, dtype=self.dtype, device=xpoint.device)
         alphas = torch.arange(npts, dtype=self.dtype, device=xpoint.device) / npts + \
-            torch.rand(1, dtype=self.dtype, device=xpoint.device) * delta
+            u.to(device=xpoint.device, dtype=self.dtype).reshape(1) * delta
         xgrid = xintegrated[:, None, :] * alphas[None, :, None]
         Kpis = self.forward(xpoint, xgrid.reshape(-1, D), params=params).reshape(Np, Ni, npts)
         dists = xintegrated.pow(2.).sum(dim=-1).sqrt()

@@ -63,36 +63,49 @@ class SviGP(nn.Module):
         raise NotImplementedError
 
     def _make_grams(self, xbatch, integrated_obs=False, semi_integrated_estimator="analytic",
-                    semi_integrated_samps=10):
+                    semi_integrated_samps=10, mc_offset=None, grid_rows=None):
         """(Knm, Knn_diag) for a minibatch (`svi_gp.py:48-76`): on a grid model the fused HIP
-        kernels of `hipgp_amd.kuf` write Knm directly in the PCG layout."""
+        kernels of `hipgp_amd.kuf` write Knm directly in the PCG layout.
+
+        Not in the reference (sharded fits): mc_offset -- the MC line-integral estimator's offset
+        draw to use instead of drawing one here (`hipgp_amd.dist.shared_mc_offset`); grid_rows =
+        (a, b) -- only the Knm columns of the grid's axis-0 rows [a, b) (a grid-block slab,
+        `hipgp_amd.slab.SlabFit`: columns [a * M / m0, b * M / m0) of the full Knm)."""
         params = self.get_kernel_params()
+        grids, xinduce = getattr(self, "xgrids", None), self.xinduce
+        if grid_rows is not None:
+            a, b = grid_rows
+            rest = self.xinduce.shape[0] // len(grids[0])
+            grids = [grids[0][a:b]] + list(grids[1:])
+            xinduce = xinduce[a * rest:b * rest]
         if integrated_obs:
-            return self._make_integrated_grams(xbatch, params, semi_integrated_estimator, semi_integrated_samps)
+            return self._make_integrated_grams(xbatch, params, semi_integrated_estimator, semi_integrated_samps,
+                                               grids, xinduce, mc_offset)
         Knm = None
-        if getattr(self, "xgrids", None) is not None:
+        if grids is not None:
             from hipgp_amd.kuf import kuf_grid
-            Knm = kuf_grid(self.kernel, self.xgrids, xbatch, params)    # fused HIP kernel
+            Knm = kuf_grid(self.kernel, grids, xbatch, params)          # fused HIP kernel
         if Knm is None:
-            Knm = self.kernel(xbatch, self.xinduce, params)
+            Knm = self.kernel(xbatch, xinduce, params)
         return Knm, self.kernel.diag(xbatch, params)
 
-    def _make_integrated_grams(self, xbatch, params, estimator, samps):
+    def _make_integrated_grams(self, xbatch, params, estimator, samps, grids=None, xinduce=None, mc_offset=None):
         """Line-integral observations, `svi_gp.py:55-69`: Knm by the analytic SqExp integral or
         the biased MC estimator (fused HIP kernels on the grid, `hipgp_amd.kuf`), Knn_diag by the
         doubly-integrated table (`hgp_knn_doubly_diag`)."""
         from hipgp_amd import kuf
-        grids = getattr(self, "xgrids", None)
+        if xinduce is None:
+            grids, xinduce = getattr(self, "xgrids", None), self.xinduce
         if estimator == "analytic":
             Knm = kuf.kuf_semi_sqexp(self.kernel, grids, xbatch, params) if grids is not None else None
             if Knm is None:
-                Knm = self.kernel.k_semi(self.xinduce, xbatch, params).transpose(0, 1)
+                Knm = self.kernel.k_semi(xinduce, xbatch, params).transpose(0, 1)
         elif estimator == "mc-biased":
-            Knm = kuf.kuf_semi_mc(self.kernel, grids, xbatch, params, samps) if grids is not None else None
+            Knm = kuf.kuf_semi_mc(self.kernel, grids, xbatch, params, samps, u=mc_offset) if grids is not None else None
             if Knm is None:
-                Knm = self.kernel.k_semi_mc(self.xinduce, xbatch, params, npts=samps).transpose(0, 1)
+                Knm = self.kernel.k_semi_mc(xinduce, xbatch, params, npts=samps, u=mc_offset).transpose(0, 1)
         elif estimator == "numerical":
-            Knm = self.kernel.k_semi_num(self.xinduce, xbatch, params).transpose(0, 1)
+            Knm = self.kernel.k_semi_num(xinduce, xbatch, params).transpose(0, 1)
         else:
             raise NotImplementedError
         return Knm, self.kernel.k_doubly_diag(xbatch, params)
@@ -182,8 +195,12 @@ def _fit_options(kw):
     # (sharded when torch.distributed is initialised with world size > 1), True, False;
     # "shard": "rhs" (each rank solves its rows of every minibatch, hipgp_amd.dist) or "grid"
     # (each rank owns an axis-0 slab of the inducing grid, hipgp_amd.slab.SlabKmm)
+    # "slab": a prebuilt hipgp_amd.slab.SlabToeplitz for shard="grid" (tests inject a CPU engine);
+    # "dist_timeout_s": the process-group timeout when the fit initialises the group itself --
+    # only rank 0 runs the epoch callback (predictions), the other ranks wait at a barrier
     o.update(distributed=kw.get("distributed", "auto"), shard=kw.get("shard", "rhs"),
-             process_group=kw.get("process_group", None), compute_kn=kw.get("compute_kn", None))
+             process_group=kw.get("process_group", None), compute_kn=kw.get("compute_kn", None),
+             slab=kw.get("slab", None), dist_timeout_s=kw.get("dist_timeout_s", 4 * 3600))
     assert o["shard"] in ("rhs", "grid"), "shard must be 'rhs' or 'grid', got {}".format(o["shard"])
     return o
 
@@ -212,12 +229,14 @@ def _fit_world(o, mod=None):
     up = dist.is_available() and dist.is_initialized()
     if (not up and o["distributed"] is not False and dist.is_available()
             and int(os.environ.get("WORLD_SIZE", "1")) > 1):
+        import datetime
+        timeout = datetime.timedelta(seconds=float(o["dist_timeout_s"]))
         if o["do_cuda"]:
             local = int(os.environ.get("LOCAL_RANK", "0"))
             torch.cuda.set_device(local)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=timeout)
         else:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=timeout)
         up = True
     if o["distributed"] is False or (o["distributed"] == "auto" and not (up and dist.get_world_size(o["process_group"]) > 1)):
         return False, 1, 0
@@ -250,8 +269,8 @@ def svigp_fit(mod, odir, xtrain, ytrain, noise_std_train, xtest, ftest, etest, x
     sharded, world_size, rank = _fit_world(o, mod)
     if sharded and "LOCAL_RANK" in os.environ:
         o["cuda_num"] = int(os.environ["LOCAL_RANK"])
-    if sharded and o["shard"] == "grid" and (o["learn_kernel"] or o["learn_noise"] or o["integrated_obs"]):
-        raise NotImplementedError("shard='grid' runs the natural-gradient fit of point observations with fixed "
+    if sharded and o["shard"] == "grid" and (o["learn_kernel"] or o["learn_noise"]):
+        raise NotImplementedError("shard='grid' runs the natural-gradient fit with fixed kernel / noise "
                                   "hyper-parameters; use shard='rhs' to learn them")
     device = torch.device("cuda:{}".format(o["cuda_num"]))
     print0 = print if rank == 0 else (lambda *a, **k: None)
@@ -286,6 +305,16 @@ def svigp_fit(mod, odir, xtrain, ytrain, noise_std_train, xtest, ftest, etest, x
         print0("device: cuda:{}".format(o["cuda_num"]))
         mod = mod.cuda_params(o["cuda_num"])
 
+    # grid-block sharding: the slab operators are built once (the kernel is fixed in this mode);
+    # the mean-field family keeps kn in slabs (SlabFit), the block family gathers it (SlabKmm)
+    slabfit = kmm = None
+    if sharded and o["shard"] == "grid":
+        from hipgp_amd.slab import SlabFit, SlabKmm
+        if getattr(mod, "name", None) == "mean-field":
+            slabfit = SlabFit(mod, group=o["process_group"], slab=o["slab"])
+        else:
+            kmm = SlabKmm.from_model(mod, group=o["process_group"]) if o["slab"] is None else SlabKmm(o["slab"])
+
     trace = []
     mod.fit_trace = trace
     best_elbo = -np.inf
@@ -319,15 +348,19 @@ def svigp_fit(mod, odir, xtrain, ytrain, noise_std_train, xtest, ftest, etest, x
                                                    integrated_obs=o["integrated_obs"],
                                                    semi_integrated_estimator=estimator,
                                                    semi_integrated_samps=o["num_semi_mc_samples"])
+            elif slabfit is not None:           # shard == "grid", mean-field: kn stays in slabs
+                lval = slabfit.elbo_and_grad(xb, yb, sb, maxiter_cg=o["maxiter_cg"], integrated_obs=o["integrated_obs"],
+                                             semi_integrated_estimator=estimator,
+                                             semi_integrated_samps=o["num_semi_mc_samples"])
             else:
-                kmm = None
-                if sharded:                     # shard == "grid": the solve on axis-0 slabs
-                    from hipgp_amd.slab import SlabKmm
-                    kmm = SlabKmm.from_model(mod, group=o["process_group"])
+                u = None
+                if kmm is not None and o["integrated_obs"] and estimator == "mc-biased":
+                    from hipgp_amd.dist import shared_mc_offset
+                    u = shared_mc_offset(mod.kernel.dtype, xb.device, o["process_group"])
                 lval = mod.elbo_and_grad(xbatch=xb, ybatch=yb, noise_std_batch=sb, maxiter_cg=o["maxiter_cg"],
                                          integrated_obs=o["integrated_obs"], semi_integrated_estimator=estimator,
                                          semi_integrated_samps=o["num_semi_mc_samples"],
-                                         print_debug_info=o["print_debug_info"], Kmm=kmm)
+                                         print_debug_info=o["print_debug_info"], Kmm=kmm, mc_offset=u)
             if hyper_opt is not None:
                 (-lval).backward()
                 if sharded:
@@ -378,6 +411,11 @@ def svigp_fit(mod, odir, xtrain, ytrain, noise_std_train, xtest, ftest, etest, x
                                    xvalid=xvalid, fvalid=fvalid, evalid=evalid)
         for k, v in zip(("ftest_eval", "etest_eval", "fgrid_eval", "egrid_eval", "fvalid_eval", "evalid_eval"), evals):
             times[k].append(v)
+        if sharded:
+            # the other ranks wait here while rank 0 runs the epoch callback (its own timeout:
+            # dist_timeout_s when this fit initialised the group)
+            import torch.distributed as dist
+            dist.barrier(group=o["process_group"])
 
     report = pd.DataFrame(times, index=["epoch{}".format(i) for i in range(o["epochs"])])
     report.loc["Total"] = report.sum()

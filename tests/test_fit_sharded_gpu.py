@@ -51,12 +51,41 @@ def _g19_model(fx):
     return mod, dict(lr=1e-2, schedule_lr=False, batch_size=200, epochs=1, maxiter_cg=20, learn_kernel=False)
 
 
-def _run(case, distributed, shard="rhs", nbatch=None):
-    if case == "g19":
+def _semi_model():
+    """Config 5's kind of fit on a small 3-D grid (10 x 9 x 8): line-integral observations
+    (`run_domain_experiment.py:276` trains with integrated_obs), a Matern-5/2 kernel (no k_semi:
+    the MC estimator, `svi_gp.py:61-64`, whose offset the shards must share)."""
+    import ziggy.hipgp as hg
+    import ziggy.kernels as zk
+    dt = torch.float64
+    grids = [torch.linspace(-1, 1, 10, dtype=dt), torch.linspace(-1, 1, 9, dtype=dt),
+             torch.linspace(-.5, .5, 8, dtype=dt)]
+    # well-conditioned (ell 0.2, nugget 1e-2): 20 PCG iterations of two exact implementations (the
+    # oracle and the slab recurrence) agree to 5e-16 there, so 1e-10 pins the sharding; at ell 0.25
+    # (0.14 spacing along z) they end 4.5e-11 apart and a fit step amplifies that to 1e-9
+    mod = hg.MeanFieldToeplitzGP(zk.Matern(nu=2.5, dtype=dt), grids, num_obs=64, sig2_init=1., ell_init=.2,
+                                 init_Svar=.5, learn_kernel=False, jitter_val=1e-2, dtype=dt)
+    rs = np.random.RandomState(5)
+    x = rs.uniform(-.9, .9, (64, 3)) * np.array([1, 1, .5])
+    y = np.sin(2 * x[:, :1]) * np.cos(x[:, 1:2]) + .05 * rs.randn(64, 1)
+    s = np.full((64, 1), .1)
+    with torch.no_grad():
+        mod.global_theta1.copy_(torch.tensor(rs.randn(mod.Mprime, 1) * .1))
+    kw = dict(lr=1e-2, batch_size=16, epochs=1, maxiter_cg=20, learn_kernel=False, integrated_obs=True,
+              semi_integrated_estimator="mc-biased", num_semi_mc_samples=10)
+    return mod, kw, (x, y, s)
+
+
+def _run(case, distributed, shard="rhs", nbatch=None, seed=None):
+    if seed is not None:
+        torch.manual_seed(seed)
+    if case == "semi":
+        mod, kw, (x, y, s) = _semi_model()
+    elif case == "g19":
         fx = load("G19", "f64")
         mod, kw = _g19_model(fx)
         x, y, s = (fx[f"box_{k}"] for k in "xys")
-    else:
+    if case not in ("semi", "g19"):
         fx = load("G18", "f64")
         mod, kw = _g18_model(fx, case)
         x, y, s = (fx[f"{case}_{k}"] for k in "xys")
@@ -73,7 +102,8 @@ def _run(case, distributed, shard="rhs", nbatch=None):
 
 
 RUNS = {"g18_ng_rhs": ("ng", "rhs", None), "g18_hk_rhs": ("hk", "rhs", None),
-        "g19_box_rhs": ("g19", "rhs", 5), "g19_box_grid": ("g19", "grid", 5)}
+        "g19_box_rhs": ("g19", "rhs", 5), "g19_box_grid": ("g19", "grid", 5),
+        "semi_rhs": ("semi", "rhs", None), "semi_grid": ("semi", "grid", None)}
 
 
 def _worker(rank, ws, port, backend, what, out):
@@ -100,7 +130,9 @@ def _worker(rank, ws, port, backend, what, out):
             out[rank] = kn.cpu().numpy()
         else:
             case, shard, nb = RUNS[what]
-            out[rank] = _run(case, True, shard, nb)
+            # the line-integral runs seed every rank differently: the MC offset must come from
+            # rank 0's draw (hipgp_amd.dist.shared_mc_offset), not from alike-seeded RNGs
+            out[rank] = _run(case, True, shard, nb, seed=1000 + rank if case == "semi" else None)
     finally:
         dist.destroy_process_group()
 
@@ -116,10 +148,14 @@ def _spawn(ws, backend, what):
 
 @pytest.mark.parametrize("what,ws,backend", [("g18_ng_rhs", 2, "gloo"), ("g18_hk_rhs", 2, "gloo"),
                                              ("g19_box_rhs", 2, "gloo"), ("g19_box_grid", 2, "gloo"),
-                                             ("g19_box_rhs", 1, "nccl")])
+                                             ("g19_box_rhs", 1, "nccl"), ("g19_box_grid", 1, "nccl"),
+                                             ("semi_rhs", 2, "gloo"), ("semi_grid", 2, "gloo"),
+                                             ("semi_grid", 1, "nccl")])
 def test_sharded_fit_matches_single_process(what, ws, backend):
+    """g19_box_grid / semi_grid: shard="grid" on the mean-field family keeps kn in slabs
+    (hipgp_amd.slab.SlabFit); semi_*: line-integral observations (config 5's observation type)."""
     case, shard, nb = RUNS[what]
-    ref_snaps, ref_trace = _run(case, False, nbatch=nb)
+    ref_snaps, ref_trace = _run(case, False, nbatch=nb, seed=1000 if case == "semi" else None)
     res = _spawn(ws, backend, what)
     for r, (snaps, trace) in enumerate(res):
         assert snaps.shape == ref_snaps.shape
@@ -146,3 +182,74 @@ def test_slab_compute_kn_G5():
         for r, kn in enumerate(_spawn(ws, backend, "g5_slab")):
             assert rel_err(kn, fx["kn"]) < 1e-8, (ws, r, rel_err(kn, fx["kn"]))
             assert rel_err(kn, kn1) < 1e-10, (ws, r, rel_err(kn, kn1))
+
+
+def _c5_mem_worker(rank, ws, port, mode, out):
+    """One config-5 minibatch (256 x 256 x 128 grid, Matern-5/2, fp32, B = 25 line-integral
+    observations, MC estimator) on two same-device ranks in `mode` ("gather": SlabKmm behind
+    compute_kn(Kmm=), full kn on every rank; "slab": SlabFit, kn kept in slabs).  Records the
+    rank's peak torch allocation during the step, the plan's device bytes outside torch, the
+    ELBO and the theta gradients' norms."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        import ziggy.hipgp as hg
+        import ziggy.kernels as zk
+        from hipgp_amd.dist import shared_mc_offset
+        from hipgp_amd.slab import SlabFit, SlabKmm
+        dt = torch.float32
+        grids = [torch.linspace(-1, 1, 256, dtype=dt), torch.linspace(-1, 1, 256, dtype=dt),
+                 torch.linspace(-.5, .5, 128, dtype=dt)]
+        mod = hg.MeanFieldToeplitzGP(zk.Matern(nu=2.5, dtype=dt), grids, num_obs=100_000, sig2_init=1.,
+                                     ell_init=.1, learn_kernel=False, jitter_val=1e-3, dtype=dt).cuda_params(0)
+        g = torch.Generator().manual_seed(7)
+        x = ((torch.rand(25, 3, generator=g) * 2 - 1) * torch.tensor([.9, .9, .45])).to(DEV)
+        y = torch.randn(25, 1, generator=g).to(DEV)
+        s = torch.full((25, 1), .1, device=DEV)
+        torch.manual_seed(11)
+        if mode == "slab":
+            fit = SlabFit(mod)
+            step = lambda: fit.elbo_and_grad(x, y, s, maxiter_cg=2, integrated_obs=True,
+                                             semi_integrated_estimator="mc-biased", semi_integrated_samps=10)
+            plan = fit.slab.engine.plan
+        else:
+            kmm = SlabKmm.from_model(mod)
+            plan = kmm.slab.engine.plan
+            step = lambda: mod.elbo_and_grad(x, y, s, maxiter_cg=2, integrated_obs=True,
+                                             semi_integrated_estimator="mc-biased", semi_integrated_samps=10,
+                                             Kmm=kmm, mc_offset=shared_mc_offset(dt, x.device))
+        torch.cuda.synchronize()
+        base = torch.cuda.memory_allocated()
+        torch.cuda.reset_peak_memory_stats()
+        elbo = float(step())
+        torch.cuda.synchronize()
+        pm = plan.mem()
+        out[rank] = {"peak_torch": torch.cuda.max_memory_allocated(), "base_torch": base,
+                     "plan_scratch": pm["scratch"], "plan_tables": pm["tables"], "elbo": elbo,
+                     "g1": float(mod.global_theta1.grad.norm()), "g2": float(mod.global_theta2.grad.norm())}
+    finally:
+        dist.destroy_process_group()
+
+
+def test_grid_fit_memory_C5_geometry():
+    """Round 6: at config 5's geometry (B = 25, two same-device ranks) keeping kn
+    in slabs needs at most 0.6x the per-rank device memory of the gathering SlabKmm path (torch
+    peak during the minibatch + the plan's own buffers), with the same ELBO and gradients."""
+    res = {}
+    for mode in ("gather", "slab"):
+        mgr = mp.Manager()
+        out = mgr.dict()
+        port = 29760 + os.getpid() % 100 + (1 if mode == "slab" else 0)
+        mp.spawn(_c5_mem_worker, args=(2, port, mode, out), nprocs=2, join=True)
+        res[mode] = [dict(out[r]) for r in range(2)]
+    tot = {m: max(r["peak_torch"] + r["plan_scratch"] + r["plan_tables"] for r in res[m]) for m in res}
+    print("C5 B=25 ws2 per-rank device bytes:", {m: round(v / 2**30, 2) for m, v in tot.items()},
+          "ratio", tot["slab"] / tot["gather"], res)
+    assert tot["slab"] <= 0.6 * tot["gather"], (tot, res)
+    for r in range(2):
+        a, b = res["gather"][r], res["slab"][r]
+        assert abs(a["elbo"] - b["elbo"]) <= 1e-4 * abs(a["elbo"]), (a, b)
+        assert abs(a["g1"] - b["g1"]) <= 1e-4 * a["g1"] and abs(a["g2"] - b["g2"]) <= 1e-4 * a["g2"], (a, b)

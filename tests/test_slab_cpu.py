@@ -37,6 +37,8 @@ def _worker(rank, ws, port, case, out, a2a_max=None):
             slab.A2A_MAX_BYTES = a2a_max     # exchanges in pieces (same count on every rank)
         T = _oracle(case)
         S = SlabToeplitz(T.dims, CpuSlabEngine(T))
+        if a2a_max is not None:
+            S.xchg_budget = 1                # and one right-hand side per exchange chunk
         rs = np.random.RandomState(4)
         v = torch.tensor(rs.randn(3, T.M))
         w = torch.tensor(rs.randn(3, T.Mp))
@@ -89,10 +91,11 @@ def test_slab_ops_and_pcg_gloo(case, ws):
 
 
 def test_slab_split_exchanges_uneven_gloo():
-    """Exchanges split into pieces (A2A_MAX_BYTES lowered to 2 KiB) with uneven row splits (13
+    """Exchanges split into pieces (A2A_MAX_BYTES lowered to 256 bytes) with uneven row splits (13
     rows, 24 expanded rows over 3 ranks): every rank must issue the same number of pieces --
     the count comes from the largest rank's total, not the rank's own -- and the results stay
-    the oracle's (hipgp_amd/slab.py a2a_parts)."""
+    the oracle's (hipgp_amd/slab.py a2a_parts).  The right-hand sides also go through
+    the exchange one at a time (xchg_budget: the chunked apply, one shared arena)."""
     case, ws = "2d", 3
     T = _oracle(case)
     rs = np.random.RandomState(4)
@@ -101,7 +104,7 @@ def test_slab_split_exchanges_uneven_gloo():
     mgr = mp.Manager()
     out = mgr.dict()
     port = 29700 + os.getpid() % 90
-    mp.spawn(_worker, args=(ws, port, case, out, 2048), nprocs=ws, join=True)
+    mp.spawn(_worker, args=(ws, port, case, out, 256), nprocs=ws, join=True)
     assert len(out) == ws
     parts = [out[r]["parts"] for r in range(ws)]
     assert all(p == parts[0] for p in parts), parts

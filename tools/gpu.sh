@@ -8,6 +8,7 @@
 #   pytest            the whole -m gpu suite            pytest=EXPR   only tests matching -k EXPR
 #   smoke             __graft_entry__.smoke()
 #   bench             python bench.py (defaults)        bench=ARGS    with these arguments ('+' = space)
+#   bench_trim[=ARGS] the bench with HGP_POOL_MB=1024 (idle plans trimmed: per-call re-allocation)
 #   configs           tools/bench_configs.py (five-config table)
 #   phases[=C2,C4]    tools/kn_phases.py --only ...
 #   passtime=D/B/OP[,D/B/OP...]   tools/passtime.py --dims D --rhs B --op OP (D: 4096x4096)
@@ -49,6 +50,12 @@ print("bench:", round(d["value"]), "RHS-matvecs/s", round(d["ms_per_step"], 4), 
       c4.get("ms"), c4.get("phase_median_ms"), c4.get("plan_scratch_bytes"), c4.get("error"))
 EOF
       ;;
+    bench_trim)
+      # the config-4 leg with the idle-plan pool forced to trim (HGP_POOL_MB=1024): every call
+      # re-allocates the plan's scratch, as round 5's 62 GB C4 plan did under the 1/8 budget
+      HGP_POOL_MB=1024 timeout -k 10 600 python bench.py --no-cpu-baseline $arg > ${O}_bench_trim.json 2> ${O}_bench_trim.err \
+        || fail "$step" $? ${O}_bench_trim.err
+      python -c "import json,sys; d=json.loads(open('${O}_bench_trim.json').read().strip().splitlines()[-1]); print('trimmed pool C4 leg:', json.dumps(d.get('strong_c4')))" ;;
     configs)
       timeout -k 10 900 python tools/bench_configs.py > ${O}_configs.jsonl 2> ${O}_configs.err || fail "$step" $? ${O}_configs.err
       cat ${O}_configs.jsonl ;;
