@@ -107,6 +107,11 @@ def test_meanfield_elbo_C3():
         assert float((a - b).norm() / b.norm()) < 1e-4, float((a - b).norm() / b.norm())
 
 
+# fp32 vs the fp64 plan at B = 200 (solve, kn): 10x the largest gap measured on the GPU, instead
+# of round 5's flat 1e-3 (profiles/r6_B200_gaps.txt: C3 1.13e-5 / 5.80e-6, C4 1.14e-5 / 5.88e-6)
+B200_BOUND = {2048: (1.2e-4, 6e-5), 4096: (1.2e-4, 6e-5)}
+
+
 @pytest.mark.parametrize("m", [2048, 4096], ids=["C3_2048x2048_B200", "C4_4096x4096_B200"])
 def test_configs_own_batch_B200(m):
     """The configs' own minibatch (C3 / C4: 200 RHS, `run_ukhousing_experiment.py:31`,
@@ -114,10 +119,11 @@ def test_configs_own_batch_B200(m):
     `_solve` and `compute_kn` of all 200 RHS in one call.  A seeded subset of 5 rows (first,
     last, chunk-boundary neighbours and a middle row) is checked (a) against the fp64 plan of
     the same problem -- SURVEY §8(c)'s PCG rule in the form the other full-size tests use here
-    (nugget 0.1: fp32 and fp64 differ by the implementation's rounding, ~1e-5; bound 1e-3) -- and
+    (nugget 0.1: fp32 and fp64 differ by the implementation's rounding, ~1e-5) -- and
     (b) against the same rows solved in a batch of 2 (other chunks, other streams, other batch
     positions): every RHS runs its own FFTs and fixed-order reductions, so a row's result does
-    not depend on the batch around it -- bitwise in practice, held to 1e-6."""
+    not depend on the batch around it -- bitwise in practice, held to 1e-6.  The fp64 bound is
+    10x the measured gap (B200_BOUND)."""
     B = 200
     g = torch.Generator(device=DEV).manual_seed(31)
     b = torch.randn(B, m * m, device=DEV, generator=g, dtype=torch.float32)
@@ -146,9 +152,10 @@ def test_configs_own_batch_B200(m):
     b64 = b[rows].double()
     x64 = T64._solve(b64, do_precond=True, maxiter=20, tol=1e-8)
     rel = float(((xs - x64).norm(dim=1) / x64.norm(dim=1)).max())
-    assert rel < 1e-3, rel
     res = (T64._matmul_by_K(xs) - b64).norm(dim=1) / b64.norm(dim=1)
-    assert float(res.max()) < 0.05, res
     kn64 = T64._matmul_by_RT(T64.inv_matmul(b64, do_precond=True, maxiter=20, tol=1e-8))
     rel_kn = float(((kns - kn64).norm(dim=1) / kn64.norm(dim=1)).max())
-    assert rel_kn < 1e-3, rel_kn
+    print(f"B200 m={m}: solve fp32 vs fp64 {rel:.3e}, kn {rel_kn:.3e}, residual {float(res.max()):.3e}")
+    assert rel < B200_BOUND[m][0], rel
+    assert float(res.max()) < 0.05, res
+    assert rel_kn < B200_BOUND[m][1], rel_kn

@@ -21,9 +21,13 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     dist.init_process_group("nccl", device_id=dev)
-    G = 1 << 30
-    sizes = [2 * G - (1 << 20), 2 * G + (1 << 20), int(2.4e9), 4 * G - (1 << 20), 4 * G + (1 << 20)]
-    for dtype in (torch.float64, torch.float32, torch.uint8):
+    G, Mi = 1 << 30, 1 << 20
+    # round 6, first probe (profiles/r6_a2a_limit.jsonl): every size from 2 GiB - 1 MiB up came back
+    # with exactly its second half wrong; this sweep brackets the threshold below that
+    sizes = [256 * Mi, 512 * Mi, G - Mi, G, G + Mi, G + 256 * Mi, G + 512 * Mi, 2 * G - 256 * Mi, 2 * G - Mi]
+    if os.environ.get("A2A_SIZES"):
+        sizes = [int(float(v)) for v in os.environ["A2A_SIZES"].split(",")]
+    for dtype in (torch.float32, torch.float64):
         esz = torch.empty((), dtype=dtype).element_size()
         for nbytes in sizes:
             n = nbytes // esz
@@ -43,9 +47,13 @@ def main():
                     res["ok"] = nbad == 0
                     res["mismatches"] = nbad
                     if nbad:
-                        idx = torch.nonzero(bad)[:, 0]
-                        res["first_bad_byte"] = int(idx[0]) * esz
-                        res["last_bad_byte"] = int(idx[-1]) * esz
+                        blk = 1 << 12                 # locate the bad range by 4096-element blocks
+                        nb = n // blk
+                        anyb = bad[:nb * blk].view(nb, blk).any(dim=1)
+                        idx = torch.nonzero(anyb)[:, 0]
+                        if idx.numel():
+                            res["first_bad_byte"] = int(idx[0]) * blk * esz
+                            res["last_bad_block_end_byte"] = (int(idx[-1]) + 1) * blk * esz
                     del src, out, bad
                 except RuntimeError as e:
                     res["ok"] = False

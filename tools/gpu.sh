@@ -14,7 +14,7 @@
 #   passtime=D/B/OP[,D/B/OP...]   tools/passtime.py --dims D --rhs B --op OP (D: 4096x4096)
 #   profile           rocprofv3 --kernel-trace --stats of the bench (tools/profile.sh)
 #   pmc               PMC HBM bytes of the C2 K matvec (tools/pmc_kop.sh)
-#   py=SCRIPT+ARGS    any python script (timeout 600 s)
+#   py=SCRIPT+ARGS    any python script (timeout 600 s; log ${TAG}_py<k>.log for the k-th py step)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -22,6 +22,7 @@ export TMPDIR=/tmp
 TAG=${TAG:-run}
 O=gpurun_out/${TAG}
 
+npy=0
 fail() { echo "[gpu.sh] step '$1' failed (rc $2)"; [ -n "$3" ] && tail -30 "$3"; exit 1; }
 
 for step in "$@"; do
@@ -76,8 +77,9 @@ EOF
       bash tools/pmc_kop.sh > ${O}_pmc_kop.log 2>&1 || fail "$step" $? ${O}_pmc_kop.log
       grep traffic_bytes_per_op gpurun_out/pmc_kop/pmc_kop_C2.json ;;
     py)
-      timeout -k 10 600 python -u $arg > ${O}_py.log 2>&1 || fail "$step" $? ${O}_py.log
-      tail -40 ${O}_py.log ;;
+      npy=$((npy + 1))
+      timeout -k 10 600 python -u $arg > ${O}_py${npy}.log 2>&1 || fail "$step" $? ${O}_py${npy}.log
+      tail -40 ${O}_py${npy}.log ;;
     *)
       echo "[gpu.sh] unknown step '$step'"; exit 2 ;;
   esac
