@@ -1,6 +1,8 @@
 // hgp_pass_dispatch.hpp — instantiation + launch of k_pass for one dtype (included by
 // hgp_pass_f32.hip / hgp_pass_f64.hip so the two compile in parallel).
 #pragma once
+#include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 #include "hgp_internal.hpp"
@@ -9,17 +11,33 @@
 
 namespace hgp {
 
+// Co-residency experiments (round 6): a minimum dynamic-LDS request per block for the
+// 2-D column conv (HGP_CONV_LDS_MIN), row-forward (HGP_ROWF_LDS_MIN) and row-inverse
+// (HGP_ROWI_LDS_MIN) kernels, in bytes, caps how many blocks of one kind a CU takes, so the other
+// stream's pass can share the CU.  Unset (0): the kernel's own LDS size.  Read once per process.
+inline int lds_min_env(const char* name) {
+  const char* e = std::getenv(name);
+  const int v = e ? std::atoi(e) : 0;
+  return v < 0 ? 0 : (v > LDS_CAP ? LDS_CAP : v);
+}
+inline int lds_conv_min() { static const int v = lds_min_env("HGP_CONV_LDS_MIN"); return v; }
+inline int lds_rowf_min() { static const int v = lds_min_env("HGP_ROWF_LDS_MIN"); return v; }
+inline int lds_rowi_min() { static const int v = lds_min_env("HGP_ROWI_LDS_MIN"); return v; }
+
 template <typename T, int H, int MODE, int LAY>
 static hipError_t launch_one(const PassDesc& d, int64_t nblocks, hipStream_t s) {
   using Cfg = PassCfg<T, H, LAY>;
+  constexpr bool col2d = (MODE == PASS_CONV || MODE == PASS_CONVC) &&
+                         (LAY == LAY_CONTIG || LAY == LAY_CONTIG_G || LAY == LAY_CONTIG_Q);
+  const int lds = col2d ? std::max<int>(Cfg::LDS, lds_conv_min()) : Cfg::LDS;
   static bool attr_set = false;   // opt in to > 64 KB dynamic LDS once per instance
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)k_pass<T, H, MODE, LAY>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS);
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  hipLaunchKernelGGL((k_pass<T, H, MODE, LAY>), dim3((unsigned)nblocks), dim3(Cfg::THREADS), Cfg::LDS, s, d);
+  hipLaunchKernelGGL((k_pass<T, H, MODE, LAY>), dim3((unsigned)nblocks), dim3(Cfg::THREADS), lds, s, d);
   return hipGetLastError();
 }
 
@@ -123,14 +141,15 @@ static hipError_t launch_rowt_inv(const PassDesc& d, hipStream_t s) {
   using Cfg = RowTCfg<T, H, G, true>;
   const int64_t nb = (int64_t)d.Q * ((d.Rn + Cfg::C - 1) / Cfg::C);
   if (nb <= 0) return hipSuccess;
+  const int lds = std::max<int>(Cfg::LDS, lds_rowi_min());
   static bool attr_set = false;   // opt in to > 64 KB dynamic LDS once per instance
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)k_row_inv_t<T, H, EPI, G>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS);
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  hipLaunchKernelGGL((k_row_inv_t<T, H, EPI, G>), dim3((unsigned)nb), dim3(Cfg::THREADS), Cfg::LDS, s, d);
+  hipLaunchKernelGGL((k_row_inv_t<T, H, EPI, G>), dim3((unsigned)nb), dim3(Cfg::THREADS), lds, s, d);
   return hipGetLastError();
 }
 
@@ -148,13 +167,14 @@ static hipError_t launch_rowt_g(int inv, int epi, const PassDesc& d, hipStream_t
   }
   const int64_t nb = (int64_t)d.Q * ((d.Rn + Cfg::C - 1) / Cfg::C);
   if (nb <= 0) return hipSuccess;
+  const int lds = std::max<int>(Cfg::LDS, lds_rowf_min());
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_row_fwd_t<T, H, G>, hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS);
+    hipError_t e = hipFuncSetAttribute((const void*)k_row_fwd_t<T, H, G>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  hipLaunchKernelGGL((k_row_fwd_t<T, H, G>), dim3((unsigned)nb), dim3(Cfg::THREADS), Cfg::LDS, s, d);
+  hipLaunchKernelGGL((k_row_fwd_t<T, H, G>), dim3((unsigned)nb), dim3(Cfg::THREADS), lds, s, d);
   return hipGetLastError();
 }
 

@@ -1,0 +1,49 @@
+"""Co-residency sweep (GPU box): the batched K op (and others) timed by tools/passtime.py in fresh
+processes under different minimum-LDS requests of the 2-D column conv / row kernels
+(HGP_CONV_LDS_MIN, HGP_ROWF_LDS_MIN, HGP_ROWI_LDS_MIN; hgp_pass_dispatch.hpp), which cap how
+many blocks of one kind a CU takes so that the two RHS streams' passes can share CUs.
+
+    python tools/lds_sweep.py [--cases "4096x4096/25/K;..."] [--settings "-;C=54000;C=54000,F=80000"]
+Each setting runs as a child process (this process never touches the GPU)."""
+import argparse
+import json
+import os
+import subprocess
+import sys
+
+KEYS = {"C": "HGP_CONV_LDS_MIN", "F": "HGP_ROWF_LDS_MIN", "I": "HGP_ROWI_LDS_MIN"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cases", default="4096x4096/25/K;4096x4096/25/CINV;2048x2048/200/K;1024x1024/32/K")
+    ap.add_argument("--settings", default="-;C=41000;C=54000;C=81000;I=41000;C=54000,I=54000")
+    ap.add_argument("--reps", type=int, default=2)
+    a = ap.parse_args()
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cases = [c for c in a.cases.split(";") if c]
+    for setting in a.settings.split(";"):
+        env = dict(os.environ)
+        for kv in ([] if setting.strip() in ("", "-") else setting.split(",")):
+            k, v = kv.split("=")
+            env[KEYS[k.strip()]] = v.strip()
+        for case in cases:
+            dims, rhs, op = case.split("/")
+            dims = dims.replace("x", ",")
+            for rep in range(a.reps):
+                r = subprocess.run([sys.executable, os.path.join(root, "tools", "passtime.py"), "--dims", dims,
+                                    "--rhs", rhs, "--op", op], env=env, capture_output=True, text=True, timeout=300)
+                line = r.stdout.strip().splitlines()[-1] if r.stdout.strip() else ""
+                try:
+                    d = json.loads(line)
+                except ValueError:
+                    print(json.dumps({"setting": setting, "case": case, "error": r.stderr[-400:]}), flush=True)
+                    if r.returncode not in (0, 1):
+                        sys.exit(r.returncode)
+                    continue
+                print(json.dumps({"setting": setting, "case": case, "rep": rep, "op_ms": d["op_ms"],
+                                  "passes_ms": d["passes_ms"], "frac": d.get("frac")}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
