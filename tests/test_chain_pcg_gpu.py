@@ -33,7 +33,10 @@ def _plan(dims, dt, chain):
     return P
 
 
-@pytest.mark.parametrize("dt,maxiter,tol,bound", [(torch.float64, 20, -1.0, 1e-12), (torch.float64, 500, 1.0, 1e-12),
+# 20 iterations: the two orders of the same arithmetic agree to ~1e-13 (fp64); run to the break
+# (115 iterations on this problem) the Krylov recurrence amplifies that rounding to ~5e-6 -- the
+# same iteration count and a converged true residual are what the break case pins
+@pytest.mark.parametrize("dt,maxiter,tol,bound", [(torch.float64, 20, -1.0, 1e-12), (torch.float64, 500, 1.0, 1e-4),
                                                   (torch.float32, 20, -1.0, 1e-5)])
 def test_chained_pcg_matches_default(dt, maxiter, tol, bound):
     dims = (300, 260)
@@ -43,6 +46,10 @@ def test_chained_pcg_matches_default(dt, maxiter, tol, bound):
     for chain in (False, True):
         P = _plan(dims, dt, chain)
         x, it = P.pcg(b, maxiter, tol, precond=True, return_iters=True)
+        if tol > 0:     # the break's own test: every RHS's true residual below tol (to rounding)
+            from hipgp_amd import _lib
+            res = (P.apply(_lib.OP_K, x) - b).norm(dim=1)
+            assert float(res.max()) < 1.05 * tol, (chain, res)
         out[chain] = (x.double().cpu().numpy(), it)
         del P
     (x0, it0), (x1, it1) = out[False], out[True]
