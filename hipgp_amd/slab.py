@@ -35,9 +35,12 @@ def split(n, parts, k):
     return start, start + base + (1 if k < extra else 0)
 
 
-# largest all-to-all handed to RCCL in one call: a 2.4 GB exchange (config 5's R^T, two fp64
-# RHS, world size 1) came back wrong from one all_to_all_single, so larger exchanges go in pieces
-# (tools/a2a_limit.py measures where a single call breaks)
+# largest all-to-all handed to RCCL in one call.  Measured (tools/a2a_limit.py, world size 1,
+# profiles/r6_a2a_limit_probe{1,2}.jsonl): one all_to_all_single of up to 1024 MiB is exact; from
+# 1025 MiB on, for float32 and float64 alike and with or without explicit split sizes, every byte
+# from about the middle of the buffer to its end comes back wrong -- a BYTE-count limit of 2^30
+# in the RCCL self-exchange path (round 5 met it as a 2.4 GB config-5 R^T exchange).  Larger
+# exchanges therefore go in pieces of at most 2^30 bytes (a2a_parts, the same count on every rank)
 A2A_MAX_BYTES = 1 << 30
 
 
