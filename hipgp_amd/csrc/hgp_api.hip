@@ -147,6 +147,9 @@ struct hgp_plan {
   // pack the 2-D K / C^-1 intermediate's real DC and Nyquist columns into one (PassDesc::dcny;
   // HGP_DCNY=0: off)
   bool dcny_pack = true;
+  // RHS chunks of equal size, their count a multiple of the stream count (run_op), so the streams
+  // carry equal work; HGP_BALANCED_CHUNKS=0: the round-5 fixed-size chunks (last one ragged)
+  bool balanced_chunks = true;
   hipStream_t side[3] = {nullptr, nullptr, nullptr};
   hipEvent_t ev_fork = nullptr, ev_join[3] = {nullptr, nullptr, nullptr};
   // hipGraph of a repeated hgp_toeplitz_apply (same op, buffers, RHS count, workspaces, stream):
@@ -477,8 +480,19 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
   const int64_t rows_out = (d == 1) ? 1 : (d == 2 ? g.out[0] : g.out[0] * g.out[1]);
   const int64_t rn_last = (d == 1) ? 1 : (d == 3 && !gen3) ? g.out[0] * ((g.out[1] + 1) / 2) : (rows_out + 1) / 2;
 
-  int64_t chunk = 0;
-  for (int64_t q0 = 0; q0 < nrhs; q0 += Qc, ++chunk) {
+  // chunk j of nch: RHS [j nrhs / nch, (j + 1) nrhs / nch).  Balanced (default): nch = ceil(nrhs /
+  // Qc) rounded up to a multiple of NS and sizes that differ by at most one, so the NS streams get
+  // equal work (fixed Qc-sized chunks left e.g. C3's 200 RHS as 63 + 63 + 63 + 11: 126 RHS on one
+  // stream, 74 on the other; C4's 25 as 8 + 8 + 8 + 1).  Every chunk still fits its Qc workspace slot.
+  int64_t nch = (nrhs + Qc - 1) / Qc;
+  if (P->balanced_chunks && NS > 1 && nch > 1) nch = (nch + NS - 1) / NS * NS;
+  auto chunk_q0 = [&](int64_t j) -> int64_t {
+    return P->balanced_chunks ? j * nrhs / nch : std::min(nrhs, j * Qc);
+  };
+  for (int64_t chunk = 0; chunk < nch; ++chunk) {
+    const int64_t q0 = chunk_q0(chunk);
+    const int qn = (int)(chunk_q0(chunk + 1) - q0);
+    if (qn <= 0) continue;
     const int slot = (int)(chunk % NS);
     hipStream_t st = streams[slot];
     int pass_no = 0;
@@ -487,7 +501,6 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
       if (only_pass >= 0 && only_pass != me) return 0;
       return launch<T>(H, mode, lay, D, lines, st);
     };
-    const int qn = (int)std::min(Qc, nrhs - q0);
     const T* xi = xin + q0 * g.in_M;
     T* yo = yout + q0 * g.out_M;
     const T* dvc = dv ? dv + q0 * g.out_M : nullptr;
@@ -1556,6 +1569,8 @@ int hgp_plan_create(int device, int ndim, const int64_t* m, int dtype, int64_t m
   if (cp) P->chain_pcg = std::atoi(cp) != 0;
   const char* dn = std::getenv("HGP_DCNY");
   if (dn) P->dcny_pack = std::atoi(dn) != 0;
+  const char* bc = std::getenv("HGP_BALANCED_CHUNKS");
+  if (bc) P->balanced_chunks = std::atoi(bc) != 0;
   int rc = 0;
   for (int a = 0; a < d && rc == 0; ++a) {
     if (dtype == HGP_F64) {

@@ -1,7 +1,9 @@
 """Co-residency sweep (GPU box): the batched K op (and others) timed by tools/passtime.py in fresh
 processes under different minimum-LDS requests of the 2-D column conv / row kernels
 (HGP_CONV_LDS_MIN, HGP_ROWF_LDS_MIN, HGP_ROWI_LDS_MIN; hgp_pass_dispatch.hpp), which cap how
-many blocks of one kind a CU takes so that the two RHS streams' passes can share CUs.
+many blocks of one kind a CU takes so that the two RHS streams' passes can share CUs -- or any other
+environment knob of the plan (B: HGP_BALANCED_CHUNKS, S: HGP_STREAMS, W: HGP_WS_MB).  A case
+"phases:C3,C4" runs tools/kn_phases.py (compute_kn set-up / PCG / R^T) instead of passtime.
 
     python tools/lds_sweep.py [--cases "4096x4096/25/K;..."] [--settings "-;C=54000;C=54000,F=80000"]
 Each setting runs as a child process (this process never touches the GPU)."""
@@ -11,7 +13,8 @@ import os
 import subprocess
 import sys
 
-KEYS = {"C": "HGP_CONV_LDS_MIN", "F": "HGP_ROWF_LDS_MIN", "I": "HGP_ROWI_LDS_MIN"}
+KEYS = {"C": "HGP_CONV_LDS_MIN", "F": "HGP_ROWF_LDS_MIN", "I": "HGP_ROWI_LDS_MIN",
+        "B": "HGP_BALANCED_CHUNKS", "S": "HGP_STREAMS", "W": "HGP_WS_MB"}
 
 
 def main():
@@ -28,6 +31,17 @@ def main():
             k, v = kv.split("=")
             env[KEYS[k.strip()]] = v.strip()
         for case in cases:
+            if case.startswith("phases:"):       # compute_kn phase split (tools/kn_phases.py)
+                for rep in range(a.reps):
+                    r = subprocess.run([sys.executable, os.path.join(root, "tools", "kn_phases.py"), "--only",
+                                        case.split(":", 1)[1]], env=env, capture_output=True, text=True, timeout=600)
+                    for line in r.stdout.strip().splitlines():
+                        if line.startswith("{"):
+                            print(json.dumps({"setting": setting, "case": case, "rep": rep, **json.loads(line)}), flush=True)
+                    if r.returncode != 0:
+                        print(json.dumps({"setting": setting, "case": case, "error": r.stderr[-400:]}), flush=True)
+                        sys.exit(r.returncode)
+                continue
             dims, rhs, op = case.split("/")
             dims = dims.replace("x", ",")
             for rep in range(a.reps):
