@@ -25,14 +25,22 @@ def main():
     a = ap.parse_args()
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     cases = [c for c in a.cases.split(";") if c]
-    for setting in a.settings.split(";"):
+    settings = a.settings.split(";")
+
+    def env_of(setting):
         env = dict(os.environ)
         for kv in ([] if setting.strip() in ("", "-") else setting.split(",")):
             k, v = kv.split("=")
             env[KEYS[k.strip()]] = v.strip()
-        for case in cases:
-            if case.startswith("phases:"):       # compute_kn phase split (tools/kn_phases.py)
-                for rep in range(a.reps):
+        return env
+
+    # settings interleaved per case and repetition (A B A B ...), so a drift of the box's clock
+    # over the sweep does not masquerade as a difference between settings
+    for case in cases:
+        for rep in range(a.reps):
+            for setting in settings:
+                env = env_of(setting)
+                if case.startswith("phases:"):       # compute_kn phase split (tools/kn_phases.py)
                     r = subprocess.run([sys.executable, os.path.join(root, "tools", "kn_phases.py"), "--only",
                                         case.split(":", 1)[1]], env=env, capture_output=True, text=True, timeout=600)
                     for line in r.stdout.strip().splitlines():
@@ -41,10 +49,9 @@ def main():
                     if r.returncode != 0:
                         print(json.dumps({"setting": setting, "case": case, "error": r.stderr[-400:]}), flush=True)
                         sys.exit(r.returncode)
-                continue
-            dims, rhs, op = case.split("/")
-            dims = dims.replace("x", ",")
-            for rep in range(a.reps):
+                    continue
+                dims, rhs, op = case.split("/")
+                dims = dims.replace("x", ",")
                 r = subprocess.run([sys.executable, os.path.join(root, "tools", "passtime.py"), "--dims", dims,
                                     "--rhs", rhs, "--op", op], env=env, capture_output=True, text=True, timeout=300)
                 line = r.stdout.strip().splitlines()[-1] if r.stdout.strip() else ""
