@@ -147,9 +147,11 @@ struct hgp_plan {
   // pack the 2-D K / C^-1 intermediate's real DC and Nyquist columns into one (PassDesc::dcny;
   // HGP_DCNY=0: off)
   bool dcny_pack = true;
-  // RHS chunks of equal size, their count a multiple of the stream count (run_op), so the streams
-  // carry equal work; HGP_BALANCED_CHUNKS=0: the round-5 fixed-size chunks (last one ragged)
-  bool balanced_chunks = true;
+  // HGP_BALANCED_CHUNKS=1: RHS chunks of equal size, their count a multiple of the stream count
+  // (run_op), so the streams carry equal work.  Off: measured neutral with the settings
+  // interleaved on one box (C3 PCG(20) 391 vs 390 ms, C4 209 vs 209 ms, C3 / C4 K op +-0.3 %;
+  // profiles/r6i_balanced_chunks_ab_interleaved.jsonl) -- the fixed Qc-sized chunks stay
+  bool balanced_chunks = false;
   hipStream_t side[3] = {nullptr, nullptr, nullptr};
   hipEvent_t ev_fork = nullptr, ev_join[3] = {nullptr, nullptr, nullptr};
   // hipGraph of a repeated hgp_toeplitz_apply (same op, buffers, RHS count, workspaces, stream):
@@ -480,7 +482,7 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
   const int64_t rows_out = (d == 1) ? 1 : (d == 2 ? g.out[0] : g.out[0] * g.out[1]);
   const int64_t rn_last = (d == 1) ? 1 : (d == 3 && !gen3) ? g.out[0] * ((g.out[1] + 1) / 2) : (rows_out + 1) / 2;
 
-  // chunk j of nch: RHS [j nrhs / nch, (j + 1) nrhs / nch).  Balanced (default): nch = ceil(nrhs /
+  // chunk j of nch: RHS [j nrhs / nch, (j + 1) nrhs / nch).  Balanced (HGP_BALANCED_CHUNKS=1): nch = ceil(nrhs /
   // Qc) rounded up to a multiple of NS and sizes that differ by at most one, so the NS streams get
   // equal work (fixed Qc-sized chunks left e.g. C3's 200 RHS as 63 + 63 + 63 + 11: 126 RHS on one
   // stream, 74 on the other; C4's 25 as 8 + 8 + 8 + 1).  Every chunk still fits its Qc workspace slot.
