@@ -7,7 +7,8 @@ dots, the single-rank plan the fused device PCG.  World size 3 check
 rank-block addressing of HGP_SLAB_CONV_A2A with remainder splits.  The slab PCG allocates
 nothing per iteration (torch.cuda.memory_stats: the same number of device allocations for 3
 and 9 iterations) and its break rule gives the single-rank plan's iteration count (fp64; fp32 within a
-few iterations of it, the solution held to the single-rank plan's true residual)."""
+few iterations of it, the solution held to the single-rank plan's true residual).  The exchange
+run one right-hand side at a time (round 6's chunked apply) gives the batched results."""
 import os
 
 import numpy as np
@@ -67,6 +68,12 @@ def _worker(rank, ws, port, case, out):
         xb, itb = S.pcg(S.scatter_rows(v), maxiter=200, tol=tol_brk)
         res["brk"], res["brk_it"], res["brk_tol"] = xb.double().cpu().numpy(), itb, tol_brk
         res["kn"] = S.compute_kn(S.scatter_rows(v), maxiter=10, tol=1e-30).double().cpu().numpy()
+        # the exchange one right-hand side at a time (the chunked apply of round 6: xchg_budget,
+        # one shared arena); every RHS runs its own transforms, so the results do not move
+        S.xchg_budget = 1
+        res["K_chunk1"] = S.apply(_lib.OP_K, S.scatter_rows(v, "m")).double().cpu().numpy()
+        res["RT_chunk1"] = S.apply(_lib.OP_RT, S.scatter_rows(v, "m")).double().cpu().numpy()
+        res["pcg_chunk1"] = S.pcg(S.scatter_rows(v), maxiter=10, tol=1e-30)[0].double().cpu().numpy()
         torch.cuda.synchronize()
         out[rank] = res
     finally:
@@ -109,6 +116,10 @@ def test_slab_ranks_same_device(case, ws):
         assert out[r]["pcg_it"] == 10
         a3, a9 = out[r]["alloc_counts"]
         assert a3 == a9, (r, a3, a9)
+        # one-RHS exchange chunks give the batched results (each RHS is transformed on its own)
+        for k in ("K", "RT", "pcg"):
+            a, b = out[r][k + "_chunk1"], out[r][k]
+            assert float(np.max(np.abs(a - b))) <= (1e-13 if dt == torch.float64 else 1e-6) * float(np.max(np.abs(b))), (r, k)
     xb, itb = P.pcg(v, 200, out[0]["brk_tol"], precond=True, return_iters=True)
     assert itb < 200
     # every rank stops at the same iteration (the all-rank break)
