@@ -80,8 +80,9 @@ def parse():
 
 
 # tools/pmc_kop.sh summaries, newest round first (the kernels of the op change between rounds)
-PMC_FILES = [os.path.join(ROOT, "profiles", f) for f in ("r5_pmc_kop_C2.json", "r4_pmc_kop_C2.json",
-                                                          "r3_pmc_kop_C2.json", "r2_pmc_kop_C2.json")]
+PMC_FILES = [os.path.join(ROOT, "profiles", f) for f in ("r6_pmc_kop_C2.json", "r5_pmc_kop_C2.json",
+                                                          "r4_pmc_kop_C2.json", "r3_pmc_kop_C2.json",
+                                                          "r2_pmc_kop_C2.json")]
 
 
 def pmc_traffic(M, B):
