@@ -29,7 +29,7 @@ def main():
 
     def env_of(setting):
         env = dict(os.environ)
-        for kv in ([] if setting.strip() in ("", "-") else setting.split(",")):
+        for kv in ([] if setting.strip() in ("", "-", "base") else setting.split(",")):
             k, v = kv.split("=")
             env[KEYS[k.strip()]] = v.strip()
         return env
