@@ -49,7 +49,7 @@ def a2a_parts(totals_bytes):
     receive totals of this exchange.  It must be the SAME on every rank -- a rank that issued
     one all-to-all while a peer issued several would hang or pair mismatched pieces -- so it
     comes from the largest total of any rank, which every rank computes from the shared
-    partition (SlabToeplitz._bufs), never from its own byte count alone."""
+    partition (SlabToeplitz._geom), never from its own byte count alone."""
     biggest = max([0] + [int(t) for t in totals_bytes])
     return max(1, -(-biggest // A2A_MAX_BYTES))
 
