@@ -1,5 +1,6 @@
 #!/bin/bash
-# One parametrised GPU-box runner (replaces the per-call tools/gpu_r*_*.sh one-offs).
+# One parametrised GPU-box runner.  It replaces the per-call tools/gpu_r*_*.sh one-offs of rounds
+# 2-5 (the headers of older profiles/ files cite them; they are in the git history before round 6).
 #
 #   TAG=r6a bash tools/gpu.sh STEP [STEP ...]
 #
