@@ -362,9 +362,13 @@ __device__ __forceinline__ void dft(C2<T>* v) {
 // wavefront (position-fast layouts with H/P <= 64 threads per line): a wave's LDS
 // instructions execute in order, so only the compiler must be kept from moving LDS accesses
 // across the exchange -- no s_barrier.  Otherwise a block barrier.
+#ifndef HGP_DIAG_NO_BARRIER
+#define HGP_DIAG_NO_BARRIER 0   // 1: DIAGNOSTIC BUILD ONLY (racy, wrong results): no block barrier at
+                                // the multi-wave exchanges, to time what those barriers cost
+#endif
 template <bool WAVE>
 __device__ __forceinline__ void xsync() {
-  if constexpr (WAVE) {
+  if constexpr (WAVE || HGP_DIAG_NO_BARRIER) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");

@@ -14,7 +14,7 @@ import subprocess
 import sys
 
 KEYS = {"C": "HGP_CONV_LDS_MIN", "F": "HGP_ROWF_LDS_MIN", "I": "HGP_ROWI_LDS_MIN",
-        "B": "HGP_BALANCED_CHUNKS", "S": "HGP_STREAMS", "W": "HGP_WS_MB"}
+        "B": "HGP_BALANCED_CHUNKS", "S": "HGP_STREAMS", "W": "HGP_WS_MB", "L": "HGP_LIB"}
 
 
 def main():
