@@ -123,9 +123,12 @@ def sharded_compute_kn(model, Knm_local, maxiter_cg=10, tol=1e-8, exact_break=No
     kernel_grad = (torch.is_grad_enabled() and bool(model.learn_kernel)
                    and bool(model.log_sig2.requires_grad or model.log_ell.requires_grad))
     if Knm_local.shape[0] == 0 and not (exact_break and kernel_grad):
+        tick("setup")                 # every rank reports the same phases (a caller may barrier in them)
         if exact_break:
             from hipgp_amd.plan import pcg_idle_rank
             pcg_idle_rank(maxiter_cg, Knm_local.device, group)
+        tick("pcg")
+        tick("rt")
         return Knm_local.new_zeros((0, model.Mprime))
     if Kmm is None:
         Kmm = model.toeplitz()
@@ -137,6 +140,7 @@ def sharded_compute_kn(model, Knm_local, maxiter_cg=10, tol=1e-8, exact_break=No
     tick("pcg")
     if Knm_local.shape[0] == 0:
         # keep the solve in the graph (its backward joins the other ranks' all-reduces)
+        tick("rt")
         return Knm_local.new_zeros((0, model.Mprime)) + 0 * d0.sum()
     Kmm.set_batch_shape(d0.shape[:-1])
     kn = Kmm._matmul_by_RT(d0)

@@ -43,3 +43,19 @@ def test_bench_refuses_world_size_mismatch_exit_code():
                        capture_output=True, text=True, timeout=300)
     assert p.returncode == 2, p.stderr
     assert "refusing" in p.stderr and "WORLD_SIZE=3" in p.stderr
+
+
+def test_empty_shard_reports_every_phase():
+    """The bench's config-4 leg barriers inside sharded_compute_kn's phase hook: a rank with no
+    right-hand sides must report the same phases as the others, or the barriers would not pair."""
+    import torch
+    import ziggy.hipgp as hg
+    import ziggy.kernels as zk
+    from hipgp_amd.dist import sharded_compute_kn
+    grids = [torch.linspace(-1, 1, 6), torch.linspace(-1, 1, 5)]
+    mod = hg.MeanFieldToeplitzGP(zk.Matern(nu=1.5, dtype=torch.float32), grids, num_obs=10, learn_kernel=False,
+                                 dtype=torch.float32)
+    seen = []
+    kn = sharded_compute_kn(mod, torch.zeros(0, mod.M), exact_break=False, on_phase=seen.append)
+    assert kn.shape == (0, mod.Mprime)
+    assert seen == ["setup", "pcg", "rt"]
