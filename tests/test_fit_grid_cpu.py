@@ -128,15 +128,15 @@ def _worker(rank, ws, port, case, shard, out):
 def _spawn(ws, case, shard):
     mgr = mp.Manager()
     out = mgr.dict()
-    port = 29500 + os.getpid() % 97 + 3 * ws + (11 if shard == "grid" else 0) + (40 if case == "semi" else 0)
+    port = 29500 + os.getpid() % 97 + 5 * ws + (17 if shard == "grid" else 0) + (40 if case == "semi" else 0)
     mp.spawn(_worker, args=(ws, port, case, shard, out), nprocs=ws, join=True)
     assert len(out) == ws
     return [out[r] for r in range(ws)]
 
 
-def _check(case, shard):
+def _check(case, shard, ws=2):
     (ref, ref_tr), = _spawn(1, case, "rhs")           # the single-process fit (world size 1, seed 1000)
-    res = _spawn(2, case, shard)
+    res = _spawn(ws, case, shard)
     for r, (snaps, tr) in enumerate(res):
         assert snaps.shape == ref.shape
         assert np.array_equal(snaps, res[0][0]), r     # bit-identical parameters on every rank
@@ -148,6 +148,12 @@ def _check(case, shard):
 
 def test_grid_fit_kn_in_slabs_matches_single_process_gloo():
     _check("g19", "grid")
+
+
+def test_grid_fit_three_ranks_uneven_slabs_gloo():
+    """World size 3: uneven axis-0 slabs (8 rows as 3 + 3 + 2, 14 expanded rows as 5 + 5 + 4) on the
+    line-integral 3-D fit, so the Knm sub-grids, kn column ranges and statistic slices are ragged."""
+    _check("semi", "grid", ws=3)
 
 
 def test_integrated_obs_rhs_shard_shared_mc_offset_gloo():

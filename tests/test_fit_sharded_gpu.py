@@ -150,7 +150,7 @@ def _spawn(ws, backend, what):
                                              ("g19_box_rhs", 2, "gloo"), ("g19_box_grid", 2, "gloo"),
                                              ("g19_box_rhs", 1, "nccl"), ("g19_box_grid", 1, "nccl"),
                                              ("semi_rhs", 2, "gloo"), ("semi_grid", 2, "gloo"),
-                                             ("semi_grid", 1, "nccl")])
+                                             ("semi_grid", 3, "gloo"), ("semi_grid", 1, "nccl")])
 def test_sharded_fit_matches_single_process(what, ws, backend):
     """g19_box_grid / semi_grid: shard="grid" on the mean-field family keeps kn in slabs
     (hipgp_amd.slab.SlabFit); semi_*: line-integral observations (config 5's observation type)."""
