@@ -15,6 +15,7 @@
 #   passtime=D/B/OP[,D/B/OP...]   tools/passtime.py --dims D --rhs B --op OP (D: 4096x4096)
 #   profile           rocprofv3 --kernel-trace --stats of the bench (tools/profile.sh)
 #   pmc               PMC HBM bytes of the C2 K matvec (tools/pmc_kop.sh)
+#   profcfg=D/B/OP[,...]  per-kernel stats + PMC bytes of one batched op (tools/prof_cfg.sh)
 #   py=SCRIPT+ARGS    any python script (timeout 600 s; log ${TAG}_py<k>.log for the k-th py step)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -74,6 +75,14 @@ EOF
       cat ${O}_passtime.txt ;;
     profile)
       bash tools/profile.sh ${TAG} || fail "$step" $? ;;
+    profcfg)
+      # per-kernel stats + PMC HBM bytes of one batched operator: profcfg=4096x4096/25/RT[,...]
+      for spec in ${arg//,/ }; do
+        IFS=/ read -r dims rhs op <<< "$spec"
+        SHAPE=${dims//x/,} RHS=$rhs OP=$op TAG=${TAG}_${dims}_${op} bash tools/prof_cfg.sh > ${O}_profcfg_${dims}_${op}.txt 2>&1 \
+          || fail "$step ($spec)" $? ${O}_profcfg_${dims}_${op}.txt
+        tail -25 ${O}_profcfg_${dims}_${op}.txt
+      done ;;
     pmc)
       bash tools/pmc_kop.sh > ${O}_pmc_kop.log 2>&1 || fail "$step" $? ${O}_pmc_kop.log
       grep traffic_bytes_per_op gpurun_out/pmc_kop/pmc_kop_C2.json ;;
