@@ -147,6 +147,11 @@ struct hgp_plan {
   // pack the 2-D K / C^-1 intermediate's real DC and Nyquist columns into one (PassDesc::dcny;
   // HGP_DCNY=0: off)
   bool dcny_pack = true;
+  // the fp32 1024-point K / C^-1 column conv with two lines per wave, radix-32 stages (LAY_CONTIG2,
+  // HGP_CONV_P32=1): one LDS exchange per transform instead of two, but 2 waves per SIMD instead of 4
+  // (the LDS images bound a CU to 16 lines either way) -- measured slower, C2 column pass 0.149 ->
+  // 0.171 ms (profiles/r6r_conv_p32_ab.txt); kept as an opt-in for that measurement
+  bool conv_p32 = false;
   // HGP_BALANCED_CHUNKS=1: RHS chunks of equal size, their count a multiple of the stream count
   // (run_op), so the streams carry equal work.  Off: measured neutral with the settings
   // interleaved on one box (C3 PCG(20) 391 vs 390 ms, C4 209 vs 209 ms, C3 / C4 K op +-0.3 %;
@@ -593,7 +598,13 @@ int run_op(hgp_plan* P, int op, const void* x, void* y, int64_t nrhs, const void
         b_lay = use_grp ? glay : quad ? LAY_CONTIG_Q : LAY_CONTIG_G;
         b_lines = (int64_t)qn * ((H1 + G2) / G2) * G2;
       } else {
-        b_lay = LAY_CONTIG;
+        // fp32 1024-point lines of exactly H rows in and out (no zero padding, no crop): two lines
+        // per wave, radix-32 stages (LAY_CONTIG2); its wave-shared buffer resource needs the chunk's
+        // intermediate below 2 GiB
+        const bool two = std::is_same<T, float>::value && P->conv_p32 && conv_mode == PASS_CONV &&
+                         g.L[0] == 2048 && g.in[0] == 1024 && g.out[0] == 1024 &&
+                         (int64_t)qn * B1 * (int64_t)cs < ((int64_t)1 << 31) - ((int64_t)1 << 20);
+        b_lay = two ? LAY_CONTIG2 : LAY_CONTIG;
         b_lines = (int64_t)qn * (dcny > 0 ? Bd.Rn - 1 : Bd.Rn);
       }
       HGP_TRY(run((int)(g.L[0] / 2), conv_mode, b_lay, Bd, b_lines));
@@ -1571,6 +1582,8 @@ int hgp_plan_create(int device, int ndim, const int64_t* m, int dtype, int64_t m
   if (cp) P->chain_pcg = std::atoi(cp) != 0;
   const char* dn = std::getenv("HGP_DCNY");
   if (dn) P->dcny_pack = std::atoi(dn) != 0;
+  const char* c32 = std::getenv("HGP_CONV_P32");
+  if (c32) P->conv_p32 = std::atoi(c32) != 0;
   const char* bc = std::getenv("HGP_BALANCED_CHUNKS");
   if (bc) P->balanced_chunks = std::atoi(bc) != 0;
   int rc = 0;

@@ -215,9 +215,15 @@ template <typename T, int H> struct PFor {
 // radix-4 / -2 stages first and the factor 3 in the LAST stage (radix 3 * min(4, H / 3), which
 // divides P = 12): every non-last stage's span NS is then a power of two dividing TT, as the
 // exchange index math of fft_xchg needs.
+// P = 32 (the 1024-point column lines of two lines per wave, hgp_pass.hpp HGP_P_CONV_1024): radix-32
+// stages (1024 = 32 x 32, one LDS exchange per transform instead of two); 0: two radix-16 DFTs per
+// stage
+#ifndef HGP_RADIX32
+#define HGP_RADIX32 1
+#endif
 template <int H, int P> struct Stages {
   static constexpr bool TRI = !is_pow2(H);
-  static constexpr int RMAX = P < 16 ? P : 16;   // in-register DFTs up to 16 points (P = 32: two per stage)
+  static constexpr int RMAX = (P >= 32 && HGP_RADIX32) ? 32 : P < 16 ? P : 16;   // in-register DFT size
   // tri lengths: radix-4 stages with P = 12 (three butterflies a thread), radix-8 with P = 24
   static constexpr int RTRI = P % 8 == 0 ? 8 : 4;
   static constexpr int last_tri() { return 3 * (H / 3 >= 4 ? 4 : H / 3); }
@@ -285,7 +291,38 @@ __device__ __forceinline__ C2<T> rot12(C2<T> v, int Q) {
   }
 }
 
-// In-register DFT of size R (natural order in and out), R in {1,2,3,4,6,8,12,16}.
+// multiply by exp(DIR * 2*pi*i*Q/32) (the radix-32 DFT's inner twiddles); Q a compile-time
+// constant.  Even Q: rot16.
+template <typename T, int DIR>
+__device__ __forceinline__ C2<T> rot32(C2<T> v, int Q) {
+  Q &= 31;
+  if ((Q & 1) == 0) return rot16<T, DIR>(v, Q >> 1);
+  // cos / sin of 2 pi j / 32, j = 1, 3, 5, 7
+  const T c1 = (T)0.98078528040323044913, s1 = (T)0.19509032201612826785;
+  const T c3 = (T)0.83146961230254523708, s3 = (T)0.55557023301960222474;
+  if (DIR > 0) Q = (32 - Q) & 31;           // inverse: exp(+i th) = forward rotation by -Q
+  // forward: multiply by (cos th, -sin th), th = 2 pi Q / 32; Q = 8 m + j with j odd
+  switch (Q) {
+    case 1: return cmulk<T>(v, c1, -s1);
+    case 3: return cmulk<T>(v, c3, -s3);
+    case 5: return cmulk<T>(v, s3, -c3);
+    case 7: return cmulk<T>(v, s1, -c1);
+    case 9: return cmulk<T>(v, -s1, -c1);
+    case 11: return cmulk<T>(v, -s3, -c3);
+    case 13: return cmulk<T>(v, -c3, -s3);
+    case 15: return cmulk<T>(v, -c1, -s1);
+    case 17: return cmulk<T>(v, -c1, s1);
+    case 19: return cmulk<T>(v, -c3, s3);
+    case 21: return cmulk<T>(v, -s3, c3);
+    case 23: return cmulk<T>(v, -s1, c1);
+    case 25: return cmulk<T>(v, s1, c1);
+    case 27: return cmulk<T>(v, s3, c3);
+    case 29: return cmulk<T>(v, c3, s3);
+    default: return cmulk<T>(v, c1, s1);    // 31
+  }
+}
+
+// In-register DFT of size R (natural order in and out), R in {1,2,3,4,6,8,12,16,32}.
 template <typename T, int R, int DIR>
 __device__ __forceinline__ void dft(C2<T>* v) {
   if constexpr (R == 1) {
@@ -344,7 +381,10 @@ __device__ __forceinline__ void dft(C2<T>* v) {
       for (int n1 = 0; n1 < R1; ++n1) a[n1] = v[R2 * n1 + n2];
       dft<T, R1, DIR>(a);
 #pragma unroll
-      for (int k1 = 0; k1 < R1; ++k1) y[n2 * R1 + k1] = rot16<T, DIR>(a[k1], (n2 * k1 * (16 / R)) & 15);
+      for (int k1 = 0; k1 < R1; ++k1) {
+        if constexpr (R == 32) y[n2 * R1 + k1] = rot32<T, DIR>(a[k1], n2 * k1);
+        else y[n2 * R1 + k1] = rot16<T, DIR>(a[k1], (n2 * k1 * (16 / R)) & 15);
+      }
     }
 #pragma unroll
     for (int k1 = 0; k1 < R1; ++k1) {
@@ -431,8 +471,31 @@ __device__ __forceinline__ void stage_twiddle(C2<T>* a, int kk, const C2<T>* __r
 #ifdef HGP_DIAG_NO_STAGE_TW
   return;   // DIAGNOSTIC BUILD ONLY (wrong results): tools/isa_mix.py counts what the stage twiddles cost
 #endif
-  const C2<T> w = tw_at<T, H>(tab, (2 * (H / (NS * R))) * kk);
-  if constexpr (HGP_TW_CHAIN) {
+  const int q1 = (2 * (H / (NS * R))) * kk;   // w = W_L^q1; w^r = W_L^{q1 r}, q1 r < L
+  const C2<T> w = tw_at<T, H>(tab, q1);
+  if constexpr (R > 16) {
+    // radix 32: w^1..w^7 by binary powering, w^{8m} from the table, w^{8m + j} = w^{8m} w^j (at
+    // most 4 products deep, ~20 live VGPRs instead of 62 for all 31 powers)
+    C2<T> wp[8];
+    wp[1] = w;
+#pragma unroll
+    for (int r = 2; r < 8; ++r) {
+      const int hi = (r & (r - 1)) == 0 ? r / 2 : (1 << (31 - __builtin_clz(r)));
+      wp[r] = cmul<T>(wp[hi], wp[r - hi]);
+    }
+#pragma unroll
+    for (int r = 1; r < 8; ++r) a[r] = (DIR < 0) ? cmul<T>(a[r], wp[r]) : cmulc<T>(a[r], wp[r]);
+#pragma unroll
+    for (int m = 1; m < R / 8; ++m) {
+      const C2<T> w8 = tw_at<T, H>(tab, q1 * 8 * m);
+      a[8 * m] = (DIR < 0) ? cmul<T>(a[8 * m], w8) : cmulc<T>(a[8 * m], w8);
+#pragma unroll
+      for (int j = 1; j < 8; ++j) {
+        const C2<T> wr = cmul<T>(w8, wp[j]);
+        a[8 * m + j] = (DIR < 0) ? cmul<T>(a[8 * m + j], wr) : cmulc<T>(a[8 * m + j], wr);
+      }
+    }
+  } else if constexpr (HGP_TW_CHAIN) {
     C2<T> wr = w;
 #pragma unroll
     for (int r = 1; r < R; ++r) {

@@ -51,6 +51,12 @@
 //                 comes from one block at one time (no partially written 32-B sectors, which the
 //                 plain G = 4 order with one column per block left to four blocks, C4 K op conv
 //                 writes 1.54x their bytes, profiles/r4_C4K_kernel_bytes_final.txt).
+//   LAY_CONTIG2 : LAY_CONTIG for the fp32 1024-point K / C^-1 column conv (PASS_CONV) with 32 points
+//                 per thread: two lines per wave (TT = 32), radix-32 stages, so one LDS exchange per
+//                 transform instead of two.  The wave's two lines share one raw-buffer resource based
+//                 at the smaller of their offsets (32-bit lane offsets: the host picks this layout only
+//                 when the chunk's intermediate is < 2 GiB, and only for in_len = out_len = H -- no zero
+//                 padding and no crop, which the per-line resource ranges of LAY_CONTIG provide).
 //   LAY_GRP2 / LAY_GRP4: the grouped-column intermediate as LAY_CONTIG_G, but a block holds the
 //                 G = 2 / 4 columns of one group of one RHS with threads column-fast (the strided
 //                 mapping, C = G): every load / store instruction of a wave covers one contiguous
@@ -144,7 +150,7 @@ namespace hgp {
 
 enum { PASS_FWD = 0, PASS_INV = 1, PASS_CONV = 2, PASS_CONVC = 3 };   // CONV: real spectrum, CONVC: complex
 enum { LAY_STRIDED = 0, LAY_CONTIG = 1, LAY_RP = 2, LAY_R1 = 3, LAY_CONTIG_G = 4, LAY_SEG_C = 5, LAY_SEG_S = 6,
-       LAY_GRP2 = 7, LAY_GRP4 = 8, LAY_CONTIG_Q = 9 };
+       LAY_GRP2 = 7, LAY_GRP4 = 8, LAY_CONTIG_Q = 9, LAY_CONTIG2 = 10 };
 // element offset of position p within its line in the quad order (LAY_CONTIG_Q, wg_off<4>)
 __host__ __device__ constexpr int quad_pos(int p) { return ((p >> 2) << 4) + ((p & 3) << 1); }
 // columns per block of the interleaved grouped layouts (0: not one)
@@ -241,10 +247,16 @@ constexpr int CG_LOADS = 8;
 #ifndef HGP_MINW_CONTIG_P8
 #define HGP_MINW_CONTIG_P8 6
 #endif
+// 32 points per thread: two lines per wave (TT = 32), radix-32 stages; 16 lines per CU as at P = 16
+// (the LDS images bound it), in 2 waves per SIMD of up to 256 VGPRs
+#ifndef HGP_MINW_CONTIG_P32
+#define HGP_MINW_CONTIG_P32 2
+#endif
 template <typename T, int H, int LAY> struct PassP {
-  static constexpr bool CONTIG_LINE = LAY == LAY_CONTIG || LAY == LAY_CONTIG_G || LAY == LAY_CONTIG_Q;
+  static constexpr bool CONTIG_LINE = LAY == LAY_CONTIG || LAY == LAY_CONTIG_G || LAY == LAY_CONTIG_Q || LAY == LAY_CONTIG2;
   static constexpr bool F32 = std::is_same<T, float>::value;
-  static constexpr int v = (F32 && is_tri(H) && H >= HGP_TRI_P_CONV_MIN && CONTIG_LINE) ? HGP_TRI_P_CONV
+  static constexpr int v = LAY == LAY_CONTIG2 ? 32
+                         : (F32 && is_tri(H) && H >= HGP_TRI_P_CONV_MIN && CONTIG_LINE) ? HGP_TRI_P_CONV
                          : (F32 && H == 1024 && CONTIG_LINE && HGP_P_CONV_1024 > 0) ? HGP_P_CONV_1024
                                                                                     : PFor<T, H>::v;
 };
@@ -261,7 +273,8 @@ template <typename T, int H, int LAY> struct PassCfg {
     while (c > 1 && (c * TT > 1024 || lds_bytes_for(c) > LDS_CAP)) c >>= 1;
     return c;
   }
-  static constexpr int ROWT = (LAY == LAY_CONTIG || LAY == LAY_CONTIG_G || LAY == LAY_CONTIG_Q || LAY == LAY_SEG_C)
+  static constexpr int ROWT = (LAY == LAY_CONTIG || LAY == LAY_CONTIG_G || LAY == LAY_CONTIG_Q || LAY == LAY_SEG_C ||
+                               LAY == LAY_CONTIG2)
                                   ? (TT >= 128 ? HGP_CONTIG_THREADS_LONG : H <= 512 ? HGP_CONTIG_THREADS_SHORT : HGP_CONTIG_THREADS)
                                   : HGP_ROW_THREADS;
   static constexpr int c_contig() {
@@ -292,6 +305,7 @@ template <typename T, int H, int LAY> struct PassCfg {
   static constexpr int MINW_AUTO = MINW_LDS < 1 ? 1 : (MINW_LDS > 4 ? 4 : MINW_LDS);
   // (3 waves per SIMD only for lines of 4 waves: 3 whole blocks per CU)
   static constexpr int MINW_CL = (P == 24) ? 3 : (H == 1024 && P == 8) ? HGP_MINW_CONTIG_P8
+                                 : (H == 1024 && P == 32) ? HGP_MINW_CONTIG_P32
                                  : (!is_pow2(H) && TT >= 256) ? HGP_MINW_CONTIG_TRI
                                  : (H >= 4096 && TT == 256) ? HGP_MINW_CONTIG_4096
                                  : H >= 2048 ? HGP_MINW_CONTIG_LONG : H <= 512 ? HGP_MINW_CONTIG_SHORT : HGP_MINW_CONTIG;
@@ -302,7 +316,7 @@ template <typename T, int H, int LAY> struct PassCfg {
   static constexpr int MINW_SET = lay_grp(LAY) ? (MINW_CL > MINW_BLK ? MINW_CL : MINW_BLK)
                                  : lay_smap(LAY) ? (TT >= 16 ? HGP_MINW_STRIDED : HGP_MINW_STRIDED_SMALL)
                                  : LAY == LAY_CONTIG_Q ? (MINW_Q > MINW_BLK ? MINW_Q : MINW_BLK)
-                                 : (LAY == LAY_CONTIG || LAY == LAY_CONTIG_G || LAY == LAY_SEG_C) ? MINW_CL
+                                 : (LAY == LAY_CONTIG || LAY == LAY_CONTIG_G || LAY == LAY_SEG_C || LAY == LAY_CONTIG2) ? MINW_CL
                                                                                                   : HGP_MINW_ROW;
   static constexpr int MINW = MINW_SET > 0 ? MINW_SET : MINW_AUTO;
 };
@@ -437,7 +451,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
     if (!valid) { q = 0; r = 0; }
     if constexpr (LAY == LAY_CONTIG_Q) gbase = (int64_t)(r >> 2) * d.in.r_stride * 4 + ((r >> 1) & 1) * 8 + (r & 1);
     else gbase = (int64_t)(r / G) * d.in.r_stride * G + (r % G);
-  } else if constexpr (LAY == LAY_CONTIG || LAY == LAY_SEG_C) {
+  } else if constexpr (LAY == LAY_CONTIG || LAY == LAY_SEG_C || LAY == LAY_CONTIG2) {
     // RHS-fastest: the C lines of a block are the same column r of C right-hand sides, so
     // they share one spectrum line; the XCD remap keeps the blocks of one column (all its
     // RHS) on one XCD, so the line is fetched into that L2 once.  Packed DC / Nyquist
@@ -593,7 +607,8 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
 #endif
   constexpr bool QUAD = LAY == LAY_CONTIG_Q;
   constexpr bool CONTIG = (LAY == LAY_CONTIG || LAY == LAY_CONTIG_G || QUAD);
-  constexpr bool BUF = (std::is_same<T, float>::value || HGP_BUF_F64) && CONTIG && (TT % 64 == 0);
+  constexpr bool TWO = LAY == LAY_CONTIG2;   // two lines per wave on one shared resource
+  constexpr bool BUF = (std::is_same<T, float>::value || HGP_BUF_F64) && ((CONTIG && (TT % 64 == 0)) || TWO);
   // element stride of a line's positions: 1, or G in the grouped layout; the range then ends
   // one element past the line's last valid position ((len - 1) G + 1 elements).  Quad order:
   // the offset of p = t + x (x a multiple of 4: TT k, H) splits into the lane's quad_pos(t) and
@@ -604,8 +619,29 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
     if (QUAD) return ((uint32_t)quad_pos(len - 1) + 1u) * (uint32_t)sizeof(C2<T>);
     return ((uint32_t)(len - 1) * (uint32_t)st + 1u) * (uint32_t)sizeof(C2<T>);
   };
-  const BufRsrc rin = buf_rsrc(BUF ? (const void*)in_c : nullptr, (BUF && valid && d.in.len > 0) ? range_b(d.in.len, ips) : 0u);
-  const BufRsrc rout = buf_rsrc(BUF ? (const void*)out_c : nullptr, (BUF && valid && d.out.len > 0) ? range_b(d.out.len, ops) : 0u);
+  // LAY_CONTIG2: the resources start at the smaller of the wave's two line offsets (lanes 0 and
+  // 32), each lane adds its line's byte distance from there; invalid lines get an offset past the
+  // 2^31 - 1 byte range (their loads return 0, their stores are dropped; the host keeps the chunk's
+  // views below 2 GiB, so a valid offset plus the per-position step never reaches it)
+  int64_t two_ib = 0, two_ob = 0;
+  uint32_t lane_bi = lane_b, lane_bo = lane_b;
+  if constexpr (TWO) {
+    const int64_t io = (int64_t)q * d.in.q_stride + (int64_t)r * d.in.r_stride;
+    const int64_t oo = (int64_t)q * d.out.q_stride + (int64_t)r * d.out.r_stride;
+    auto rl = [](int64_t v, int lane) -> int64_t {
+      const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, lane);
+      const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), lane);
+      return (int64_t)(((uint64_t)hi << 32) | lo);
+    };
+    two_ib = rl(io, 0) < rl(io, 32) ? rl(io, 0) : rl(io, 32);
+    two_ob = rl(oo, 0) < rl(oo, 32) ? rl(oo, 0) : rl(oo, 32);
+    lane_bi = valid ? (uint32_t)((io - two_ib) * (int64_t)sizeof(C2<T>)) + lane_b : 0x80000000u;
+    lane_bo = valid ? (uint32_t)((oo - two_ob) * (int64_t)sizeof(C2<T>)) + lane_b : 0x80000000u;
+  }
+  const BufRsrc rin = TWO ? buf_rsrc(reinterpret_cast<const C2<T>*>(d.in.ptr) + two_ib, 0x7fffffffu)
+                          : buf_rsrc(BUF ? (const void*)in_c : nullptr, (BUF && valid && d.in.len > 0) ? range_b(d.in.len, ips) : 0u);
+  const BufRsrc rout = TWO ? buf_rsrc(reinterpret_cast<const C2<T>*>(d.out.ptr) + two_ob, 0x7fffffffu)
+                           : buf_rsrc(BUF ? (const void*)out_c : nullptr, (BUF && valid && d.out.len > 0) ? range_b(d.out.len, ops) : 0u);
   if constexpr (MODE == PASS_FWD || CONV) {
     const int in_len = d.in.len;
     const int lim = in_len - 1;
@@ -617,14 +653,14 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
         const int p = t + TT * k;
         C2<T> a;
         if constexpr (BUF) {
-          a = buf_ld_c2<T>(rin, lane_b, (uint32_t)(TT * k) * es);
+          a = buf_ld_c2<T>(rin, lane_bi, (uint32_t)(TT * k) * es);
         } else {
           a = load_in(p < in_len ? p : lim);
           if (p >= in_len) a = mk<T>(0, 0);
         }
         C2<T> c = mk<T>(0, 0);
         if constexpr (FOLD) {       // beyond in_len the buffer range returns 0
-          if constexpr (BUF) c = buf_ld_c2<T>(rin, lane_b, (uint32_t)(TT * k + H) * es);
+          if constexpr (BUF) c = buf_ld_c2<T>(rin, lane_bi, (uint32_t)(TT * k + H) * es);
           else c = load_hi(p);
         }
         va[k] = cadd<T>(a, c);
@@ -684,8 +720,9 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
       // sum S0 |A|^2 + S1 |B|^2 (both columns have Hermitian weight 1).  The spectra are read per
       // position here, so this rarely taken branch (one line in H1) holds no more registers than
       // the common one.
-      const bool packed = HGP_DCNY_CONV && (LAY == LAY_CONTIG) && Cfg::WAVE && d.dcny > 0 && r == 0 && valid;
-      if constexpr (HGP_DCNY_CONV && (LAY == LAY_CONTIG) && Cfg::WAVE) {
+      constexpr bool PLAIN = LAY == LAY_CONTIG || LAY == LAY_CONTIG2;
+      const bool packed = HGP_DCNY_CONV && PLAIN && Cfg::WAVE && d.dcny > 0 && r == 0 && valid;
+      if constexpr (HGP_DCNY_CONV && PLAIN && Cfg::WAVE) {
         if (packed) {
           const T* sn = sb + (int64_t)d.dcny * d.spec_r;      // the Nyquist column's spectrum
 #pragma unroll
@@ -716,11 +753,13 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
         // them); L2-resident: every line of a block shares it (RHS-fastest map, XCD-grouped)
         T sre1[P];
         if constexpr (BUF) {
-          const BufRsrc rspec = buf_rsrc(sb, 0x7fffffffu);
+          // (LAY_CONTIG2: the two lines' spectrum columns differ; base at the spectrum, lane offset r)
+          const BufRsrc rspec = buf_rsrc(TWO ? reinterpret_cast<const T*>(d.spec) : sb, 0x7fffffffu);
+          const uint32_t sso = TWO ? (uint32_t)((int64_t)r * d.spec_r + so) : (uint32_t)so;
 #pragma unroll
           for (int k = 0; k < P; ++k) {
-            sre[k] = buf_ld<T>(rspec, (uint32_t)so * (uint32_t)sizeof(T), (uint32_t)(TT * k * sp) * (uint32_t)sizeof(T));
-            sre1[k] = buf_ld<T>(rspec, (uint32_t)so * (uint32_t)sizeof(T), (uint32_t)((H + TT * k) * sp) * (uint32_t)sizeof(T));
+            sre[k] = buf_ld<T>(rspec, sso * (uint32_t)sizeof(T), (uint32_t)(TT * k * sp) * (uint32_t)sizeof(T));
+            sre1[k] = buf_ld<T>(rspec, sso * (uint32_t)sizeof(T), (uint32_t)((H + TT * k) * sp) * (uint32_t)sizeof(T));
           }
         } else {
 #pragma unroll
@@ -804,7 +843,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
               }
             }
           } else if constexpr (BUF) {
-            buf_st_c2<T>(y, rout, lane_b, (uint32_t)(pp - t) * es);
+            buf_st_c2<T>(y, rout, lane_bo, (uint32_t)(pp - t) * es);
           } else {
             out_c[out_at(pp)] = y;
           }

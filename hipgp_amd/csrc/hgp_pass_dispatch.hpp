@@ -69,6 +69,8 @@ static hipError_t launch_h(int mode, int lay, const PassDesc& d, int64_t nblocks
     if (lay == LAY_STRIDED) return launch_one<T, H, PASS_CONV, LAY_STRIDED>(d, nblocks, s);
     if (lay == LAY_CONTIG) return launch_one<T, H, PASS_CONV, LAY_CONTIG>(d, nblocks, s);
     if (lay == LAY_R1) return launch_one<T, H, PASS_CONV, LAY_R1>(d, nblocks, s);
+    if constexpr (std::is_same<T, float>::value && H == 1024)   // two lines per wave (hgp_pass.hpp)
+      if (lay == LAY_CONTIG2) return launch_one<T, H, PASS_CONV, LAY_CONTIG2>(d, nblocks, s);
     // the grouped-column intermediate of long fp32 rows (hgp_rows.hpp RowTCfg::G); any axis-0 H
     if constexpr (std::is_same<T, float>::value) {
       if (lay == LAY_CONTIG_G) return launch_one<T, H, PASS_CONV, LAY_CONTIG_G>(d, nblocks, s);
@@ -103,6 +105,10 @@ static PassGeom geom_h(int lay) {
   if (lay == LAY_STRIDED) return geom_one<T, H, LAY_STRIDED>();
   if (lay == LAY_SEG_S) return geom_one<T, H, LAY_SEG_S>();
   if (lay == LAY_CONTIG) return geom_one<T, H, LAY_CONTIG>();
+  if (lay == LAY_CONTIG2) {
+    if constexpr (std::is_same<T, float>::value && H == 1024) return geom_one<T, H, LAY_CONTIG2>();
+    return PassGeom{0, 0, 0};
+  }
   if (lay == LAY_CONTIG_G) return geom_one<T, H, LAY_CONTIG_G>();
   if (lay == LAY_CONTIG_Q) return geom_one<T, H, LAY_CONTIG_Q>();
   if (lay == LAY_SEG_C) return geom_one<T, H, LAY_SEG_C>();

@@ -458,3 +458,40 @@ def test_dcny_packed_columns(dims, dt, tol):
     xa = plans["1"].pcg(v, 10, 1e-30, precond=True).double()
     xb = plans["0"].pcg(v, 10, 1e-30, precond=True).double()
     assert float((xa - xb).norm() / xb.norm()) < (1e-9 if dt == torch.float64 else 1e-4)
+
+
+@pytest.mark.parametrize("nrhs", [1, 8, 13], ids=["q1", "q8", "q13"])
+def test_conv_two_lines_per_wave_opt_in(nrhs):
+    """Round 6: the opt-in fp32 1024-point column conv with two lines per wave and radix-32 stages
+    (HGP_CONV_P32=1, LAY_CONTIG2: one wave-shared buffer resource for two lines; measured slower
+    and kept off by default, profiles/r6r_conv_p32_ab.txt).  C2's grid (in_len = out_len = H):
+    K and C^-1 against the default layout to rounding and K against the oracle, over odd RHS counts
+    (a wave's two lines then straddle RHS and column boundaries, and the last block holds invalid
+    lines); the fused PCG (spectral dots, packed DC / Nyquist line) against the default plan."""
+    from hipgp_amd import _lib
+    from hipgp_amd.plan import ToeplitzPlan
+    dims, dt = (1024, 1024), torch.float32
+    grids = [np.linspace(-1, 1, m) for m in dims]
+    col_np = zo.toeplitz_column(grids, lambda x, y: zo.kernel_eval("matern", x, y, (1., .05), nu=1.5), 1e-2)
+    col = torch.tensor(col_np, device=DEV, dtype=dt)
+    plans = {}
+    for knob in ("1", "0"):
+        os.environ["HGP_CONV_P32"] = knob
+        try:
+            P = ToeplitzPlan(dims, dt, DEV)
+        finally:
+            del os.environ["HGP_CONV_P32"]
+        P.set_column(col)
+        plans[knob] = P
+    g = torch.Generator(device=DEV).manual_seed(17 + nrhs)
+    v = torch.randn(nrhs, int(np.prod(dims)), device=DEV, generator=g, dtype=torch.float64).to(dt)
+    for op in (_lib.OP_K, _lib.OP_CINV):
+        a, b = plans["1"].apply(op, v).double(), plans["0"].apply(op, v).double()
+        err = float((a - b).abs().max() / b.abs().max())
+        assert err < 2e-6, (op, err)
+    ref = zo.ToeplitzOracle(col_np, dims).matmul_K(v[:2].double().cpu().numpy())
+    got = plans["1"].apply(_lib.OP_K, v[:2]).double().cpu().numpy()
+    assert float(np.max(np.abs(got - ref)) / np.max(np.abs(ref))) < 1e-5
+    xa = plans["1"].pcg(v, 10, 1e-30, precond=True).double()
+    xb = plans["0"].pcg(v, 10, 1e-30, precond=True).double()
+    assert float((xa - xb).norm() / xb.norm()) < 1e-4
