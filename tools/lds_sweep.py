@@ -2,7 +2,7 @@
 processes under different minimum-LDS requests of the 2-D column conv / row kernels
 (HGP_CONV_LDS_MIN, HGP_ROWF_LDS_MIN, HGP_ROWI_LDS_MIN; hgp_pass_dispatch.hpp), which cap how
 many blocks of one kind a CU takes so that the two RHS streams' passes can share CUs -- or any other
-environment knob of the plan (B: HGP_BALANCED_CHUNKS, S: HGP_STREAMS, W: HGP_WS_MB, P: HGP_CONV_P32).  A case
+environment knob of the plan (B: HGP_BALANCED_CHUNKS, S: HGP_STREAMS, W: HGP_WS_MB, P: HGP_CONV_P32, R: HGP_LR).  A case
 "phases:C3,C4" runs tools/kn_phases.py (compute_kn set-up / PCG / R^T) instead of passtime.
 
     python tools/lds_sweep.py [--cases "4096x4096/25/K;..."] [--settings "-;C=54000;C=54000,F=80000"]
@@ -15,7 +15,7 @@ import sys
 
 KEYS = {"C": "HGP_CONV_LDS_MIN", "F": "HGP_ROWF_LDS_MIN", "I": "HGP_ROWI_LDS_MIN",
         "B": "HGP_BALANCED_CHUNKS", "S": "HGP_STREAMS", "W": "HGP_WS_MB", "L": "HGP_LIB",
-        "P": "HGP_CONV_P32"}
+        "P": "HGP_CONV_P32", "R": "HGP_LR"}
 
 
 def main():
