@@ -658,13 +658,18 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
           a = load_in(p < in_len ? p : lim);
           if (p >= in_len) a = mk<T>(0, 0);
         }
-        C2<T> c = mk<T>(0, 0);
         if constexpr (FOLD) {       // beyond in_len the buffer range returns 0
+          C2<T> c;
           if constexpr (BUF) c = buf_ld_c2<T>(rin, lane_bi, (uint32_t)(TT * k + H) * es);
           else c = load_hi(p);
+          va[k] = cadd<T>(a, c);
+          vb[k] = cmul<T>(csub<T>(a, c), tw_at<T, H>(tab, p));
+        } else {
+          // no second half: x[p] itself (an explicit "+ 0" is not folded -- it maps -0 to +0 --
+          // and cost one packed add per point)
+          va[k] = a;
+          vb[k] = cmul<T>(a, tw_at<T, H>(tab, p));
         }
-        va[k] = cadd<T>(a, c);
-        vb[k] = cmul<T>(csub<T>(a, c), tw_at<T, H>(tab, p));
       }
     };
     if constexpr (CAN_FOLD) {
