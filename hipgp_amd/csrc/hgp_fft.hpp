@@ -435,30 +435,13 @@ template <typename T, int H> struct TwTab {
   static constexpr int BYTES = ENTRIES * (int)sizeof(C2<T>);
 };
 
-// Stage-1 power table (PT, opt-in per kernel): the radix-16 stage that follows the first radix-16
-// stage (NS = 16) multiplies a thread's 16 values by w^r, w = W_H^{kk H / 256}, kk = its position
-// mod 16 -- the same 15 powers in all four transforms of a line.  PT holds them for every kk,
-// PT[kk * PT_PITCH + r - 1] = W_L^{2 (H / 256) kk r} (r = 1..15), right after the W_L table: 8 LDS
-// reads of 16 B per use instead of 14 products, each power one rounding from the exact value
-// (pitch 18: the 16 rows' 16-byte reads fall on distinct banks).
-constexpr int PT_PITCH = 18;
-constexpr int PT_ENTRIES = 16 * PT_PITCH;
-
-// copy the table layout above from the global W_L^q array (all threads of the block); PT: the
-// power table after it (twg holds the whole circle q < L)
-template <typename T, int H, bool PT = false>
+// copy the table layout above from the global W_L^q array (all threads of the block)
+template <typename T, int H>
 __device__ __forceinline__ void stage_tw(C2<T>* tab, const C2<T>* __restrict__ twg, int tid, int nthreads) {
   using TW = TwTab<T, H>;
   for (int q = tid; q < TW::ENTRIES; q += nthreads) {
     if constexpr (TW::TWO) tab[q] = q < TW::S ? twg[q] : twg[(q - TW::S) * TW::S];
     else tab[q] = twg[q];
-  }
-  if constexpr (PT) {
-    static_assert(is_pow2(H) && H >= 256, "power table: radix-16 second stage");
-    for (int e = tid; e < 16 * 15; e += nthreads) {
-      const int kk = e / 15, r = e - kk * 15 + 1;
-      tab[TW::ENTRIES + kk * PT_PITCH + r - 1] = twg[(2 * (H / 256) * kk * r) % (2 * H)];
-    }
   }
 }
 
@@ -483,17 +466,11 @@ __device__ __forceinline__ C2<T> tw_at(const C2<T>* __restrict__ tab, int q) {
 #ifndef HGP_TW_CHAIN
 #define HGP_TW_CHAIN 0
 #endif
-template <typename T, int H, int R, int DIR, int NS, bool PT = false>
+template <typename T, int H, int R, int DIR, int NS>
 __device__ __forceinline__ void stage_twiddle(C2<T>* a, int kk, const C2<T>* __restrict__ tab) {
 #ifdef HGP_DIAG_NO_STAGE_TW
   return;   // DIAGNOSTIC BUILD ONLY (wrong results): tools/isa_mix.py counts what the stage twiddles cost
 #endif
-  if constexpr (PT && R == 16 && NS == 16) {
-    const C2<T>* __restrict__ row = tab + TwTab<T, H>::ENTRIES + kk * PT_PITCH;
-#pragma unroll
-    for (int r = 1; r < R; ++r) a[r] = (DIR < 0) ? cmul<T>(a[r], row[r - 1]) : cmulc<T>(a[r], row[r - 1]);
-    return;
-  }
   const int q1 = (2 * (H / (NS * R))) * kk;   // w = W_L^q1; w^r = W_L^{q1 r}, q1 r < L
   const C2<T> w = tw_at<T, H>(tab, q1);
   if constexpr (R > 16) {
@@ -564,7 +541,7 @@ __device__ __forceinline__ int lds_at(int pbase, int base, int x, bool base16) {
 // block's LDS image lives at lds_phys(base + e*STRIDE) (STRIDE = 1: line-contiguous image;
 // STRIDE = C: lines interleaved).  tab: LDS half table of W_L^q (L = 2H, see tw_at), so
 // W_H^e = W_L^{2e}.  All threads of the block must call it when T > 1 (block barriers).
-template <typename T, int H, int P, int DIR, int STRIDE, bool WAVE, int S, bool PT = false>
+template <typename T, int H, int P, int DIR, int STRIDE, bool WAVE, int S>
 __device__ __forceinline__ void fft_stage(C2<T> (&v)[P], C2<T>* lds, int base, int t,
                                           const C2<T>* __restrict__ tab) {
   using St = Stages<H, P>;
@@ -579,7 +556,7 @@ __device__ __forceinline__ void fft_stage(C2<T> (&v)[P], C2<T>* lds, int base, i
       if constexpr (NS > 1) {
         const int j = t + b * TT;
         // w = W_H^{kk*H/(NS*R)}: one LDS lookup, its powers in registers (stage_twiddle)
-        stage_twiddle<T, H, R, DIR, NS, PT>(a[b], j & (NS - 1), tab);
+        stage_twiddle<T, H, R, DIR, NS>(a[b], j & (NS - 1), tab);
       }
       dft<T, R, DIR>(a[b]);
     }
@@ -601,7 +578,7 @@ __device__ __forceinline__ void fft_stage(C2<T> (&v)[P], C2<T>* lds, int base, i
       const int prb = lds_phys(rb);
 #pragma unroll
       for (int k = 0; k < P; ++k) v[k] = lds[lds_at(prb, rb, TT * k * STRIDE, false)];
-      fft_stage<T, H, P, DIR, STRIDE, WAVE, S + 1, PT>(v, lds, base, t, tab);
+      fft_stage<T, H, P, DIR, STRIDE, WAVE, S + 1>(v, lds, base, t, tab);
     } else {
 #pragma unroll
       for (int b = 0; b < NB; ++b)
@@ -611,7 +588,7 @@ __device__ __forceinline__ void fft_stage(C2<T> (&v)[P], C2<T>* lds, int base, i
   }
 }
 
-template <typename T, int H, int P, int DIR, int STRIDE, bool WAVE = false, bool PT = false>
+template <typename T, int H, int P, int DIR, int STRIDE, bool WAVE = false>
 __device__ __forceinline__ void fft_line(C2<T> (&v)[P], C2<T>* lds, int base, int t,
                                          const C2<T>* __restrict__ tab) {
   // Opaque copy of t: every twiddle index below is recomputed and re-read from LDS, instead of
@@ -619,7 +596,7 @@ __device__ __forceinline__ void fft_line(C2<T> (&v)[P], C2<T>* lds, int base, in
   // two FFTs of a line costs ~50 VGPRs and halves occupancy).
   int tt = t;
   asm volatile("" : "+v"(tt));
-  fft_stage<T, H, P, DIR, STRIDE, WAVE, 0, PT>(v, lds, base, tt, tab);
+  fft_stage<T, H, P, DIR, STRIDE, WAVE, 0>(v, lds, base, tt, tab);
 }
 
 // ---- two independent transforms of one thread group, software-pipelined over ONE exchange
@@ -629,7 +606,7 @@ __device__ __forceinline__ void fft_line(C2<T> (&v)[P], C2<T>* lds, int base, in
 // fft_line (bitwise identical results).
 
 // stage-S butterflies of the P values in v -> a, in exchange-write order a[b*R + r]
-template <typename T, int H, int P, int DIR, int S, bool PT = false>
+template <typename T, int H, int P, int DIR, int S>
 __device__ __forceinline__ void fft_bfly(const C2<T> (&v)[P], C2<T> (&a)[P], int t,
                                          const C2<T>* __restrict__ tab) {
   using St = Stages<H, P>;
@@ -640,7 +617,7 @@ __device__ __forceinline__ void fft_bfly(const C2<T> (&v)[P], C2<T> (&a)[P], int
     for (int r = 0; r < R; ++r) a[b * R + r] = v[b + r * NB];
     if constexpr (NS > 1) {
       const int j = t + b * TT;
-      stage_twiddle<T, H, R, DIR, NS, PT>(&a[b * R], j & (NS - 1), tab);
+      stage_twiddle<T, H, R, DIR, NS>(&a[b * R], j & (NS - 1), tab);
     }
     dft<T, R, DIR>(&a[b * R]);
   }
@@ -678,20 +655,20 @@ __device__ __forceinline__ void fft_final(const C2<T> (&a)[P], C2<T> (&v)[P]) {
     for (int r = 0; r < R; ++r) v[b + r * NB] = a[b * R + r];
 }
 
-template <typename T, int H, int P, int DIR, int STRIDE, bool WAVE, int S, bool PT = false>
+template <typename T, int H, int P, int DIR, int STRIDE, bool WAVE, int S>
 __device__ __forceinline__ void fft_stage2(C2<T> (&va)[P], C2<T> (&vb)[P], C2<T> (&a)[P], C2<T>* lds, int base, int t,
                                            const C2<T>* __restrict__ tab) {
   // entry: a = stage-S butterflies of va (already computed); vb holds stage-S inputs
   constexpr int NST = Stages<H, P>::count();
   if constexpr (S + 1 < NST) {
     fft_xchg<T, H, P, STRIDE, WAVE, S>(a, va, lds, base, t);       // va: stage S+1 inputs in flight
-    fft_bfly<T, H, P, DIR, S, PT>(vb, a, t, tab);                   // ... while vb's butterflies run
+    fft_bfly<T, H, P, DIR, S>(vb, a, t, tab);                       // ... while vb's butterflies run
     fft_xchg<T, H, P, STRIDE, WAVE, S>(a, vb, lds, base, t);
-    fft_bfly<T, H, P, DIR, S + 1, PT>(va, a, t, tab);               // ... while vb's reads land
-    fft_stage2<T, H, P, DIR, STRIDE, WAVE, S + 1, PT>(va, vb, a, lds, base, t, tab);
+    fft_bfly<T, H, P, DIR, S + 1>(va, a, t, tab);                   // ... while vb's reads land
+    fft_stage2<T, H, P, DIR, STRIDE, WAVE, S + 1>(va, vb, a, lds, base, t, tab);
   } else {
     fft_final<T, H, P, S>(a, va);
-    fft_bfly<T, H, P, DIR, S, PT>(vb, a, t, tab);
+    fft_bfly<T, H, P, DIR, S>(vb, a, t, tab);
     fft_final<T, H, P, S>(a, vb);
   }
 }
@@ -703,20 +680,19 @@ __device__ __forceinline__ void fft_stage2(C2<T> (&va)[P], C2<T> (&vb)[P], C2<T>
 #ifndef HGP_SEQ_MULTIWAVE
 #define HGP_SEQ_MULTIWAVE 0
 #endif
-template <typename T, int H, int P, int DIR, int STRIDE, bool WAVE = false, bool SEQ = (HGP_SEQ_MULTIWAVE && !WAVE),
-          bool PT = false>
+template <typename T, int H, int P, int DIR, int STRIDE, bool WAVE = false, bool SEQ = (HGP_SEQ_MULTIWAVE && !WAVE)>
 __device__ __forceinline__ void fft_line2(C2<T> (&va)[P], C2<T> (&vb)[P], C2<T>* lds, int base, int t,
                                           const C2<T>* __restrict__ tab) {
   if constexpr (SEQ) {
-    fft_line<T, H, P, DIR, STRIDE, WAVE, PT>(va, lds, base, t, tab);
-    fft_line<T, H, P, DIR, STRIDE, WAVE, PT>(vb, lds, base, t, tab);
+    fft_line<T, H, P, DIR, STRIDE, WAVE>(va, lds, base, t, tab);
+    fft_line<T, H, P, DIR, STRIDE, WAVE>(vb, lds, base, t, tab);
     return;
   }
   int tt = t;
   asm volatile("" : "+v"(tt));
   C2<T> a[P];
-  fft_bfly<T, H, P, DIR, 0, PT>(va, a, tt, tab);
-  fft_stage2<T, H, P, DIR, STRIDE, WAVE, 0, PT>(va, vb, a, lds, base, tt, tab);
+  fft_bfly<T, H, P, DIR, 0>(va, a, tt, tab);
+  fft_stage2<T, H, P, DIR, STRIDE, WAVE, 0>(va, vb, a, lds, base, tt, tab);
 }
 
 }  // namespace hgp

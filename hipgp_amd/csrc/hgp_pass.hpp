@@ -244,12 +244,6 @@ constexpr int CG_LOADS = 8;
 #ifndef HGP_P_CONV_1024
 #define HGP_P_CONV_1024 0
 #endif
-// the stage-1 power table on the C2 column conv (hgp_fft.hpp PT): 56 fewer packed VALU per line but
-// 8 more LDS reads per transform -- measured slower (column pass 0.151 -> 0.155 ms, bench 113.6 k ->
-// 109.8 k, profiles/r6za_conv_power_table_ab.txt): off
-#ifndef HGP_PT_CONV
-#define HGP_PT_CONV 0
-#endif
 #ifndef HGP_MINW_CONTIG_P8
 #define HGP_MINW_CONTIG_P8 6
 #endif
@@ -270,12 +264,9 @@ template <typename T, int H, int LAY> struct PassP {
 template <typename T, int H, int LAY> struct PassCfg {
   static constexpr int P = PassP<T, H, LAY>::v;
   static constexpr int TT = H / P;
-  // the stage-1 power table (hgp_fft.hpp PT) on the fp32 1024-point contiguous lines (the C2 column
-  // conv): 2.3 KB more LDS per block, still two 8-line blocks per CU
-  static constexpr bool PT = HGP_PT_CONV && std::is_same<T, float>::value && H == 1024 && LAY == LAY_CONTIG && P == 16;
   // LDS: exchange image of C lines (H complex each, 1 pad slot per 16) + twiddle half table
   static constexpr int ex_elems(int c) { return c * H + ((c * H) >> 4); }
-  static constexpr int TW_BYTES = TwTab<T, H>::BYTES + (PT ? PT_ENTRIES * (int)sizeof(C2<T>) : 0);
+  static constexpr int TW_BYTES = TwTab<T, H>::BYTES;
   static constexpr int lds_bytes_for(int c) { return ex_elems(c) * (int)sizeof(C2<T>) + TW_BYTES; }
   static constexpr int c_strided() {
     int c = TT >= 16 ? HGP_CMAX_STRIDED : 64;
@@ -394,7 +385,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
   C2<T>* lds = reinterpret_cast<C2<T>*>(smem_raw);
   C2<T>* tab = lds + Cfg::EX_ELEMS;
   const C2<T>* __restrict__ twg = reinterpret_cast<const C2<T>*>(d.tw);
-  stage_tw<T, H, Cfg::PT>(tab, twg, threadIdx.x, Cfg::THREADS);
+  stage_tw<T, H>(tab, twg, threadIdx.x, Cfg::THREADS);
 
   const int tid = threadIdx.x;
   int l, t, lbase;
@@ -691,7 +682,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
 
   if constexpr (MODE == PASS_FWD) {
     // both halves' transforms interleaved over one exchange image (hgp_fft.hpp fft_line2)
-    fft_line2<T, H, P, -1, LSTRIDE, Cfg::WAVE, (HGP_SEQ_PASS == 2 || ((HGP_SEQ_PASS || HGP_SEQ_MULTIWAVE || (HGP_SEQ_PASS_2048 && TT == 128)) && !Cfg::WAVE)), Cfg::PT>(va, vb, lds, lbase, t, tab);
+    fft_line2<T, H, P, -1, LSTRIDE, Cfg::WAVE, (HGP_SEQ_PASS == 2 || ((HGP_SEQ_PASS || HGP_SEQ_MULTIWAVE || (HGP_SEQ_PASS_2048 && TT == 128)) && !Cfg::WAVE))>(va, vb, lds, lbase, t, tab);
     auto fwd_half = [&](auto half_c, C2<T>(&v)[P]) {
       constexpr int half = decltype(half_c)::value;
       if constexpr (HERM_OUT) {
@@ -726,7 +717,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
     // va ends as the even half's inverse (ye), vb as the odd half's (yo); the two halves'
     // transforms run interleaved over one exchange image (hgp_fft.hpp fft_line2)
     if constexpr (MODE == PASS_CONV) {
-      fft_line2<T, H, P, -1, LSTRIDE, Cfg::WAVE, (HGP_SEQ_PASS == 2 || ((HGP_SEQ_PASS || HGP_SEQ_MULTIWAVE || (HGP_SEQ_PASS_2048 && TT == 128)) && !Cfg::WAVE)), Cfg::PT>(va, vb, lds, lbase, t, tab);
+      fft_line2<T, H, P, -1, LSTRIDE, Cfg::WAVE, (HGP_SEQ_PASS == 2 || ((HGP_SEQ_PASS || HGP_SEQ_MULTIWAVE || (HGP_SEQ_PASS_2048 && TT == 128)) && !Cfg::WAVE))>(va, vb, lds, lbase, t, tab);
       // the packed DC + i Nyquist line (wave-uniform: one line per wave where the host packs):
       // z = a + i b with a, b the two real columns, each with its own real spectrum S0 / S1:
       // A = (Z + conj Z(-f)) / 2, B = (Z - conj Z(-f)) / 2i (herm_split through this line's LDS
@@ -796,7 +787,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
         }
       }
     } else if constexpr (MODE == PASS_CONVC) {
-      fft_line2<T, H, P, -1, LSTRIDE, Cfg::WAVE, (HGP_SEQ_PASS == 2 || ((HGP_SEQ_PASS || HGP_SEQ_MULTIWAVE || (HGP_SEQ_PASS_2048 && TT == 128)) && !Cfg::WAVE)), Cfg::PT>(va, vb, lds, lbase, t, tab);
+      fft_line2<T, H, P, -1, LSTRIDE, Cfg::WAVE, (HGP_SEQ_PASS == 2 || ((HGP_SEQ_PASS || HGP_SEQ_MULTIWAVE || (HGP_SEQ_PASS_2048 && TT == 128)) && !Cfg::WAVE))>(va, vb, lds, lbase, t, tab);
       // complex spectrum at (i, r, kperm): block-uniform base + 32-bit lane offset
       const C2<T>* sbase = reinterpret_cast<const C2<T>*>(d.spec) +
                            (GRP ? (int64_t)i0 * d.spec_r : (int64_t)i0 * d.spec_i + (int64_t)r * d.spec_r);
@@ -821,7 +812,7 @@ __global__ __launch_bounds__((PassCfg<T, H, LAY>::THREADS), (PassCfg<T, H, LAY>:
         }
       }
     }
-    fft_line2<T, H, P, +1, LSTRIDE, Cfg::WAVE, (HGP_SEQ_PASS == 2 || ((HGP_SEQ_PASS || HGP_SEQ_MULTIWAVE || (HGP_SEQ_PASS_2048 && TT == 128)) && !Cfg::WAVE)), Cfg::PT>(va, vb, lds, lbase, t, tab);
+    fft_line2<T, H, P, +1, LSTRIDE, Cfg::WAVE, (HGP_SEQ_PASS == 2 || ((HGP_SEQ_PASS || HGP_SEQ_MULTIWAVE || (HGP_SEQ_PASS_2048 && TT == 128)) && !Cfg::WAVE))>(va, vb, lds, lbase, t, tab);
     // combine in registers: y[p] = ye + conj(W_L^p) yo, y[p+H] = ye - conj(W_L^p) yo; crop.
     const int out_len = d.out.len;
     const T* dot_re = nullptr; const T* dot_im = nullptr;
